@@ -1,0 +1,125 @@
+"""ctypes binding of libavse.so (include/avse.h).
+
+`import torch` must happen before libavse.so is loaded: both link libamdhip64.so.7, so loading
+torch first makes libavse share torch's HIP runtime (one set of streams / allocations).
+
+There is no fallback: if libavse.so is missing or fails to load, every entry point raises.
+"""
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libavse.so")
+HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "avse.h")
+
+AVSE_F32 = 0
+AVSE_BF16 = 1
+AVSE_PAD_REFLECT = 0
+AVSE_PAD_CONSTANT = 1
+AVSE_NUM_STAGES = 22
+STAGE_NAMES = ("video_prep", "audio_prep", "a_conv1", "a_conv2", "a_conv3", "a_conv4", "a_conv5",
+               "v_conv1", "v_conv2", "v_conv3", "v_conv4", "v_conv5", "v_conv6", "enc_dense", "dec_dense1",
+               "dec_dense2", "d_deconv1", "d_deconv2", "d_deconv3", "d_deconv4", "d_deconv5", "d_deconv6")
+
+_c_void_p = ctypes.c_void_p
+_i64 = ctypes.c_int64
+_int = ctypes.c_int
+_flt = ctypes.c_float
+
+# name -> (restype, argtypes); every function declared in include/avse.h
+SIGNATURES = {
+    "avse_abi_version": (_int, []),
+    "avse_last_error": (ctypes.c_char_p, []),
+    "avse_ctx_create": (_int, [_int, ctypes.POINTER(_c_void_p)]),
+    "avse_ctx_destroy": (None, [_c_void_p]),
+    "avse_ctx_reserve": (_int, [_c_void_p, _i64, _int]),
+    "avse_spectrogram": (_int, [_c_void_p, _c_void_p, _i64, _i64, _int, _int, _int, _int, _flt, _flt, _flt, _flt,
+                                _int, _int, _c_void_p, _c_void_p, _c_void_p]),
+    "avse_weights_blob_floats": (_i64, []),
+    "avse_weights_load": (_int, [_c_void_p, _c_void_p, _i64, _int, ctypes.POINTER(_c_void_p)]),
+    "avse_weights_destroy": (None, [_c_void_p]),
+    "avse_forward": (_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _c_void_p,
+                            _c_void_p]),
+    "avse_video_normalize": (_int, [_c_void_p, _c_void_p, _i64, _int, _int, _int, _c_void_p, _c_void_p, _c_void_p]),
+    "avse_mse": (_int, [_c_void_p, _c_void_p, _c_void_p, _i64, _c_void_p, _c_void_p]),
+    "avse_forward_profile": (_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64,
+                                    _c_void_p, _c_void_p, ctypes.POINTER(_flt)]),
+    "avse_debug_scratch": (_int, [_c_void_p, _i64, _int, ctypes.POINTER(_c_void_p), ctypes.POINTER(_i64)]),
+}
+
+
+class AvseError(RuntimeError):
+    """A libavse call returned a non-zero status."""
+
+
+_lock = threading.Lock()
+_lib = None
+
+
+def load():
+    """Load libavse.so (once) and declare every signature.  Raises if it is missing."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise AvseError(
+                    f"{LIB_PATH} is not built: run `make -C audio-visual-speech-enhancement_amd/csrc` "
+                    "(or __graft_entry__.build()); there is no CPU fallback")
+            lib = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = lib
+    return _lib
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = load().avse_last_error().decode(errors="replace")
+        raise AvseError(f"{what} failed (status {rc}): {msg}")
+
+
+class Context:
+    """One libavse context per device (avse_ctx_create)."""
+
+    def __init__(self, device_index):
+        self.device_index = device_index
+        self.handle = _c_void_p()
+        check(load().avse_ctx_create(device_index, ctypes.byref(self.handle)), "avse_ctx_create")
+
+    def reserve(self, max_clips, dtype):
+        check(load().avse_ctx_reserve(self.handle, int(max_clips), int(dtype)), "avse_ctx_reserve")
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value and _lib is not None:
+            _lib.avse_ctx_destroy(h)
+            self.handle = None
+
+
+_ctx = {}
+
+
+def context(device=None):
+    if not torch.cuda.is_available():
+        raise AvseError("libavse needs a ROCm GPU (torch.cuda.is_available() is False); there is no CPU fallback")
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    with _lock:
+        c = _ctx.get(idx)
+    if c is None:
+        c = Context(idx)
+        with _lock:
+            _ctx[idx] = c
+    return c
+
+
+def stream_handle(device=None):
+    return _c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def ptr(t):
+    return _c_void_p(t.data_ptr()) if t is not None else _c_void_p(None)

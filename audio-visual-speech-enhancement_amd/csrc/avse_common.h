@@ -1,0 +1,103 @@
+// Shared device/host helpers for libavse (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+typedef __bf16 bf16_t;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+namespace avse {
+
+void set_error(const std::string& msg);
+
+#define AVSE_HIP_CHECK(expr)                                                                   \
+    do {                                                                                       \
+        hipError_t _e = (expr);                                                                \
+        if (_e != hipSuccess) {                                                                \
+            ::avse::set_error(std::string(#expr " failed: ") + hipGetErrorString(_e));         \
+            return 2; /* AVSE_ERR_HIP */                                                       \
+        }                                                                                      \
+    } while (0)
+
+// ---- STFT / mel front end ---------------------------------------------------------------
+struct MelTable {
+    int n_mels = 0;
+    int n_bins = 0;
+    int max_width = 0;         // max non-zero bins per band
+    int* start = nullptr;      // device [n_mels]
+    int* width = nullptr;      // device [n_mels]
+    float* weight = nullptr;   // device [n_mels][max_width]
+};
+
+struct SpecArgs {
+    const float* sig;
+    int64_t n_utt;
+    int64_t n_samples;
+    int n_fft, hop, n_frames;
+    int n_mels;
+    float amin, top_db;
+    float db_floor;           // 20*log10(amin) evaluated in double (bins <= amin)
+    int pad_mode;
+    int spf, n_slices;        // frames_per_slice (0 = plain [n_mels][T] layout)
+    float* mel_db;
+    float* stft_ri;           // nullable
+    const float2* twiddle;    // [n_fft]  e^{-2 pi i k / n_fft}
+    const float* window;      // [n_fft]  periodic Hann
+    const int* mel_start;
+    const int* mel_width;
+    const float* mel_weight;
+    int mel_max_width;
+    unsigned int* umax;       // [n_utt] ordered-float max scratch (chunked mode)
+};
+
+int launch_spectrogram(const SpecArgs& a, hipStream_t s);
+
+// ---- implicit-GEMM convolution ----------------------------------------------------------
+constexpr int MAX_TAPS = 25;
+constexpr int MAX_PHASES = 4;
+
+struct ConvPhase {
+    int py, px;          // output phase offset (deconv); 0 for forward convs
+    int ntaps;
+    int kpad;            // ntaps * cin padded to the k-slab (multiple of 32)
+    long long w_off;     // element offset of this phase's packed weights [cout][kpad]
+    int tap_off;         // offset of this phase's (dy, dx) pairs in ConvArgs::taps
+};
+
+struct ConvArgs {
+    const void* in;      // T [N][Hi][Wi][Ci] (clip stride in_clip_stride)
+    void* out;           // T
+    const void* w;       // T packed
+    const float* scale;  // [Cout]  folded BN scale (or 1)
+    const float* shift;  // [Cout]  folded bias/BN shift
+    const int2* taps;    // device (dy, dx) per tap, all phases
+    int N;
+    int Hi, Wi, Ci;
+    long long in_clip_stride;
+    int Hq, Wq;          // per-phase conv output grid
+    int sy, sx;          // input step per grid step
+    int oys, oxs;        // output step per grid step (deconv stride)
+    int Ho, Wo, Co;      // output tensor (after pool)
+    long long out_clip_stride;
+    int out_pix_stride;
+    int out_c_off;
+    int pool;            // fused 2x2 max pool
+    int act;             // 1 = LeakyReLU(0.3)
+    int nphase;
+    ConvPhase ph[MAX_PHASES];
+};
+
+int launch_conv(const ConvArgs& a, int dtype, hipStream_t s);
+int launch_video_prep(const float* video, const float* mean, const float* stdv, void* out, int64_t N,
+                      int dtype, hipStream_t s);
+int launch_audio_prep(const float* audio, void* out, int64_t N, int dtype, hipStream_t s);
+int launch_out_conv(const void* in, const float* w64, float bias, float* out, int64_t npix, int dtype,
+                    hipStream_t s);
+int launch_video_normalize(float* video, int64_t S, int H, int W, int F, const float* mean,
+                           const float* stdv, hipStream_t s);
+int launch_mse(const float* a, const float* b, int64_t n, float* loss, float* partial, hipStream_t s);
+
+}  // namespace avse

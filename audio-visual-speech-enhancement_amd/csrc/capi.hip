@@ -1,0 +1,667 @@
+// libavse C-ABI (include/avse.h): contexts, librosa-equivalent tables, weight folding/packing and
+// the layer plan of /root/reference/network.py, executed as a sequence of HIP kernel launches on
+// the caller's stream.
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/avse.h"
+#include "avse_common.h"
+
+namespace avse {
+static thread_local std::string g_err;
+void set_error(const std::string& msg) { g_err = msg; }
+}  // namespace avse
+
+using namespace avse;
+
+namespace {
+
+int fail(int code, const std::string& msg) {
+    set_error(msg);
+    return code;
+}
+
+// ---------------------------------------------------------------------------------------------
+// librosa-equivalent host tables (double precision, rounded to float once)
+// ---------------------------------------------------------------------------------------------
+double hz_to_mel(double f) {  // Slaney (htk=False)
+    const double f_sp = 200.0 / 3, min_log_hz = 1000.0, min_log_mel = min_log_hz / f_sp;
+    const double logstep = std::log(6.4) / 27.0;
+    if (f >= min_log_hz) return min_log_mel + std::log(f / min_log_hz) / logstep;
+    return f / f_sp;
+}
+double mel_to_hz(double m) {
+    const double f_sp = 200.0 / 3, min_log_hz = 1000.0, min_log_mel = min_log_hz / f_sp;
+    const double logstep = std::log(6.4) / 27.0;
+    if (m >= min_log_mel) return min_log_hz * std::exp(logstep * (m - min_log_mel));
+    return f_sp * m;
+}
+
+// librosa.filters.mel(sr, n_fft, n_mels, fmin, fmax, htk=False, norm=1) -> [n_mels][n_bins] (double)
+std::vector<double> mel_filterbank(int sr, int n_fft, int n_mels, double fmin, double fmax) {
+    const int nb = 1 + n_fft / 2;
+    std::vector<double> w((size_t)n_mels * nb, 0.0);
+    std::vector<double> fftf(nb), melf(n_mels + 2);
+    for (int k = 0; k < nb; ++k) fftf[k] = (nb == 1) ? 0.0 : (double)k * ((double)sr / 2) / (double)(nb - 1);
+    const double lo = hz_to_mel(fmin), hi = hz_to_mel(fmax);
+    for (int i = 0; i < n_mels + 2; ++i) melf[i] = mel_to_hz(lo + (hi - lo) * (double)i / (double)(n_mels + 1));
+    for (int i = 0; i < n_mels; ++i) {
+        const double d0 = melf[i + 1] - melf[i], d1 = melf[i + 2] - melf[i + 1];
+        const double enorm = 2.0 / (melf[i + 2] - melf[i]);
+        for (int k = 0; k < nb; ++k) {
+            const double lower = -(melf[i] - fftf[k]) / d0;
+            const double upper = (melf[i + 2] - fftf[k]) / d1;
+            double v = std::fmin(lower, upper);
+            if (v < 0) v = 0;
+            w[(size_t)i * nb + k] = v * enorm;
+        }
+    }
+    return w;
+}
+
+struct SpecTables {
+    int sr = -1, n_fft = -1, n_mels = -1;
+    double fmin = 0, fmax = 0;
+    float2* twiddle = nullptr;
+    float* window = nullptr;
+    MelTable mel;
+};
+
+// ---------------------------------------------------------------------------------------------
+// network plan (network.py:17-175)
+// ---------------------------------------------------------------------------------------------
+enum Kind { CONV = 0, DECONV = 1, DENSE = 2 };
+
+struct LayerDef {
+    const char* name;
+    Kind kind;
+    int cin, cout, kh, kw, sh, sw;
+    int hin, win;   // input spatial dims (1,1 for dense)
+    bool bn, pool;
+    int bn_channels;  // BN width (dec_dense2: 128 after Reshape)
+};
+
+// audio 80x20x1, video 128x128x5 (data_processor.py:12, :47-55)
+const LayerDef kLayers[] = {
+    {"a_conv1", CONV, 1, 64, 5, 5, 2, 2, 80, 20, true, false, 64},      // network.py:89
+    {"a_conv2", CONV, 64, 64, 4, 4, 1, 1, 40, 10, true, false, 64},     // :93
+    {"a_conv3", CONV, 64, 128, 4, 4, 2, 2, 40, 10, true, false, 128},   // :97
+    {"a_conv4", CONV, 128, 128, 2, 2, 2, 1, 20, 5, true, false, 128},   // :101
+    {"a_conv5", CONV, 128, 128, 2, 2, 2, 1, 10, 5, true, false, 128},   // :105
+    {"v_conv1", CONV, 5, 128, 5, 5, 1, 1, 128, 128, true, true, 128},   // :139
+    {"v_conv2", CONV, 128, 128, 5, 5, 1, 1, 64, 64, true, true, 128},   // :145
+    {"v_conv3", CONV, 128, 256, 3, 3, 1, 1, 32, 32, true, true, 256},   // :151
+    {"v_conv4", CONV, 256, 256, 3, 3, 1, 1, 16, 16, true, true, 256},   // :157
+    {"v_conv5", CONV, 256, 512, 3, 3, 1, 1, 8, 8, true, true, 512},     // :163
+    {"v_conv6", CONV, 512, 512, 3, 3, 1, 1, 4, 4, true, true, 512},     // :169
+    {"enc_dense", DENSE, 5248, 1312, 1, 1, 1, 1, 1, 1, true, false, 1312},   // :56
+    {"dec_dense1", DENSE, 1312, 1312, 1, 1, 1, 1, 1, 1, true, false, 1312},  // :69
+    {"dec_dense2", DENSE, 1312, 3200, 1, 1, 1, 1, 1, 1, true, false, 128},   // :75-78
+    {"d_deconv1", DECONV, 128, 128, 2, 2, 2, 1, 5, 5, true, false, 128},     // :113
+    {"d_deconv2", DECONV, 128, 128, 2, 2, 2, 1, 10, 5, true, false, 128},    // :117
+    {"d_deconv3", DECONV, 128, 128, 4, 4, 2, 2, 20, 5, true, false, 128},    // :121
+    {"d_deconv4", DECONV, 128, 64, 4, 4, 1, 1, 40, 10, true, false, 64},     // :125
+    {"d_deconv5", DECONV, 64, 64, 5, 5, 2, 2, 40, 10, true, false, 64},      // :129
+    {"d_deconv6", DECONV, 64, 1, 1, 1, 1, 1, 80, 20, false, false, 0},       // :133
+};
+constexpr int kNumLayers = sizeof(kLayers) / sizeof(kLayers[0]);
+constexpr float kBnEps = 1e-3f;
+
+int same_out(int n, int s) { return (n + s - 1) / s; }
+int same_pad_before(int n, int k, int s) {
+    const int out = same_out(n, s);
+    int tot = (out - 1) * s + k - n;
+    if (tot < 0) tot = 0;
+    return tot / 2;
+}
+
+int64_t blob_floats() {
+    int64_t n = 0;
+    for (int i = 0; i < kNumLayers; ++i) {
+        const LayerDef& L = kLayers[i];
+        n += (int64_t)L.kh * L.kw * L.cin * L.cout + L.cout;
+        if (L.bn) n += 4 * (int64_t)L.bn_channels;
+    }
+    return n;
+}
+
+uint16_t f2bf(float f) {
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    if ((u & 0x7f800000u) == 0x7f800000u) return (uint16_t)((u >> 16) | ((u & 0xffff) ? 0x40 : 0));
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+}
+
+}  // namespace
+
+struct avse_ctx {
+    int device = 0;
+    SpecTables spec;
+    unsigned* umax = nullptr;
+    int64_t umax_cap = 0;
+    float* mse_partial = nullptr;
+    char* arena = nullptr;
+    size_t arena_bytes = 0;
+};
+
+struct GpuLayer {
+    LayerDef def;
+    int cin_pad = 0;
+    int hq = 0, wq = 0, ho = 0, wo = 0;
+    int nphase = 1;
+    ConvPhase ph[MAX_PHASES];
+    void* w = nullptr;
+    float* scale = nullptr;
+    float* shift = nullptr;
+    int2* taps = nullptr;
+};
+
+struct avse_weights {
+    int dtype = 0;
+    int device = 0;
+    GpuLayer layers[kNumLayers - 1];  // all but d_deconv6
+    float* d6_w = nullptr;
+    float d6_bias = 0.f;
+    std::vector<void*> allocs;
+    ~avse_weights() {
+        for (void* p : allocs) (void)hipFree(p);
+    }
+};
+
+namespace {
+
+template <typename T>
+int upload(avse_weights* W, const std::vector<T>& h, T** out) {
+    void* p = nullptr;
+    if (hipMalloc(&p, sizeof(T) * (h.empty() ? 1 : h.size())) != hipSuccess) return fail(AVSE_ERR_OOM, "hipMalloc failed (weights)");
+    W->allocs.push_back(p);
+    if (!h.empty() && hipMemcpy(p, h.data(), sizeof(T) * h.size(), hipMemcpyHostToDevice) != hipSuccess)
+        return fail(AVSE_ERR_HIP, "hipMemcpy failed (weights)");
+    *out = (T*)p;
+    return 0;
+}
+
+// per-clip activation sizes (elements) of the forward scratch, in launch order
+struct Arena {
+    size_t off[32];
+    size_t per_clip_bytes;
+};
+enum Buf { B_VIN, B_AIN, B_A1, B_A2, B_A3, B_A4, B_V1, B_V2, B_V3, B_V4, B_V5, B_CAT, B_E1, B_E2, B_E3,
+           B_D1, B_D2, B_D3, B_D4, B_D5, B_COUNT };
+const size_t kBufElems[B_COUNT] = {128 * 128 * 8, 80 * 20 * 8, 40 * 10 * 64, 40 * 10 * 64, 20 * 5 * 128,
+                                   10 * 5 * 128, 64 * 64 * 128, 32 * 32 * 128, 16 * 16 * 256, 8 * 8 * 256,
+                                   4 * 4 * 512, 5248, 1312, 1312, 3200, 10 * 5 * 128, 20 * 5 * 128,
+                                   40 * 10 * 128, 40 * 10 * 64, 80 * 20 * 64};
+
+size_t arena_bytes(int64_t clips, int dtype, size_t* offs) {
+    const size_t es = dtype == AVSE_BF16 ? 2 : 4;
+    size_t off = 0;
+    for (int b = 0; b < B_COUNT; ++b) {
+        if (offs) offs[b] = off;
+        off += (kBufElems[b] * es * (size_t)clips + 255) & ~(size_t)255;
+    }
+    return off;
+}
+
+int ensure_arena(avse_ctx* c, int64_t clips, int dtype) {
+    const size_t need = arena_bytes(clips, dtype, nullptr);
+    if (need <= c->arena_bytes) return 0;
+    if (c->arena) (void)hipFree(c->arena);
+    c->arena = nullptr;
+    c->arena_bytes = 0;
+    if (hipMalloc((void**)&c->arena, need) != hipSuccess) return fail(AVSE_ERR_OOM, "hipMalloc failed (forward scratch)");
+    c->arena_bytes = need;
+    return 0;
+}
+
+int ensure_spec_tables(avse_ctx* c, int sr, int n_fft, int n_mels, double fmin, double fmax) {
+    SpecTables& t = c->spec;
+    if (t.sr == sr && t.n_fft == n_fft && t.n_mels == n_mels && t.fmin == fmin && t.fmax == fmax) return 0;
+    (void)hipFree(t.twiddle); (void)hipFree(t.window); (void)hipFree(t.mel.start); (void)hipFree(t.mel.width); (void)hipFree(t.mel.weight);
+    t = SpecTables();
+    std::vector<float2> tw(n_fft);
+    std::vector<float> win(n_fft);
+    for (int k = 0; k < n_fft; ++k) {
+        const double ang = -2.0 * M_PI * (double)k / (double)n_fft;
+        tw[k] = make_float2((float)std::cos(ang), (float)std::sin(ang));
+        win[k] = (float)(0.5 - 0.5 * std::cos(2.0 * M_PI * (double)k / (double)n_fft));
+    }
+    const int nb = 1 + n_fft / 2;
+    std::vector<double> fb = mel_filterbank(sr, n_fft, n_mels, fmin, fmax);
+    std::vector<int> st(n_mels), wd(n_mels);
+    int maxw = 1;
+    for (int m = 0; m < n_mels; ++m) {
+        int lo = -1, hi = -1;
+        for (int k = 0; k < nb; ++k)
+            if (fb[(size_t)m * nb + k] > 0) { if (lo < 0) lo = k; hi = k; }
+        st[m] = lo < 0 ? 0 : lo;
+        wd[m] = lo < 0 ? 0 : hi - lo + 1;
+        if (wd[m] > maxw) maxw = wd[m];
+    }
+    std::vector<float> wt((size_t)n_mels * maxw, 0.f);
+    for (int m = 0; m < n_mels; ++m)
+        for (int j = 0; j < wd[m]; ++j) wt[(size_t)m * maxw + j] = (float)fb[(size_t)m * nb + st[m] + j];
+    AVSE_HIP_CHECK(hipMalloc(&t.twiddle, sizeof(float2) * n_fft));
+    AVSE_HIP_CHECK(hipMalloc(&t.window, sizeof(float) * n_fft));
+    AVSE_HIP_CHECK(hipMalloc(&t.mel.start, sizeof(int) * n_mels));
+    AVSE_HIP_CHECK(hipMalloc(&t.mel.width, sizeof(int) * n_mels));
+    AVSE_HIP_CHECK(hipMalloc(&t.mel.weight, sizeof(float) * wt.size()));
+    AVSE_HIP_CHECK(hipMemcpy(t.twiddle, tw.data(), sizeof(float2) * n_fft, hipMemcpyHostToDevice));
+    AVSE_HIP_CHECK(hipMemcpy(t.window, win.data(), sizeof(float) * n_fft, hipMemcpyHostToDevice));
+    AVSE_HIP_CHECK(hipMemcpy(t.mel.start, st.data(), sizeof(int) * n_mels, hipMemcpyHostToDevice));
+    AVSE_HIP_CHECK(hipMemcpy(t.mel.width, wd.data(), sizeof(int) * n_mels, hipMemcpyHostToDevice));
+    AVSE_HIP_CHECK(hipMemcpy(t.mel.weight, wt.data(), sizeof(float) * wt.size(), hipMemcpyHostToDevice));
+    t.sr = sr; t.n_fft = n_fft; t.n_mels = n_mels; t.fmin = fmin; t.fmax = fmax;
+    t.mel.n_mels = n_mels; t.mel.n_bins = nb; t.mel.max_width = maxw;
+    return 0;
+}
+
+// Build phase/tap tables + packed [Cout][Kpad] weights for one layer.
+int build_layer(avse_weights* W, const LayerDef& L, const float* kernel, const float* bias, const float* bn) {
+    GpuLayer& G = W->layers[&L - kLayers];
+    G.def = L;
+    const int CHUNK_ELEMS = 8;   // channel padding so a 16-B chunk never straddles a tap (bf16: 8)
+    G.cin_pad = (L.cin % CHUNK_ELEMS) ? ((L.cin + CHUNK_ELEMS - 1) / CHUNK_ELEMS) * CHUNK_ELEMS : L.cin;
+    const int Cp = G.cin_pad;
+    std::vector<int2> taps;
+    std::vector<float> packed;
+    std::vector<std::vector<std::pair<int, int>>> phase_taps;   // (ky, kx) per tap
+    if (L.kind == DENSE) {
+        G.hq = G.wq = G.ho = G.wo = 1;
+        G.nphase = 1;
+        phase_taps.push_back({{0, 0}});
+        taps.push_back(make_int2(0, 0));
+        G.ph[0] = ConvPhase{0, 0, 1, 0, 0, 0};
+    } else if (L.kind == CONV) {
+        const int pt = same_pad_before(L.hin, L.kh, L.sh), pl = same_pad_before(L.win, L.kw, L.sw);
+        G.hq = same_out(L.hin, L.sh);
+        G.wq = same_out(L.win, L.sw);
+        G.ho = L.pool ? G.hq / 2 : G.hq;
+        G.wo = L.pool ? G.wq / 2 : G.wq;
+        G.nphase = 1;
+        std::vector<std::pair<int, int>> pt_list;
+        for (int ky = 0; ky < L.kh; ++ky)
+            for (int kx = 0; kx < L.kw; ++kx) {
+                pt_list.push_back({ky, kx});
+                taps.push_back(make_int2(ky - pt, kx - pl));
+            }
+        phase_taps.push_back(pt_list);
+        G.ph[0] = ConvPhase{0, 0, (int)pt_list.size(), 0, 0, 0};
+    } else {  // DECONV: TF conv2d_transpose 'SAME' to in*s, crop at pad_before = max(k - s, 0) / 2
+        const int pt = std::max(L.kh - L.sh, 0) / 2, pl = std::max(L.kw - L.sw, 0) / 2;
+        G.hq = L.hin;
+        G.wq = L.win;
+        G.ho = L.hin * L.sh;
+        G.wo = L.win * L.sw;
+        G.nphase = L.sh * L.sw;
+        if (G.nphase > MAX_PHASES) return fail(AVSE_ERR_UNSUPPORTED, "deconv stride too large");
+        for (int py = 0; py < L.sh; ++py)
+            for (int px = 0; px < L.sw; ++px) {
+                std::vector<std::pair<int, int>> pt_list;
+                const int toff = (int)taps.size();
+                for (int ky = 0; ky < L.kh; ++ky) {
+                    const int ry = py + pt - ky;
+                    if (((ry % L.sh) + L.sh) % L.sh) continue;
+                    for (int kx = 0; kx < L.kw; ++kx) {
+                        const int rx = px + pl - kx;
+                        if (((rx % L.sw) + L.sw) % L.sw) continue;
+                        pt_list.push_back({ky, kx});
+                        taps.push_back(make_int2(ry / L.sh, rx / L.sw));
+                    }
+                }
+                const int p = py * L.sw + px;
+                G.ph[p] = ConvPhase{py, px, (int)pt_list.size(), 0, 0, toff};
+                phase_taps.push_back(pt_list);
+            }
+    }
+    // pack weights per phase: W[n][j*Cp + c]
+    long long woff = 0;
+    for (int p = 0; p < G.nphase; ++p) {
+        const auto& pl_ = phase_taps[p];
+        const int kpad = (((int)pl_.size() * Cp + 31) / 32) * 32;
+        G.ph[p].kpad = kpad;
+        G.ph[p].w_off = woff;
+        packed.resize((size_t)(woff + (long long)L.cout * kpad), 0.f);
+        for (int n = 0; n < L.cout; ++n)
+            for (size_t j = 0; j < pl_.size(); ++j) {
+                const int ky = pl_[j].first, kx = pl_[j].second;
+                for (int c = 0; c < L.cin; ++c) {
+                    float v;
+                    if (L.kind == DENSE) v = kernel[(size_t)c * L.cout + n];
+                    else if (L.kind == CONV) v = kernel[(((size_t)ky * L.kw + kx) * L.cin + c) * L.cout + n];
+                    else v = kernel[(((size_t)ky * L.kw + kx) * L.cout + n) * L.cin + c];
+                    packed[(size_t)woff + (size_t)n * kpad + j * Cp + c] = v;
+                }
+            }
+        woff += (long long)L.cout * kpad;
+    }
+    // fold bias + BN into scale/shift
+    std::vector<float> scale(L.cout), shift(L.cout);
+    for (int n = 0; n < L.cout; ++n) {
+        if (L.bn) {
+            const int c = n % L.bn_channels;
+            const float* g = bn;
+            const float* b = bn + L.bn_channels;
+            const float* mu = bn + 2 * L.bn_channels;
+            const float* var = bn + 3 * L.bn_channels;
+            const double s = (double)g[c] / std::sqrt((double)var[c] + (double)kBnEps);
+            scale[n] = (float)s;
+            shift[n] = (float)(((double)bias[n] - (double)mu[c]) * s + (double)b[c]);
+        } else {
+            scale[n] = 1.f;
+            shift[n] = bias[n];
+        }
+    }
+    int rc;
+    if (W->dtype == AVSE_BF16) {
+        std::vector<uint16_t> pb(packed.size());
+        for (size_t i = 0; i < packed.size(); ++i) pb[i] = f2bf(packed[i]);
+        uint16_t* d;
+        if ((rc = upload(W, pb, &d))) return rc;
+        G.w = d;
+    } else {
+        float* d;
+        if ((rc = upload(W, packed, &d))) return rc;
+        G.w = d;
+    }
+    if ((rc = upload(W, scale, &G.scale))) return rc;
+    if ((rc = upload(W, shift, &G.shift))) return rc;
+    if ((rc = upload(W, taps, &G.taps))) return rc;
+    return 0;
+}
+
+ConvArgs conv_args(const GpuLayer& G, const void* in, long long in_clip_stride, void* out, long long out_clip_stride,
+                   int out_pix_stride, int out_c_off, int64_t N) {
+    const LayerDef& L = G.def;
+    ConvArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.in = in;
+    a.out = out;
+    a.w = G.w;
+    a.scale = G.scale;
+    a.shift = G.shift;
+    a.taps = G.taps;
+    a.N = (int)N;
+    a.Hi = L.hin;
+    a.Wi = L.win;
+    a.Ci = (L.kind == DENSE) ? L.cin : G.cin_pad;
+    a.in_clip_stride = in_clip_stride;
+    a.Hq = G.hq;
+    a.Wq = G.wq;
+    a.sy = (L.kind == CONV) ? L.sh : 1;
+    a.sx = (L.kind == CONV) ? L.sw : 1;
+    a.oys = (L.kind == DECONV) ? L.sh : 1;
+    a.oxs = (L.kind == DECONV) ? L.sw : 1;
+    a.Ho = G.ho;
+    a.Wo = G.wo;
+    a.Co = L.cout;
+    a.out_clip_stride = out_clip_stride;
+    a.out_pix_stride = out_pix_stride;
+    a.out_c_off = out_c_off;
+    a.pool = L.pool ? 1 : 0;
+    a.act = 1;
+    a.nphase = G.nphase;
+    for (int p = 0; p < G.nphase; ++p) a.ph[p] = G.ph[p];
+    return a;
+}
+
+}  // namespace
+
+// =============================================================================================
+// C-ABI
+// =============================================================================================
+extern "C" {
+
+int avse_abi_version(void) { return AVSE_ABI_VERSION; }
+const char* avse_last_error(void) { return g_err.c_str(); }
+
+int avse_ctx_create(int device, avse_ctx** out) {
+    if (!out) return fail(AVSE_ERR_INVALID, "out is NULL");
+    int n = 0;
+    AVSE_HIP_CHECK(hipGetDeviceCount(&n));
+    if (device < 0 || device >= n) return fail(AVSE_ERR_INVALID, "bad device index");
+    AVSE_HIP_CHECK(hipSetDevice(device));
+    avse_ctx* c = new avse_ctx();
+    c->device = device;
+    if (hipMalloc((void**)&c->mse_partial, sizeof(float) * 256) != hipSuccess) {
+        delete c;
+        return fail(AVSE_ERR_OOM, "hipMalloc failed (ctx)");
+    }
+    *out = c;
+    return 0;
+}
+
+void avse_ctx_destroy(avse_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipFree(c->spec.twiddle); (void)hipFree(c->spec.window);
+    (void)hipFree(c->spec.mel.start); (void)hipFree(c->spec.mel.width); (void)hipFree(c->spec.mel.weight);
+    (void)hipFree(c->umax);
+    (void)hipFree(c->mse_partial);
+    (void)hipFree(c->arena);
+    delete c;
+}
+
+int avse_ctx_reserve(avse_ctx* c, int64_t max_clips, int dtype) {
+    if (!c || max_clips < 0 || (dtype != AVSE_F32 && dtype != AVSE_BF16)) return fail(AVSE_ERR_INVALID, "bad reserve args");
+    AVSE_HIP_CHECK(hipSetDevice(c->device));
+    return ensure_arena(c, max_clips, dtype);
+}
+
+int avse_spectrogram(avse_ctx* c, const float* sig, int64_t n_utt, int64_t n_samples, int sr, int n_fft, int hop,
+                     int n_mels, float fmin, float fmax, float amin, float top_db, int pad_mode, int frames_per_slice,
+                     float* mel_db, float* stft_ri, void* stream) {
+    if (!c || !sig || !mel_db) return fail(AVSE_ERR_INVALID, "NULL argument");
+    if (n_utt < 0 || n_samples <= 0 || sr <= 0 || hop <= 0 || n_fft < 2)
+        return fail(AVSE_ERR_INVALID, "bad spectrogram geometry");
+    if (n_fft > 2048) return fail(AVSE_ERR_UNSUPPORTED, "n_fft > 2048 not supported");
+    if (n_mels < 1 || n_mels > 80) return fail(AVSE_ERR_UNSUPPORTED, "n_mels must be in [1, 80]");
+    if (pad_mode != AVSE_PAD_REFLECT && pad_mode != AVSE_PAD_CONSTANT) return fail(AVSE_ERR_INVALID, "bad pad_mode");
+    if (pad_mode == AVSE_PAD_REFLECT && n_samples <= n_fft / 2)
+        return fail(AVSE_ERR_INVALID, "reflect padding needs n_samples > n_fft/2");
+    if (frames_per_slice < 0) return fail(AVSE_ERR_INVALID, "frames_per_slice < 0");
+    AVSE_HIP_CHECK(hipSetDevice(c->device));
+    int rc = ensure_spec_tables(c, sr, n_fft, n_mels, fmin, fmax);
+    if (rc) return rc;
+    if (n_utt > c->umax_cap) {
+        (void)hipFree(c->umax);
+        c->umax = nullptr;
+        AVSE_HIP_CHECK(hipMalloc((void**)&c->umax, sizeof(unsigned) * n_utt));
+        c->umax_cap = n_utt;
+    }
+    SpecArgs a;
+    a.sig = sig;
+    a.n_utt = n_utt;
+    a.n_samples = n_samples;
+    a.n_fft = n_fft;
+    a.hop = hop;
+    a.n_frames = (int)(1 + (n_samples + 2 * (n_fft / 2) - n_fft) / hop);   // centred frames (librosa.stft)
+    a.n_mels = n_mels;
+    a.amin = amin;
+    a.db_floor = (float)(20.0 * std::log10((double)amin));   // exact value for clamped bins
+    a.top_db = top_db;
+    a.pad_mode = pad_mode;
+    a.spf = frames_per_slice;
+    a.n_slices = frames_per_slice > 0 ? a.n_frames / frames_per_slice : 0;
+    a.mel_db = mel_db;
+    a.stft_ri = stft_ri;
+    a.twiddle = c->spec.twiddle;
+    a.window = c->spec.window;
+    a.mel_start = c->spec.mel.start;
+    a.mel_width = c->spec.mel.width;
+    a.mel_weight = c->spec.mel.weight;
+    a.mel_max_width = c->spec.mel.max_width;
+    a.umax = c->umax;
+    return launch_spectrogram(a, (hipStream_t)stream);
+}
+
+int64_t avse_weights_blob_floats(void) { return blob_floats(); }
+
+int avse_weights_load(avse_ctx* c, const float* blob, int64_t n_floats, int dtype, avse_weights** out) {
+    if (!c || !blob || !out) return fail(AVSE_ERR_INVALID, "NULL argument");
+    if (dtype != AVSE_F32 && dtype != AVSE_BF16) return fail(AVSE_ERR_INVALID, "bad compute dtype");
+    if (n_floats != blob_floats())
+        return fail(AVSE_ERR_INVALID, "weight blob has " + std::to_string(n_floats) + " floats, expected " +
+                                          std::to_string(blob_floats()));
+    AVSE_HIP_CHECK(hipSetDevice(c->device));
+    avse_weights* W = new avse_weights();
+    W->dtype = dtype;
+    W->device = c->device;
+    const float* p = blob;
+    for (int i = 0; i < kNumLayers; ++i) {
+        const LayerDef& L = kLayers[i];
+        const float* kernel = p;
+        p += (size_t)L.kh * L.kw * L.cin * L.cout;
+        const float* bias = p;
+        p += L.cout;
+        const float* bn = nullptr;
+        if (L.bn) {
+            bn = p;
+            p += 4 * (size_t)L.bn_channels;
+        }
+        if (i == kNumLayers - 1) {  // d_deconv6: 1x1, 64 -> 1
+            std::vector<float> w64(kernel, kernel + 64);
+            int rc = upload(W, w64, &W->d6_w);
+            if (rc) { delete W; return rc; }
+            W->d6_bias = bias[0];
+            continue;
+        }
+        int rc = build_layer(W, L, kernel, bias, bn);
+        if (rc) { delete W; return rc; }
+    }
+    *out = W;
+    return 0;
+}
+
+void avse_weights_destroy(avse_weights* w) {
+    if (!w) return;
+    (void)hipSetDevice(w->device);
+    delete w;
+}
+
+}  // extern "C"
+
+namespace {
+// Stage order of avse_forward_profile (include/avse.h AVSE_NUM_STAGES).
+int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const float* video, const float* vmean,
+                 const float* vstd, int64_t N, float* out, hipStream_t s, hipEvent_t* ev) {
+    if (!c || !W || !audio || !video || !out) return fail(AVSE_ERR_INVALID, "NULL argument");
+    if ((vmean == nullptr) != (vstd == nullptr)) return fail(AVSE_ERR_INVALID, "vnorm_mean and vnorm_std must both be set or both NULL");
+    if (N < 0 || N > (int64_t)(1 << 30) / (128 * 128)) return fail(AVSE_ERR_INVALID, "bad N");
+    if (N == 0) return 0;
+    if (W->device != c->device) return fail(AVSE_ERR_INVALID, "weights and context are on different devices");
+    AVSE_HIP_CHECK(hipSetDevice(c->device));
+    int rc = ensure_arena(c, N, W->dtype);
+    if (rc) return rc;
+    const int dt = W->dtype;
+    size_t off[B_COUNT];
+    arena_bytes(N, dt, off);
+    auto buf = [&](int b) { return (void*)(c->arena + off[b]); };
+    auto L = [&](int i) -> const GpuLayer& { return W->layers[i]; };
+    int stage = 0;
+    auto mark = [&]() -> int {
+        if (ev) AVSE_HIP_CHECK(hipEventRecord(ev[stage], s));
+        ++stage;
+        return 0;
+    };
+    if ((rc = mark())) return rc;
+    if ((rc = launch_video_prep(video, vmean, vstd, buf(B_VIN), N, dt, s)) || (rc = mark())) return rc;
+    if ((rc = launch_audio_prep(audio, buf(B_AIN), N, dt, s)) || (rc = mark())) return rc;
+    // audio encoder (network.py:88-109)
+    const int a_in[5] = {B_AIN, B_A1, B_A2, B_A3, B_A4};
+    for (int i = 0; i < 5; ++i) {
+        const GpuLayer& G = L(i);
+        const long long in_cs = (long long)G.def.hin * G.def.win * (i == 0 ? G.cin_pad : G.def.cin);
+        ConvArgs a = (i < 4) ? conv_args(G, buf(a_in[i]), in_cs, buf(a_in[i + 1]), (long long)G.ho * G.wo * G.def.cout, G.def.cout, 0, N)
+                             : conv_args(G, buf(a_in[i]), in_cs, buf(B_CAT), 5248, G.def.cout, 0, N);   // Flatten -> concat[0:3200]
+        if ((rc = launch_conv(a, dt, s)) || (rc = mark())) return rc;
+    }
+    // video encoder (network.py:138-175)
+    const int v_in[6] = {B_VIN, B_V1, B_V2, B_V3, B_V4, B_V5};
+    for (int i = 0; i < 6; ++i) {
+        const GpuLayer& G = L(5 + i);
+        const long long in_cs = (long long)G.def.hin * G.def.win * (i == 0 ? G.cin_pad : G.def.cin);
+        ConvArgs a = (i < 5) ? conv_args(G, buf(v_in[i]), in_cs, buf(v_in[i + 1]), (long long)G.ho * G.wo * G.def.cout, G.def.cout, 0, N)
+                             : conv_args(G, buf(v_in[i]), in_cs, buf(B_CAT), 5248, G.def.cout, 3200, N);  // concat[3200:5248]
+        if ((rc = launch_conv(a, dt, s)) || (rc = mark())) return rc;
+    }
+    // fusion + decoder dense (network.py:53-58, :66-78)
+    {
+        ConvArgs a = conv_args(L(11), buf(B_CAT), 5248, buf(B_E1), 1312, 1312, 0, N);
+        if ((rc = launch_conv(a, dt, s)) || (rc = mark())) return rc;
+        a = conv_args(L(12), buf(B_E1), 1312, buf(B_E2), 1312, 1312, 0, N);
+        if ((rc = launch_conv(a, dt, s)) || (rc = mark())) return rc;
+        a = conv_args(L(13), buf(B_E2), 1312, buf(B_E3), 3200, 3200, 0, N);
+        if ((rc = launch_conv(a, dt, s)) || (rc = mark())) return rc;
+    }
+    // audio decoder (network.py:112-135)
+    const int d_in[6] = {B_E3, B_D1, B_D2, B_D3, B_D4, B_D5};
+    for (int i = 0; i < 5; ++i) {
+        const GpuLayer& G = L(14 + i);
+        const long long in_cs = (long long)G.def.hin * G.def.win * G.def.cin;
+        ConvArgs a = conv_args(G, buf(d_in[i]), in_cs, buf(d_in[i + 1]), (long long)G.ho * G.wo * G.def.cout, G.def.cout, 0, N);
+        if ((rc = launch_conv(a, dt, s)) || (rc = mark())) return rc;
+    }
+    if ((rc = launch_out_conv(buf(B_D5), W->d6_w, W->d6_bias, out, N * 80 * 20, dt, s)) || (rc = mark())) return rc;
+    return 0;
+}
+}  // namespace
+
+extern "C" {
+
+int avse_forward(avse_ctx* c, const avse_weights* W, const float* audio, const float* video, const float* vmean,
+                 const float* vstd, int64_t N, float* out, void* stream) {
+    return forward_impl(c, W, audio, video, vmean, vstd, N, out, (hipStream_t)stream, nullptr);
+}
+
+int avse_forward_profile(avse_ctx* c, const avse_weights* W, const float* audio, const float* video,
+                         const float* vmean, const float* vstd, int64_t N, float* out, void* stream, float* host_ms) {
+    if (!host_ms) return fail(AVSE_ERR_INVALID, "host_ms is NULL");
+    if (c) AVSE_HIP_CHECK(hipSetDevice(c->device));
+    hipEvent_t ev[AVSE_NUM_STAGES + 1];
+    for (int i = 0; i <= AVSE_NUM_STAGES; ++i) AVSE_HIP_CHECK(hipEventCreate(&ev[i]));
+    int rc = forward_impl(c, W, audio, video, vmean, vstd, N, out, (hipStream_t)stream, ev);
+    if (!rc) {
+        AVSE_HIP_CHECK(hipEventSynchronize(ev[AVSE_NUM_STAGES]));
+        for (int i = 0; i < AVSE_NUM_STAGES; ++i) {
+            float ms = 0.f;
+            AVSE_HIP_CHECK(hipEventElapsedTime(&ms, ev[i], ev[i + 1]));
+            host_ms[i] = ms;
+        }
+    }
+    for (int i = 0; i <= AVSE_NUM_STAGES; ++i) (void)hipEventDestroy(ev[i]);
+    return rc;
+}
+
+int avse_video_normalize(avse_ctx* c, float* video, int64_t S, int H, int W, int F, const float* mean,
+                         const float* stdv, void* stream) {
+    if (!c || !video || !mean || !stdv) return fail(AVSE_ERR_INVALID, "NULL argument");
+    if (S < 0 || H <= 0 || W <= 0 || F <= 0) return fail(AVSE_ERR_INVALID, "bad video shape");
+    if (S == 0) return 0;
+    AVSE_HIP_CHECK(hipSetDevice(c->device));
+    return launch_video_normalize(video, S, H, W, F, mean, stdv, (hipStream_t)stream);
+}
+
+int avse_mse(avse_ctx* c, const float* pred, const float* target, int64_t n, float* loss, void* stream) {
+    if (!c || !pred || !target || !loss) return fail(AVSE_ERR_INVALID, "NULL argument");
+    if (n <= 0) return fail(AVSE_ERR_INVALID, "n must be positive");
+    AVSE_HIP_CHECK(hipSetDevice(c->device));
+    return launch_mse(pred, target, n, loss, c->mse_partial, (hipStream_t)stream);
+}
+
+int avse_debug_scratch(avse_ctx* c, int64_t N, int dtype, void** base, int64_t* offsets) {
+    if (!c || !base || !offsets || N <= 0) return fail(AVSE_ERR_INVALID, "bad debug_scratch args");
+    size_t off[B_COUNT];
+    const size_t need = arena_bytes(N, dtype, off);
+    if (!c->arena || need > c->arena_bytes) return fail(AVSE_ERR_INVALID, "no forward scratch of that size yet");
+    *base = c->arena;
+    for (int b = 0; b < B_COUNT; ++b) offsets[b] = (int64_t)off[b];
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,388 @@
+// K2-K5: NHWC implicit-GEMM convolution on MFMA for gfx950, with the Keras layer tail fused.
+//
+// One kernel covers every layer of /root/reference/network.py's graph:
+//   Convolution2D(padding='same')        (network.py:89-105, :139-169)  forward taps, stride (sy, sx)
+//   Deconvolution2D(padding='same')      (network.py:113-133)            one launch, blockIdx.z = output
+//                                                                         phase (sub-pixel split), each
+//                                                                         phase a stride-1 gather conv
+//   Dense                                (network.py:56, :69, :75)       1 tap, Hi = Wi = 1, Ci = K
+// and fuses the epilogue: bias + BatchNormalization (folded to per-channel scale/shift on the
+// host), LeakyReLU(0.3), MaxPooling2D(2,2) (video convs; rows of a tile are ordered so the four
+// pixels of a pool window are the four accumulator rows one lane holds), Dropout = identity,
+// Flatten/concatenate (strided output addressing into the fused 5248-wide embedding).
+//
+// GEMM view: M = output pixels (N clips x Hq x Wq), N = Cout, K = taps x Ci.  Tile 128 x BN,
+// 256 threads = 4 wavefronts (2 x 2), each wave 64 x BN/2 built from 16x16 MFMA tiles.
+// The K loop walks 64-byte "slabs": 32 bf16 (one v_mfma_f32_16x16x32_bf16) or 16 fp32 (four
+// exact-fp32 v_mfma_f32_16x16x4_f32) per row, so the LDS geometry is identical for both dtypes.
+// A (im2col gathered on the fly, 16-byte chunks, zero padding = TF 'SAME') and B (packed weights
+// [Cout][Kpad]) are register-staged into a double-buffered, XOR-swizzled LDS tile (one barrier
+// per slab; the next slab's global loads are in flight during the current slab's MFMAs).
+#include "avse_common.h"
+
+namespace avse {
+namespace {
+
+constexpr int BM = 128;
+constexpr float LRELU = 0.3f;
+
+template <typename T> struct Vec16;
+template <> struct Vec16<bf16_t> { typedef i32x4 type; };
+template <> struct Vec16<float> { typedef i32x4 type; };
+
+__device__ __forceinline__ int swz(int row) { return ((row >> 3) & 1) * 3; }
+
+__device__ __forceinline__ float to_f(bf16_t v) { return (float)v; }
+__device__ __forceinline__ float to_f(float v) { return v; }
+template <typename T> __device__ __forceinline__ T from_f(float v);
+template <> __device__ __forceinline__ bf16_t from_f<bf16_t>(float v) { return (bf16_t)v; }
+template <> __device__ __forceinline__ float from_f<float>(float v) { return v; }
+
+struct RowInfo {
+    const char* base;   // clip base pointer (bytes)
+    int iy0, ix0;       // yq*sy, xq*sx
+    bool valid;
+};
+
+template <typename T, int BN>
+__global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
+    constexpr int CH = 16 / sizeof(T);          // elements per 16-byte chunk
+    constexpr int SLAB = 64 / sizeof(T);        // elements per 64-byte k-slab
+    constexpr int WN = BN / 2;                  // wave tile N
+    constexpr int NJ = WN / 16;                 // 16-wide N fragments per wave
+    constexpr int NI = 4;                       // 16-high M fragments per wave (64 rows)
+    constexpr int BCH = BN * 4 / 256;           // B chunks per thread
+
+    __shared__ __attribute__((aligned(16))) char lds[2 * (BM + BN) * 64];
+    // buffer b: A tile at lds + b*(BM+BN)*64, B tile right after it
+#define AS(b) (lds + (b) * (BM + BN) * 64)
+#define BS(b) (lds + (b) * (BM + BN) * 64 + BM * 64)
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wid = tid >> 6;
+    const int wm = wid >> 1, wn = wid & 1;
+    const ConvPhase ph = a.ph[blockIdx.z];
+    const int M = a.N * a.Hq * a.Wq;
+    const int m0 = blockIdx.x * BM;
+    const int n0 = blockIdx.y * BN;
+    const int nslab = ph.kpad / SLAB;
+    const int2* __restrict__ taps = a.taps + ph.tap_off;
+
+    // ---- per-thread A rows (2 chunks: rows r and r + 64, same chunk column g) ----
+    const int g = tid & 3;
+    RowInfo ri[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int row = (tid >> 2) + 64 * h;
+        const int m = m0 + row;
+        ri[h].valid = m < M;
+        const int mm = ri[h].valid ? m : 0;
+        int clip, yq, xq;
+        if (a.pool) {
+            const int p = mm >> 2, q = mm & 3;
+            const int pw = a.Wq >> 1, phh = a.Hq >> 1;
+            clip = p / (phh * pw);
+            const int r = p - clip * phh * pw;
+            yq = 2 * (r / pw) + (q >> 1);
+            xq = 2 * (r % pw) + (q & 1);
+        } else {
+            clip = mm / (a.Hq * a.Wq);
+            const int r = mm - clip * a.Hq * a.Wq;
+            yq = r / a.Wq;
+            xq = r % a.Wq;
+        }
+        ri[h].base = reinterpret_cast<const char*>(a.in) + (long long)clip * a.in_clip_stride * sizeof(T);
+        ri[h].iy0 = yq * a.sy;
+        ri[h].ix0 = xq * a.sx;
+    }
+    // chunk k position: tap j, channel c (incremental across slabs)
+    int kj = (g * CH) / a.Ci;
+    int kc = g * CH - kj * a.Ci;
+
+    const char* wbase = reinterpret_cast<const char*>(a.w) + ph.w_off * sizeof(T);
+
+    i32x4 ra[2], rb[BCH];
+    auto load_slab = [&](int s) {
+        // A
+        int2 t = (kj < ph.ntaps) ? taps[kj] : make_int2(0, 0);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            i32x4 v = {0, 0, 0, 0};
+            if (ri[h].valid && kj < ph.ntaps) {
+                const int iy = ri[h].iy0 + t.x, ix = ri[h].ix0 + t.y;
+                if (iy >= 0 && iy < a.Hi && ix >= 0 && ix < a.Wi)
+                    v = *reinterpret_cast<const i32x4*>(ri[h].base + ((long long)(iy * a.Wi + ix) * a.Ci + kc) * sizeof(T));
+            }
+            ra[h] = v;
+        }
+        // B
+#pragma unroll
+        for (int h = 0; h < BCH; ++h) {
+            const int c = tid + 256 * h;
+            const int row = c >> 2, gg = c & 3;
+            const int n = n0 + row;
+            i32x4 v = {0, 0, 0, 0};
+            if (n < a.Co)
+                v = *reinterpret_cast<const i32x4*>(wbase + ((long long)n * ph.kpad + s * SLAB + gg * CH) * sizeof(T));
+            rb[h] = v;
+        }
+        // advance the A chunk position by one slab
+        kc += SLAB;
+        while (kc >= a.Ci) { kc -= a.Ci; ++kj; }
+    };
+    auto store_slab = [&](int buf) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int row = (tid >> 2) + 64 * h;
+            *reinterpret_cast<i32x4*>(AS(buf) + row * 64 + ((g ^ swz(row)) << 4)) = ra[h];
+        }
+#pragma unroll
+        for (int h = 0; h < BCH; ++h) {
+            const int c = tid + 256 * h;
+            const int row = c >> 2, gg = c & 3;
+            *reinterpret_cast<i32x4*>(BS(buf) + row * 64 + ((gg ^ swz(row)) << 4)) = rb[h];
+        }
+    };
+
+    f32x4 acc[NI][NJ];
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+    load_slab(0);
+    store_slab(0);
+    __syncthreads();
+
+    const int fr = lane & 15, fg = lane >> 4;
+    for (int s = 0; s < nslab; ++s) {
+        const int buf = s & 1;
+        if (s + 1 < nslab) load_slab(s + 1);
+        i32x4 fa[NI], fb[NJ];
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int row = wm * 64 + 16 * i + fr;
+            fa[i] = *reinterpret_cast<const i32x4*>(AS(buf) + row * 64 + ((fg ^ swz(row)) << 4));
+        }
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int row = wn * WN + 16 * j + fr;
+            fb[j] = *reinterpret_cast<const i32x4*>(BS(buf) + row * 64 + ((fg ^ swz(row)) << 4));
+        }
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                if constexpr (sizeof(T) == 2) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                        __builtin_bit_cast(bf16x8, fa[i]), __builtin_bit_cast(bf16x8, fb[j]), acc[i][j], 0, 0, 0);
+                } else {
+                    const f32x4 av = __builtin_bit_cast(f32x4, fa[i]);
+                    const f32x4 bv = __builtin_bit_cast(f32x4, fb[j]);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], bv[e], acc[i][j], 0, 0, 0);
+                }
+            }
+        if (s + 1 < nslab) store_slab(buf ^ 1);
+        __syncthreads();
+    }
+
+#undef AS
+#undef BS
+    // ---- epilogue: scale/shift (bias + BN), [pool], LeakyReLU, strided NHWC store ----
+    T* out = reinterpret_cast<T*>(a.out);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        const int n = n0 + wn * WN + 16 * j + fr;
+        if (n >= a.Co) continue;
+        const float sc = a.scale[n], sh = a.shift[n];
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int mb = m0 + wm * 64 + 16 * i + 4 * fg;   // first of this lane's 4 rows
+            if (mb >= M) continue;
+            float v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] * sc + sh;
+            if (a.pool) {
+                float x = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
+                if (a.act) x = x >= 0.f ? x : LRELU * x;
+                const int p = mb >> 2;
+                const int pw = a.Wq >> 1, phh = a.Hq >> 1;
+                const int clip = p / (phh * pw);
+                const int r = p - clip * phh * pw;
+                const long long o = clip * a.out_clip_stride + (long long)r * a.out_pix_stride + a.out_c_off + n;
+                out[o] = from_f<T>(x);
+            } else {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int m = mb + r;
+                    if (m >= M) break;
+                    float x = v[r];
+                    if (a.act) x = x >= 0.f ? x : LRELU * x;
+                    const int clip = m / (a.Hq * a.Wq);
+                    const int rr = m - clip * a.Hq * a.Wq;
+                    const int oy = (rr / a.Wq) * a.oys + ph.py, ox = (rr % a.Wq) * a.oxs + ph.px;
+                    const long long o = clip * a.out_clip_stride + (long long)(oy * a.Wo + ox) * a.out_pix_stride + a.out_c_off + n;
+                    out[o] = from_f<T>(x);
+                }
+            }
+        }
+    }
+}
+
+// video [N][128][128][5] f32 -> (x - mean) / std -> T [N][128][128][8] (channels 5..7 zero)
+template <typename T>
+__global__ void k_video_prep(const float* __restrict__ v, const float* __restrict__ mean, const float* __restrict__ stdv,
+                             T* __restrict__ out, long long npix) {
+    for (long long p = blockIdx.x * (long long)blockDim.x + threadIdx.x; p < npix; p += (long long)gridDim.x * blockDim.x) {
+        const int hw = (int)(p % (128 * 128));
+        const float* src = v + p * 5;
+        float m = 0.f, s = 1.f;
+        const bool norm = mean != nullptr;
+        if (norm) { m = mean[hw]; s = stdv[hw]; }
+        T o[8];
+#pragma unroll
+        for (int c = 0; c < 5; ++c) {
+            float x = src[c];
+            if (norm) x = (x - m) / s;
+            o[c] = from_f<T>(x);
+        }
+#pragma unroll
+        for (int c = 5; c < 8; ++c) o[c] = from_f<T>(0.f);
+        T* dst = out + p * 8;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) dst[c] = o[c];
+    }
+}
+
+// audio [N][80][20] f32 -> T [N][80][20][8] (channel 0 = value, 1..7 zero)
+template <typename T>
+__global__ void k_audio_prep(const float* __restrict__ a, T* __restrict__ out, long long npix) {
+    for (long long p = blockIdx.x * (long long)blockDim.x + threadIdx.x; p < npix; p += (long long)gridDim.x * blockDim.x) {
+        T o[8];
+        o[0] = from_f<T>(a[p]);
+#pragma unroll
+        for (int c = 1; c < 8; ++c) o[c] = from_f<T>(0.f);
+        T* dst = out + p * 8;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) dst[c] = o[c];
+    }
+}
+
+// d_deconv6 (network.py:133): 1x1 Conv2DTranspose 64 -> 1 + bias, no BN / activation.
+template <typename T>
+__global__ void k_out_conv(const T* __restrict__ in, const float* __restrict__ w, float bias, float* __restrict__ out,
+                           long long npix) {
+    __shared__ float ws[64];
+    if (threadIdx.x < 64) ws[threadIdx.x] = w[threadIdx.x];
+    __syncthreads();
+    for (long long p = blockIdx.x * (long long)blockDim.x + threadIdx.x; p < npix; p += (long long)gridDim.x * blockDim.x) {
+        const T* src = in + p * 64;
+        float acc = 0.f;
+#pragma unroll
+        for (int c = 0; c < 64; ++c) acc = fmaf(to_f(src[c]), ws[c], acc);
+        out[p] = acc + bias;
+    }
+}
+
+__global__ void k_video_normalize(float* __restrict__ v, long long S, int H, int W, int F, const float* __restrict__ mean,
+                                  const float* __restrict__ stdv) {
+    const long long total = S * H * W * F;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+        const int hw = (int)((i / F) % ((long long)H * W));
+        v[i] = (v[i] - mean[hw]) / stdv[hw];
+    }
+}
+
+// deterministic two-pass mean((a-b)^2)
+__global__ void k_mse_partial(const float* __restrict__ a, const float* __restrict__ b, long long n, float* partial) {
+    __shared__ float red[4];
+    float s = 0.f;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+        const float d = a[i] - b[i];
+        s = fmaf(d, d, s);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) partial[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ void k_mse_final(const float* __restrict__ partial, int np, long long n, float* loss) {
+    __shared__ float red[4];
+    float s = 0.f;
+    for (int i = threadIdx.x; i < np; i += blockDim.x) s += partial[i];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) *loss = (float)(((double)red[0] + red[1] + red[2] + red[3]) / (double)n);
+}
+
+inline unsigned grid_for(long long n, int block) {
+    long long g = (n + block - 1) / block;
+    return (unsigned)(g < 1 ? 1 : (g > 8192 ? 8192 : g));
+}
+
+}  // namespace
+
+int launch_conv(const ConvArgs& a, int dtype, hipStream_t s) {
+    const int M = a.N * a.Hq * a.Wq;
+    const int BN = (a.Co <= 64) ? 64 : 128;
+    dim3 grid((M + BM - 1) / BM, (a.Co + BN - 1) / BN, a.nphase);
+    if (dtype == 1) {
+        if (BN == 64) hipLaunchKernelGGL((k_conv<bf16_t, 64>), grid, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((k_conv<bf16_t, 128>), grid, dim3(256), 0, s, a);
+    } else {
+        if (BN == 64) hipLaunchKernelGGL((k_conv<float, 64>), grid, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((k_conv<float, 128>), grid, dim3(256), 0, s, a);
+    }
+    AVSE_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int launch_video_prep(const float* video, const float* mean, const float* stdv, void* out, int64_t N, int dtype,
+                      hipStream_t s) {
+    const long long npix = (long long)N * 128 * 128;
+    if (dtype == 1) hipLaunchKernelGGL(k_video_prep<bf16_t>, dim3(grid_for(npix, 256)), dim3(256), 0, s, video, mean, stdv, (bf16_t*)out, npix);
+    else hipLaunchKernelGGL(k_video_prep<float>, dim3(grid_for(npix, 256)), dim3(256), 0, s, video, mean, stdv, (float*)out, npix);
+    AVSE_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int launch_audio_prep(const float* audio, void* out, int64_t N, int dtype, hipStream_t s) {
+    const long long npix = (long long)N * 80 * 20;
+    if (dtype == 1) hipLaunchKernelGGL(k_audio_prep<bf16_t>, dim3(grid_for(npix, 256)), dim3(256), 0, s, audio, (bf16_t*)out, npix);
+    else hipLaunchKernelGGL(k_audio_prep<float>, dim3(grid_for(npix, 256)), dim3(256), 0, s, audio, (float*)out, npix);
+    AVSE_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int launch_out_conv(const void* in, const float* w64, float bias, float* out, int64_t npix, int dtype, hipStream_t s) {
+    if (dtype == 1) hipLaunchKernelGGL(k_out_conv<bf16_t>, dim3(grid_for(npix, 256)), dim3(256), 0, s, (const bf16_t*)in, w64, bias, out, (long long)npix);
+    else hipLaunchKernelGGL(k_out_conv<float>, dim3(grid_for(npix, 256)), dim3(256), 0, s, (const float*)in, w64, bias, out, (long long)npix);
+    AVSE_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int launch_video_normalize(float* video, int64_t S, int H, int W, int F, const float* mean, const float* stdv,
+                           hipStream_t s) {
+    const long long total = (long long)S * H * W * F;
+    hipLaunchKernelGGL(k_video_normalize, dim3(grid_for(total, 256)), dim3(256), 0, s, video, (long long)S, H, W, F, mean, stdv);
+    AVSE_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int launch_mse(const float* a, const float* b, int64_t n, float* loss, float* partial, hipStream_t s) {
+    const int np = 256;
+    hipLaunchKernelGGL(k_mse_partial, dim3(np), dim3(256), 0, s, a, b, (long long)n, partial);
+    AVSE_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(k_mse_final, dim3(1), dim3(256), 0, s, partial, np, (long long)n, loss);
+    AVSE_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+}  // namespace avse

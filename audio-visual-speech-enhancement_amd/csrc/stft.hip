@@ -1,0 +1,318 @@
+// K1: fused STFT -> |X| -> Slaney mel -> dB (-> top_db clamp, -> slicing) for gfx950.
+//
+// Replaces librosa.core.stft / magphase / filters.mel / amplitude_to_db as called by
+// signal_to_spectrogram (/root/reference/data_processor.py:77-96) and the slicing of
+// preprocess_audio_signal (data_processor.py:49-57).
+//
+// n_fft = 640 (16 kHz / 25 fps, data_processor.py:44) is not a power of two.  The real
+// 640-point frame is packed as a 320-point complex sequence z[n] = x[2n] + i x[2n+1] and
+// transformed with a 16 x 20 Cooley-Tukey split, entirely within one wavefront:
+//   step 1: lane (frame f, n1 in [0,16)) does a 20-point DFT (4 x 5) over n2 of
+//           z[n1 + 16 n2] in registers, multiplies by W320^{n1 k2}, writes LDS
+//   step 2: lane (f, k2 in [0,20)) does a 16-point DFT (4 x 4) over n1 -> Z[k2 + 20 k1]
+//   step 3: lane (f, k) untangles X[k], X[320-k] from Z[k], Z[320-k]  -> |X| in LDS
+//   step 4: lane (f, mel band) sparse Slaney dot (<= max_width bins) -> dB
+// Each 64-lane block handles one chunk of up to 21 frames of one utterance, 3 frames per
+// pass (48 / 60 active lanes in steps 1 / 2).  When the chunk covers the whole utterance (the
+// 200-ms segment case: 3200 samples -> 21 frames) the top_db clamp (max over the WHOLE
+// [80, T] array, including the frame the slicing later drops) happens in-kernel; otherwise each
+// chunk publishes its max with an ordered-uint atomicMax and a clamp kernel follows.
+//
+// Other n_fft (e.g. 533 at 29.97 fps) use k_spec_dft: a direct DFT, one block per frame.
+#include "avse_common.h"
+
+namespace avse {
+
+namespace {
+
+constexpr int FPG = 3;          // frames per pass
+constexpr int CHUNK = 21;       // frames per block (7 passes)
+constexpr int ZS = 340;         // float2 slots per frame in LDS (20 rows x 17, padded)
+constexpr int MS = 324;         // floats per frame of |X| (321 used)
+
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+    return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+// multiply by -i
+__device__ __forceinline__ float2 cmni(float2 a) { return make_float2(a.y, -a.x); }
+
+__device__ __forceinline__ void dft4(float2& x0, float2& x1, float2& x2, float2& x3) {
+    float2 a = cadd(x0, x2), b = csub(x0, x2), c = cadd(x1, x3), d = cmni(csub(x1, x3));
+    x0 = cadd(a, c);
+    x2 = csub(a, c);
+    x1 = cadd(b, d);
+    x3 = csub(b, d);
+}
+
+// forward 5-point DFT (W = e^{-2 pi i / 5})
+__device__ __forceinline__ void dft5(float2& x0, float2& x1, float2& x2, float2& x3, float2& x4) {
+    const float c1 = 0.30901699437494745f, c2 = -0.8090169943749475f;
+    const float s1 = 0.9510565162951535f, s2 = 0.5877852522924731f;
+    float2 t1 = cadd(x1, x4), t2 = cadd(x2, x3), t3 = csub(x1, x4), t4 = csub(x2, x3);
+    float2 a1 = make_float2(x0.x + c1 * t1.x + c2 * t2.x, x0.y + c1 * t1.y + c2 * t2.y);
+    float2 a2 = make_float2(x0.x + c2 * t1.x + c1 * t2.x, x0.y + c2 * t1.y + c1 * t2.y);
+    // p = s1 t3 + s2 t4 ; q = s2 t3 - s1 t4 ; -i p, -i q
+    float2 p = make_float2(s1 * t3.x + s2 * t4.x, s1 * t3.y + s2 * t4.y);
+    float2 q = make_float2(s2 * t3.x - s1 * t4.x, s2 * t3.y - s1 * t4.y);
+    float2 y0 = cadd(x0, cadd(t1, t2));
+    float2 mp = cmni(p), mq = cmni(q);
+    x0 = y0;
+    x1 = cadd(a1, mp);
+    x4 = csub(a1, mp);
+    x2 = cadd(a2, mq);
+    x3 = csub(a2, mq);
+}
+
+__device__ __forceinline__ float sample_at(const float* __restrict__ s, long long L, long long i, int pad_mode) {
+    if (i < 0) {
+        if (pad_mode != 0) return 0.f;
+        i = -i;
+    } else if (i >= L) {
+        if (pad_mode != 0) return 0.f;
+        i = 2 * (L - 1) - i;
+    }
+    return s[i];
+}
+
+__device__ __forceinline__ float2 sample_pair(const float* __restrict__ s, long long L, long long i, int pad_mode) {
+    if (i >= 0 && i + 1 < L) return *reinterpret_cast<const float2*>(s + i);
+    return make_float2(sample_at(s, L, i, pad_mode), sample_at(s, L, i + 1, pad_mode));
+}
+
+__device__ __forceinline__ unsigned int f2ord(float f) {
+    unsigned int u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float ord2f(unsigned int u) {
+    return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
+}
+
+__device__ __forceinline__ long long out_index(int spf, int n_slices, int n_mels, int T, long long u, int m, int t) {
+    if (spf > 0) {
+        int sl = t / spf;
+        if (sl >= n_slices) return -1;
+        return ((u * n_slices + sl) * n_mels + m) * (long long)spf + (t - sl * spf);
+    }
+    return (u * n_mels + m) * (long long)T + t;
+}
+
+// One 64-lane block per (chunk of CHUNK frames, utterance).
+__global__ __launch_bounds__(64) void k_spec640(SpecArgs a, int n_chunks) {
+    __shared__ float2 zbuf[FPG * ZS];
+    __shared__ float mbuf[FPG * MS];
+    __shared__ float dbuf[80 * CHUNK];
+
+    const int lane = threadIdx.x;
+    const int chunk = blockIdx.x;
+    const long long u = blockIdx.y;
+    const int T = a.n_frames;
+    const int t0 = chunk * CHUNK;
+    const int nf = min(CHUNK, T - t0);
+    const long long L = a.n_samples;
+    const float* __restrict__ sig = a.sig + u * L;
+    const float2* __restrict__ tw = a.twiddle;   // W640^k
+    const float* __restrict__ win = a.window;
+    const int n_mels = a.n_mels;
+    float vmax = -INFINITY;
+
+    for (int g = 0; g < nf; g += FPG) {
+        const int ng = min(FPG, nf - g);
+        // ---- step 1: 20-point DFTs over n2, lane = (f, n1) ----
+        {
+            const int f = lane >> 4, n1 = lane & 15;
+            if (f < ng) {
+                const long long s0 = (long long)(t0 + g + f) * a.hop - 320;
+                float2 v[20];
+#pragma unroll
+                for (int n2 = 0; n2 < 20; ++n2) {
+                    const int n = n1 + 16 * n2;
+                    float2 x = sample_pair(sig, L, s0 + 2 * n, a.pad_mode);
+                    float2 w = *reinterpret_cast<const float2*>(win + 2 * n);
+                    v[n2] = make_float2(x.x * w.x, x.y * w.y);
+                }
+                // n2 = 5a + b ; k2 = c + 4d
+#pragma unroll
+                for (int b = 0; b < 5; ++b) dft4(v[b], v[5 + b], v[10 + b], v[15 + b]);
+                // v[5c + b] now holds T[b][c]; twiddle W20^{bc} = W640^{32 bc}
+#pragma unroll
+                for (int b = 1; b < 5; ++b)
+#pragma unroll
+                    for (int c = 1; c < 4; ++c) v[5 * c + b] = cmul(v[5 * c + b], tw[32 * b * c]);
+#pragma unroll
+                for (int c = 0; c < 4; ++c) dft5(v[5 * c], v[5 * c + 1], v[5 * c + 2], v[5 * c + 3], v[5 * c + 4]);
+                // v[5c + d] = Y[c + 4d]; twiddle W320^{n1 k2} = W640^{2 n1 k2}
+                float2* zf = zbuf + f * ZS;
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+#pragma unroll
+                    for (int d = 0; d < 5; ++d) {
+                        const int k2 = c + 4 * d;
+                        float2 y = v[5 * c + d];
+                        if (k2) y = cmul(y, tw[(2 * n1 * k2) % 640]);
+                        zf[k2 * 17 + n1] = y;
+                    }
+            }
+        }
+        __syncthreads();
+        // ---- step 2: 16-point DFTs over n1, lane = (f, k2) ----
+        {
+            const int f = lane / 20, k2 = lane - 20 * (lane / 20);
+            const bool act = f < ng;
+            float2 v[16];
+            float2* zf = zbuf + min(f, FPG - 1) * ZS;
+            if (act) {
+#pragma unroll
+                for (int n1 = 0; n1 < 16; ++n1) v[n1] = zf[k2 * 17 + n1];
+            }
+            __syncthreads();
+            if (act) {
+                // n1 = 4a + b ; k1 = c + 4d
+#pragma unroll
+                for (int b = 0; b < 4; ++b) dft4(v[b], v[4 + b], v[8 + b], v[12 + b]);
+#pragma unroll
+                for (int b = 1; b < 4; ++b)
+#pragma unroll
+                    for (int c = 1; c < 4; ++c) v[4 * c + b] = cmul(v[4 * c + b], tw[40 * b * c]);
+#pragma unroll
+                for (int c = 0; c < 4; ++c) dft4(v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3]);
+                // v[4c + d] = Z[k2 + 20 (c + 4d)]
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+#pragma unroll
+                    for (int d = 0; d < 4; ++d) zf[k2 + 20 * (c + 4 * d)] = v[4 * c + d];
+            }
+        }
+        __syncthreads();
+        // ---- step 3: real-FFT untangling + magnitude, item = (f, k), k in [0,160] ----
+        for (int it = lane; it < ng * 161; it += 64) {
+            const int f = it / 161, k = it - 161 * f;
+            const float2* zf = zbuf + f * ZS;
+            const float2 zk = zf[k];
+            const float2 zm = zf[k == 0 ? 0 : 320 - k];
+            // E = (Zk + conj Zm)/2 ; O = -i/2 (Zk - conj Zm)
+            const float2 E = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y));
+            const float2 O = make_float2(0.5f * (zk.y + zm.y), -0.5f * (zk.x - zm.x));
+            const float2 WO = cmul(tw[k], O);
+            const float2 X = cadd(E, WO);
+            const float2 Xm = make_float2(E.x - WO.x, -(E.y - WO.y));   // X[320 - k] = conj(E - W^k O)
+            float* mf = mbuf + f * MS;
+            mf[k] = sqrtf(X.x * X.x + X.y * X.y);
+            mf[320 - k] = sqrtf(Xm.x * Xm.x + Xm.y * Xm.y);
+            if (a.stft_ri) {
+                const long long t = t0 + g + f;
+                float2* o = reinterpret_cast<float2*>(a.stft_ri);
+                o[(u * 321 + k) * T + t] = X;
+                if (k != 160) o[(u * 321 + (320 - k)) * T + t] = Xm;
+            }
+        }
+        __syncthreads();
+        // ---- step 4: Slaney mel + dB, item = (f, m) ----
+        for (int it = lane; it < ng * n_mels; it += 64) {
+            const int f = it / n_mels, m = it - n_mels * f;
+            const float* mf = mbuf + f * MS + a.mel_start[m];
+            const float* wm = a.mel_weight + m * a.mel_max_width;
+            const int wdt = a.mel_width[m];
+            float acc = 0.f;
+            for (int j = 0; j < wdt; ++j) acc = fmaf(mf[j], wm[j], acc);
+            const float db = acc > a.amin ? 20.0f * log10f(acc) : a.db_floor;
+            vmax = fmaxf(vmax, db);
+            dbuf[m * CHUNK + g + f] = db;
+        }
+        __syncthreads();
+    }
+    // ---- block max + clamp / publish ----
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) vmax = fmaxf(vmax, __shfl_xor(vmax, o));
+    const bool single = (n_chunks == 1);
+    const float floor_db = (single && a.top_db >= 0.f) ? vmax - a.top_db : -INFINITY;
+    for (int it = lane; it < n_mels * nf; it += 64) {
+        const int m = it / nf, tl = it - nf * m;
+        const long long oi = out_index(a.spf, a.n_slices, n_mels, T, u, m, t0 + tl);
+        if (oi >= 0) a.mel_db[oi] = fmaxf(dbuf[m * CHUNK + tl], floor_db);
+    }
+    if (!single && lane == 0) atomicMax(a.umax + u, f2ord(vmax));
+}
+
+// Direct DFT fallback for n_fft != 640: one 256-thread block per (frame, utterance).
+__global__ __launch_bounds__(256) void k_spec_dft(SpecArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    const int N = a.n_fft, nb = N / 2 + 1;
+    float* xb = sm;            // [N]
+    float* mb = sm + N;        // [nb]
+    const int t = blockIdx.x;
+    const long long u = blockIdx.y;
+    const long long L = a.n_samples;
+    const float* sig = a.sig + u * L;
+    const long long s0 = (long long)t * a.hop - N / 2;
+    for (int n = threadIdx.x; n < N; n += 256) xb[n] = sample_at(sig, L, s0 + n, a.pad_mode) * a.window[n];
+    __syncthreads();
+    for (int k = threadIdx.x; k < nb; k += 256) {
+        float re = 0.f, im = 0.f;
+        int idx = 0;
+        for (int n = 0; n < N; ++n) {
+            const float2 w = a.twiddle[idx];
+            re = fmaf(xb[n], w.x, re);
+            im = fmaf(xb[n], w.y, im);
+            idx += k;
+            if (idx >= N) idx -= N;
+        }
+        mb[k] = sqrtf(re * re + im * im);
+        if (a.stft_ri) reinterpret_cast<float2*>(a.stft_ri)[(u * nb + k) * a.n_frames + t] = make_float2(re, im);
+    }
+    __syncthreads();
+    float vmax = -INFINITY;
+    for (int m = threadIdx.x; m < a.n_mels; m += 256) {
+        const float* mf = mb + a.mel_start[m];
+        const float* wm = a.mel_weight + m * a.mel_max_width;
+        float acc = 0.f;
+        for (int j = 0; j < a.mel_width[m]; ++j) acc = fmaf(mf[j], wm[j], acc);
+        const float db = acc > a.amin ? 20.0f * log10f(acc) : a.db_floor;
+        vmax = fmaxf(vmax, db);
+        const long long oi = out_index(a.spf, a.n_slices, a.n_mels, a.n_frames, u, m, t);
+        if (oi >= 0) a.mel_db[oi] = db;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) vmax = fmaxf(vmax, __shfl_xor(vmax, o));
+    if ((threadIdx.x & 63) == 0) atomicMax(a.umax + u, f2ord(vmax));
+}
+
+__global__ void k_spec_clamp(SpecArgs a) {
+    const long long per_u = (a.spf > 0) ? (long long)a.n_slices * a.n_mels * a.spf : (long long)a.n_mels * a.n_frames;
+    const long long total = per_u * a.n_utt;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+        const long long u = i / per_u;
+        const float fl = ord2f(a.umax[u]) - a.top_db;
+        a.mel_db[i] = fmaxf(a.mel_db[i], fl);
+    }
+}
+
+}  // namespace
+
+int launch_spectrogram(const SpecArgs& a, hipStream_t s) {
+    if (a.n_utt <= 0) return 0;
+    const bool need_clamp_pass = a.top_db >= 0.f;
+    if (a.n_fft == 640) {
+        const int n_chunks = (a.n_frames + CHUNK - 1) / CHUNK;
+        if (n_chunks > 1) AVSE_HIP_CHECK(hipMemsetAsync(a.umax, 0, sizeof(unsigned) * a.n_utt, s));
+        hipLaunchKernelGGL(k_spec640, dim3(n_chunks, (unsigned)a.n_utt), dim3(64), 0, s, a, n_chunks);
+        AVSE_HIP_CHECK(hipGetLastError());
+        if (n_chunks > 1 && need_clamp_pass) {
+            hipLaunchKernelGGL(k_spec_clamp, dim3(1024), dim3(256), 0, s, a);
+            AVSE_HIP_CHECK(hipGetLastError());
+        }
+        return 0;
+    }
+    AVSE_HIP_CHECK(hipMemsetAsync(a.umax, 0, sizeof(unsigned) * a.n_utt, s));
+    const size_t shm = sizeof(float) * (a.n_fft + a.n_fft / 2 + 1);
+    hipLaunchKernelGGL(k_spec_dft, dim3(a.n_frames, (unsigned)a.n_utt), dim3(256), shm, s, a);
+    AVSE_HIP_CHECK(hipGetLastError());
+    if (need_clamp_pass) {
+        hipLaunchKernelGGL(k_spec_clamp, dim3(1024), dim3(256), 0, s, a);
+        AVSE_HIP_CHECK(hipGetLastError());
+    }
+    return 0;
+}
+
+}  // namespace avse

@@ -1,0 +1,74 @@
+"""SpeechEnhancementNetwork — drop-in for /root/reference/network.py's inference API on MI355X.
+
+build / predict / evaluate / load / save keep the reference's signatures and tensor shapes
+(`predict` takes [N, 80, 20] + [N, 128, 128, 5] and returns np.squeeze of [N, 80, 20, 1]).
+The forward pass is libavse's avse_forward (HIP kernels); there is no Keras and no CPU fallback.
+Training (network.py:177-206) is out of scope for this build.
+"""
+import numpy as np
+import torch
+
+from . import ops
+from .model import AUDIO_SHAPE, VIDEO_SHAPE, KerasModel
+
+
+class SpeechEnhancementNetwork(object):
+
+    def __init__(self, model, compute_dtype="float32", device=None):
+        self.__model = model
+        self.__compute_dtype = compute_dtype
+        self.__device = device
+        self.__dw = None
+
+    @property
+    def model(self):
+        return self.__model
+
+    def device_weights(self):
+        if self.__dw is None:
+            self.__dw = ops.DeviceWeights(self.__model, self.__compute_dtype, self.__device)
+        return self.__dw
+
+    @classmethod
+    def build(cls, audio_spectrogram_shape, video_shape, seed=0, compute_dtype="float32"):
+        """network.py:17-40 — fresh Keras-default-initialised network for these input shapes."""
+        if tuple(audio_spectrogram_shape) != AUDIO_SHAPE or tuple(video_shape) != VIDEO_SHAPE:
+            raise NotImplementedError(
+                f"kernels are specialised for audio {AUDIO_SHAPE} and video {VIDEO_SHAPE} "
+                f"(16 kHz / 25 fps, 200-ms slices); got {tuple(audio_spectrogram_shape)}, {tuple(video_shape)}")
+        return SpeechEnhancementNetwork(KerasModel.init(seed=seed), compute_dtype)
+
+    def train(self, *args, **kwargs):
+        raise NotImplementedError("training (network.py:177-206) is outside this build's hot path")
+
+    def predict_device(self, mixed_spectrograms, video_samples, video_normalizer=None):
+        """Device-tensor forward: [N, 80, 20] x [N, 128, 128, 5] -> [N, 80, 20] (no squeeze)."""
+        a = ops.to_device(mixed_spectrograms, self.__device)
+        v = ops.to_device(video_samples, a.device)
+        m = s = None
+        if video_normalizer is not None:
+            m, s = video_normalizer.device_stats(a.device)
+        return ops.forward(self.device_weights(), a, v, m, s)
+
+    def predict(self, mixed_spectrograms, video_samples, video_normalizer=None):
+        """network.py:208-212.  video_normalizer (optional) fuses VideoNormalizer.normalize into the
+        first video conv instead of normalising the array in place beforehand."""
+        out = self.predict_device(mixed_spectrograms, video_samples, video_normalizer)
+        if isinstance(mixed_spectrograms, torch.Tensor):
+            return out.squeeze()
+        return np.squeeze(out.cpu().numpy())
+
+    def evaluate(self, mixed_spectrograms, video_samples, speech_spectrograms, video_normalizer=None):
+        """network.py:214-220: mean squared error of the prediction over every element."""
+        pred = self.predict_device(mixed_spectrograms, video_samples, video_normalizer)
+        target = ops.to_device(speech_spectrograms, pred.device).reshape(pred.shape)
+        return float(ops.mse(pred, target).item())
+
+    @staticmethod
+    def load(model_cache_path, compute_dtype="float32"):
+        """network.py:222-226 (own safetensors format; Keras HDF5 needs the converter)."""
+        return SpeechEnhancementNetwork(KerasModel.load(model_cache_path), compute_dtype)
+
+    def save(self, model_cache_path):
+        """network.py:228-229."""
+        self.__model.save(model_cache_path)

@@ -1,0 +1,154 @@
+"""Device-level entry points: torch (ROCm) tensors in, torch tensors out, arithmetic in libavse.
+
+Every function here is a thin shape/dtype check around one C-ABI call (include/avse.h) launched
+on torch's current HIP stream.  Nothing computes on the CPU.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from .model import KerasModel, blob_floats
+
+DTYPES = {"float32": _lib.AVSE_F32, "fp32": _lib.AVSE_F32, "bfloat16": _lib.AVSE_BF16, "bf16": _lib.AVSE_BF16}
+
+
+def _dev_f32(t, name, shape=None):
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        raise TypeError(f"{name} must be a ROCm device tensor")
+    if t.dtype != torch.float32:
+        raise TypeError(f"{name} must be float32, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    if shape is not None and tuple(t.shape[-len(shape):]) != tuple(shape):
+        raise ValueError(f"{name} has shape {tuple(t.shape)}, expected [..., {shape}]")
+    return t
+
+
+def n_frames(n_samples, hop, n_fft):
+    """Centred STFT frame count (librosa.stft, center=True): 1 + (L + 2*(n_fft//2) - n_fft) // hop."""
+    return 1 + (n_samples + 2 * (n_fft // 2) - n_fft) // hop
+
+
+def spectrogram(sig, sample_rate=16000, n_fft=640, hop_length=160, n_mels=80, fmin=0.0, fmax=8000.0,
+                amin=1e-5, top_db=80.0, pad_mode="reflect", frames_per_slice=0, return_stft=False):
+    """K1: STFT -> mel -> dB for a batch of utterances.
+
+    sig [U, L] float32 device tensor.  Returns mel_db [U, n_mels, T] (frames_per_slice == 0) or
+    [U, n_slices, n_mels, frames_per_slice]; with return_stft also the complex64 STFT [U, 1+n_fft//2, T].
+    """
+    _dev_f32(sig, "sig")
+    if sig.dim() != 2:
+        raise ValueError("sig must be [n_utterances, n_samples]")
+    U, L = sig.shape
+    T = n_frames(L, hop_length, n_fft)
+    if frames_per_slice:
+        ns = T // frames_per_slice
+        out = torch.empty((U, ns, n_mels, frames_per_slice), dtype=torch.float32, device=sig.device)
+    else:
+        out = torch.empty((U, n_mels, T), dtype=torch.float32, device=sig.device)
+    stft = torch.empty((U, 1 + n_fft // 2, T, 2), dtype=torch.float32, device=sig.device) if return_stft else None
+    pm = {"reflect": _lib.AVSE_PAD_REFLECT, "constant": _lib.AVSE_PAD_CONSTANT}[pad_mode]
+    ctx = _lib.context(sig.device)
+    with torch.cuda.device(sig.device):
+        _lib.check(_lib.load().avse_spectrogram(
+            ctx.handle, _lib.ptr(sig), U, L, int(sample_rate), int(n_fft), int(hop_length), int(n_mels),
+            float(fmin), float(fmax), float(amin), float(-1.0 if top_db is None else top_db), pm,
+            int(frames_per_slice), _lib.ptr(out), _lib.ptr(stft), _lib.stream_handle(sig.device)), "avse_spectrogram")
+    if return_stft:
+        return out, torch.view_as_complex(stft)
+    return out
+
+
+class DeviceWeights:
+    """avse_weights: BN-folded, GEMM-packed weights resident on one device."""
+
+    def __init__(self, model, dtype="float32", device=None):
+        if not isinstance(model, KerasModel):
+            raise TypeError("model must be a KerasModel")
+        self.dtype = DTYPES[dtype] if isinstance(dtype, str) else int(dtype)
+        self.ctx = _lib.context(device)
+        blob = model.to_blob()
+        assert blob.size == blob_floats() == _lib.load().avse_weights_blob_floats()
+        self.handle = ctypes.c_void_p()
+        with torch.cuda.device(self.ctx.device_index):
+            _lib.check(_lib.load().avse_weights_load(self.ctx.handle, blob.ctypes.data_as(ctypes.c_void_p), blob.size,
+                                                     self.dtype, ctypes.byref(self.handle)), "avse_weights_load")
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value and _lib._lib is not None:
+            _lib._lib.avse_weights_destroy(h)
+            self.handle = None
+
+
+def forward(weights, audio, video, vnorm_mean=None, vnorm_std=None, out=None):
+    """K2-K5: network forward.  audio [N, 80, 20], video [N, 128, 128, 5] float32 device tensors
+    (video un-normalised when vnorm_* are given).  Returns [N, 80, 20] float32."""
+    _dev_f32(audio, "audio", (80, 20))
+    _dev_f32(video, "video", (128, 128, 5))
+    N = audio.shape[0]
+    if video.shape[0] != N:
+        raise ValueError("audio and video batch sizes differ")
+    if (vnorm_mean is None) != (vnorm_std is None):
+        raise ValueError("vnorm_mean and vnorm_std must both be given")
+    if vnorm_mean is not None:
+        _dev_f32(vnorm_mean, "vnorm_mean", (128, 128))
+        _dev_f32(vnorm_std, "vnorm_std", (128, 128))
+    if out is None:
+        out = torch.empty((N, 80, 20), dtype=torch.float32, device=audio.device)
+    with torch.cuda.device(audio.device):
+        _lib.check(_lib.load().avse_forward(weights.ctx.handle, weights.handle, _lib.ptr(audio), _lib.ptr(video),
+                                            _lib.ptr(vnorm_mean), _lib.ptr(vnorm_std), N, _lib.ptr(out),
+                                            _lib.stream_handle(audio.device)), "avse_forward")
+    return out
+
+
+def forward_profile(weights, audio, video, vnorm_mean=None, vnorm_std=None, out=None):
+    """forward() with HIP events between kernel launches (synchronises); returns (out, {stage: ms})."""
+    N = audio.shape[0]
+    if out is None:
+        out = torch.empty((N, 80, 20), dtype=torch.float32, device=audio.device)
+    ms = (ctypes.c_float * _lib.AVSE_NUM_STAGES)()
+    with torch.cuda.device(audio.device):
+        _lib.check(_lib.load().avse_forward_profile(weights.ctx.handle, weights.handle, _lib.ptr(audio), _lib.ptr(video),
+                                                    _lib.ptr(vnorm_mean), _lib.ptr(vnorm_std), N, _lib.ptr(out),
+                                                    _lib.stream_handle(audio.device), ms), "avse_forward_profile")
+    return out, dict(zip(_lib.STAGE_NAMES, [float(x) for x in ms]))
+
+
+def video_normalize_(video, mean, std):
+    """In place: video[s, :, :, f] = (video[s, :, :, f] - mean) / std (data_processor.py:208-212)."""
+    _dev_f32(video, "video")
+    _dev_f32(mean, "mean")
+    _dev_f32(std, "std")
+    S, H, W, F = video.shape
+    ctx = _lib.context(video.device)
+    with torch.cuda.device(video.device):
+        _lib.check(_lib.load().avse_video_normalize(ctx.handle, _lib.ptr(video), S, H, W, F, _lib.ptr(mean),
+                                                    _lib.ptr(std), _lib.stream_handle(video.device)),
+                   "avse_video_normalize")
+    return video
+
+
+def mse(pred, target):
+    """Keras mean_squared_error over every element -> 0-dim device tensor."""
+    _dev_f32(pred, "pred")
+    _dev_f32(target, "target")
+    if pred.numel() != target.numel():
+        raise ValueError("pred/target sizes differ")
+    loss = torch.empty((), dtype=torch.float32, device=pred.device)
+    ctx = _lib.context(pred.device)
+    with torch.cuda.device(pred.device):
+        _lib.check(_lib.load().avse_mse(ctx.handle, _lib.ptr(pred), _lib.ptr(target), pred.numel(), _lib.ptr(loss),
+                                        _lib.stream_handle(pred.device)), "avse_mse")
+    return loss
+
+
+def to_device(x, device=None):
+    """numpy / tensor -> contiguous float32 device tensor (host->device copy only)."""
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    if isinstance(x, torch.Tensor):
+        return x.to(device=dev, dtype=torch.float32).contiguous()
+    return torch.from_numpy(np.ascontiguousarray(x, dtype=np.float32)).to(dev)

@@ -1,0 +1,154 @@
+/*
+ * avse.h — C-ABI of libavse.so, the MI355X-native (gfx950) hot path of
+ * melspectrum007/audio-visual-speech-enhancement.
+ *
+ * The reference has no FFI layer: its hot path is the Python API below, whose arithmetic is
+ * delegated to librosa / numpy / Keras.  Each entry point names the reference interface it
+ * replaces (file:line into /root/reference).  The build's Python package
+ * (audio-visual-speech-enhancement_amd/) binds these symbols with ctypes; INTEGRATION.md shows
+ * the binding a maintainer of the reference would add.
+ *
+ * Conventions
+ *  - Every data pointer is a DEVICE pointer into caller-owned memory, unless the parameter name
+ *    starts with host_.
+ *  - Calls are asynchronous and ordered on `stream` (a hipStream_t passed as void*; NULL = the
+ *    legacy default stream).  No call synchronises the device.
+ *  - Every call returns an int status (AVSE_OK = 0).  avse_last_error() returns a thread-local
+ *    message for the last failing call on this thread.
+ *  - A context belongs to one device; it is not thread-safe (lock externally).
+ *  - Buffers are row-major, C-contiguous, float32 unless stated.
+ */
+#ifndef AVSE_H
+#define AVSE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AVSE_ABI_VERSION 1
+
+enum avse_status {
+    AVSE_OK = 0,
+    AVSE_ERR_INVALID = 1,      /* bad argument / shape                                  */
+    AVSE_ERR_HIP = 2,          /* HIP runtime error (message in avse_last_error)       */
+    AVSE_ERR_UNSUPPORTED = 3,  /* configuration outside what the kernels implement      */
+    AVSE_ERR_OOM = 4           /* device allocation failed                             */
+};
+
+enum avse_dtype { AVSE_F32 = 0, AVSE_BF16 = 1 };
+enum avse_pad_mode { AVSE_PAD_REFLECT = 0, AVSE_PAD_CONSTANT = 1 };
+
+typedef struct avse_ctx avse_ctx;
+typedef struct avse_weights avse_weights;
+
+/* ---- library / context ----------------------------------------------------------------- */
+
+int avse_abi_version(void);
+const char* avse_last_error(void);
+
+/* One context per device: owns the DFT twiddle / window / mel tables and the forward scratch. */
+int avse_ctx_create(int device, avse_ctx** out);
+void avse_ctx_destroy(avse_ctx* ctx);
+
+/* Pre-size the forward scratch for up to max_clips clips so that later avse_forward calls never
+ * allocate (required before capturing avse_forward into a hipGraph). */
+int avse_ctx_reserve(avse_ctx* ctx, int64_t max_clips, int compute_dtype);
+
+/* ---- audio front end ------------------------------------------------------------------- */
+
+/* Replaces signal_to_spectrogram(audio_signal, n_fft, hop_length, mel=True, db=True)
+ * (data_processor.py:77-96): librosa.core.stft (:79, periodic Hann, centred, pad_mode) ->
+ * magphase (:80) -> librosa.filters.mel(sr, n_fft, n_mels, fmin, fmax) (Slaney) np.dot (:83-91)
+ * -> librosa.amplitude_to_db(ref=1, amin, top_db) (:94), the top_db clamp taken over each
+ * utterance's WHOLE [n_mels, T] array, and — when frames_per_slice > 0 — the slicing of
+ * preprocess_audio_signal (data_processor.py:49-57) fused into the store.
+ *
+ *   sig      [n_utt][n_samples]                  channel-0 samples (already padded/truncated)
+ *   T        = 1 + n_samples / hop               (centred frames)
+ *   mel_db   frames_per_slice == 0: [n_utt][n_mels][T]
+ *            frames_per_slice  > 0: [n_utt][n_slices][n_mels][frames_per_slice],
+ *                                   n_slices = T / frames_per_slice (trailing frames dropped
+ *                                   from the output but still inside the top_db max)
+ *   stft_ri  nullable; [n_utt][n_fft/2+1][T][2]  complex STFT (re, im), librosa layout
+ *
+ * n_fft == 640 runs the mixed-radix (16 x 20) FFT kernel; other n_fft <= 2048 (e.g. 533 at
+ * 29.97 fps, data_processor.py:44) run a direct-DFT kernel. */
+int avse_spectrogram(avse_ctx* ctx, const float* sig, int64_t n_utt, int64_t n_samples,
+                     int sr, int n_fft, int hop, int n_mels, float fmin, float fmax,
+                     float amin, float top_db, int pad_mode, int frames_per_slice,
+                     float* mel_db, float* stft_ri, void* stream);
+
+/* ---- network --------------------------------------------------------------------------- */
+
+/* Number of float32 values in a canonical weight blob (see avse_weights_load). */
+int64_t avse_weights_blob_floats(void);
+
+/* Replaces SpeechEnhancementNetwork.load (network.py:222-226) for the build's own weight format.
+ * host_blob: the Keras-layout tensors of network.py's layers in creation order (float32):
+ *   for each conv / dense / transposed-conv layer: kernel, bias
+ *     conv (kh, kw, cin, cout); transposed conv (kh, kw, cout, cin); dense (in, out)
+ *   followed, when the layer has a BatchNormalization, by gamma, beta, moving_mean,
+ *   moving_variance.
+ *   order: a_conv1..5, v_conv1..6, enc_dense, dec_dense1, dec_dense2, d_deconv1..6
+ *   (d_deconv6 has no BatchNormalization).
+ * BN (eps 1e-3) is folded into per-channel scale/shift; kernels are repacked for the implicit
+ * GEMM and uploaded in compute_dtype (AVSE_F32 or AVSE_BF16).  Synchronous. */
+int avse_weights_load(avse_ctx* ctx, const float* host_blob, int64_t n_floats, int compute_dtype,
+                      avse_weights** out);
+void avse_weights_destroy(avse_weights* w);
+
+/* Replaces SpeechEnhancementNetwork.predict's Model.predict (network.py:208-212) and the
+ * VideoNormalizer.normalize it is preceded by (data_processor.py:208-212,
+ * speech_enhancer.py:74), fused:
+ *   audio      [N][80][20]        mixed mel-dB spectrograms (the expand_dims(-1) is implicit)
+ *   video      [N][128][128][5]   mouth crops, NOT normalised
+ *   vnorm_mean [128][128]         nullable: VideoNormalizer mean image (applied in-kernel)
+ *   vnorm_std  [128][128]         nullable: VideoNormalizer std image
+ *   out        [N][80][20]        predicted speech mel-dB spectrograms (float32)
+ * Computes in the weights' compute dtype, accumulating in float32. */
+int avse_forward(avse_ctx* ctx, const avse_weights* w, const float* audio, const float* video,
+                 const float* vnorm_mean, const float* vnorm_std, int64_t N, float* out,
+                 void* stream);
+
+/* Stages of the forward pass, in launch order (avse_forward_profile). */
+#define AVSE_NUM_STAGES 22
+/*  0 video prep (normalise + cast)   1 audio prep      2-6 a_conv1..a_conv5
+ *  7-12 v_conv1..v_conv6              13 enc_dense  14 dec_dense1  15 dec_dense2
+ *  16-20 d_deconv1..d_deconv5         21 d_deconv6 (1x1 -> float32 output)            */
+
+/* avse_forward with a HIP event recorded between consecutive kernel launches; synchronises the
+ * stream and writes each stage's elapsed milliseconds to host_ms[AVSE_NUM_STAGES]. */
+int avse_forward_profile(avse_ctx* ctx, const avse_weights* w, const float* audio, const float* video,
+                         const float* vnorm_mean, const float* vnorm_std, int64_t N, float* out,
+                         void* stream, float* host_ms);
+
+/* VideoNormalizer.normalize (data_processor.py:208-212), in place on device:
+ *   video[s, :, :, f] = (video[s, :, :, f] - mean) / std   for video [S][H][W][F]. */
+int avse_video_normalize(avse_ctx* ctx, float* video, int64_t S, int H, int W, int F,
+                         const float* mean, const float* std, void* stream);
+
+/* SpeechEnhancementNetwork.evaluate's loss (network.py:214-220, Keras mean_squared_error over
+ * every element): *loss = mean((pred - target)^2) over n values; loss is a device float. */
+int avse_mse(avse_ctx* ctx, const float* pred, const float* target, int64_t n, float* loss,
+             void* stream);
+
+/* ---- diagnostics ----------------------------------------------------------------------- */
+
+/* Number of forward scratch buffers reported by avse_debug_scratch. */
+#define AVSE_DEBUG_NBUF 20
+
+/* Layout of the forward scratch for batch N in compute_dtype, valid after an avse_forward call
+ * with that N: *base = device base pointer, offsets[i] = byte offset of buffer i, in launch order:
+ *   0 video-in [N][128][128][8]  1 audio-in [N][80][20][8]  2-5 a_conv1..a_conv4
+ *   6-10 v_conv1..v_conv5 (pooled)  11 concat [N][5248]  12 enc_dense  13 dec_dense1
+ *   14 dec_dense2 [N][5][5][128]  15-19 d_deconv1..d_deconv5          (all NHWC, compute dtype)
+ * Test / debugging aid only. */
+int avse_debug_scratch(avse_ctx* ctx, int64_t N, int compute_dtype, void** base, int64_t* offsets);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AVSE_H */

@@ -1,0 +1,140 @@
+"""K2-K5 parity: libavse forward vs the Keras-semantics oracle (oracle/keras_ref.py, float64).
+
+Tolerances (DESIGN.md "Parity"):
+  fp32 path  — relative RMS  ||gpu - ref||_2 / ||ref||_2 <= 1e-5 and absolute RMS <= 1e-4 x max(1, RMS(ref))
+               (the north star's "enhanced magnitude within 1e-4 RMS"; exact-fp32 MFMA, fp32 accumulation)
+  bf16 path  — relative RMS <= 3e-2 (bf16 operands, fp32 accumulation; SURVEY.md §7 "Tolerance vs bf16")
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import synth_video
+from oracle import keras_ref as K
+from oracle import librosa_ref as R
+
+pytestmark = pytest.mark.gpu
+
+BUF_NAMES = ["video_in", "audio_in", "a_conv1", "a_conv2", "a_conv3", "a_conv4", "v_conv1", "v_conv2", "v_conv3",
+             "v_conv4", "v_conv5", "concat", "enc_dense", "dec_dense1", "dec_dense2", "d_deconv1", "d_deconv2",
+             "d_deconv3", "d_deconv4", "d_deconv5"]
+BUF_SHAPES = {"video_in": (128, 128, 8), "audio_in": (80, 20, 8), "a_conv1": (40, 10, 64), "a_conv2": (40, 10, 64),
+              "a_conv3": (20, 5, 128), "a_conv4": (10, 5, 128), "v_conv1": (64, 64, 128), "v_conv2": (32, 32, 128),
+              "v_conv3": (16, 16, 256), "v_conv4": (8, 8, 256), "v_conv5": (4, 4, 512), "concat": (5248,),
+              "enc_dense": (1312,), "dec_dense1": (1312,), "dec_dense2": (5, 5, 128), "d_deconv1": (10, 5, 128),
+              "d_deconv2": (20, 5, 128), "d_deconv3": (40, 10, 128), "d_deconv4": (40, 10, 64),
+              "d_deconv5": (80, 20, 64)}
+
+
+def make_inputs(N, seed):
+    rng = np.random.default_rng(seed)
+    from conftest import synth_audio
+    x = synth_audio(rng, N, 3200)
+    mel = np.stack([R.signal_to_spectrogram(x[i], 16000, 640, 160)[0][:, :20] for i in range(N)]).astype(np.float32)
+    video = synth_video(rng, N)
+    return mel, video
+
+
+def rel_rms(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.sqrt(np.mean((a - b) ** 2)) / max(np.sqrt(np.mean(b ** 2)), 1e-30))
+
+
+def scratch(dw, N):
+    """Read libavse's intermediate activations (avse_debug_scratch) as float32 numpy arrays."""
+    from avse_amd import _lib
+    base = ctypes.c_void_p()
+    offs = (ctypes.c_int64 * 20)()
+    _lib.check(_lib.load().avse_debug_scratch(dw.ctx.handle, N, dw.dtype, ctypes.byref(base), offs), "debug")
+    dt = torch.bfloat16 if dw.dtype == _lib.AVSE_BF16 else torch.float32
+    es = 2 if dw.dtype == _lib.AVSE_BF16 else 4
+    out = {}
+    torch.cuda.synchronize()
+    for i, name in enumerate(BUF_NAMES):
+        n = N * int(np.prod(BUF_SHAPES[name]))
+        t = torch.empty(n, dtype=dt, device="cuda")
+        from avse_amd import _lib as L
+        hip = ctypes.CDLL("libamdhip64.so.7")
+        hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        rc = hip.hipMemcpy(ctypes.c_void_p(t.data_ptr()), ctypes.c_void_p(base.value + offs[i]), n * es, 3)
+        assert rc == 0
+        out[name] = t.float().cpu().numpy().reshape((N,) + BUF_SHAPES[name])
+    return out
+
+
+def run_case(gpu, N, dtype, seed=0, normalize=False):
+    from avse_amd import ops
+    from avse_amd.model import KerasModel
+    model = KerasModel.init(seed=seed, randomize=True)
+    mel, video = make_inputs(N, seed + 100)
+    mean = std = None
+    vref = video
+    if normalize:
+        mean, std = R.video_normalizer_fit(video)
+        vref = R.video_normalize(video, mean, std).astype(np.float32)
+    inter = {}
+    ref = K.forward(model.layer_dict(), mel, vref, intermediates=inter)
+    dw = ops.DeviceWeights(model, dtype)
+    args = [ops.to_device(mel), ops.to_device(video)]
+    if normalize:
+        args += [ops.to_device(mean), ops.to_device(std)]
+    got = ops.forward(dw, *args).cpu().numpy()
+    return got, ref, inter, dw
+
+
+@pytest.mark.parametrize("N", [1, 3, 37])
+def test_forward_fp32_matches_oracle(gpu, N):
+    got, ref, inter, dw = run_case(gpu, N, "float32", seed=N)
+    err = rel_rms(got, ref)
+    abs_rms = float(np.sqrt(np.mean((got.astype(np.float64) - ref) ** 2)))
+    if err > 1e-5:
+        sc = scratch(dw, N)
+        report = {k: rel_rms(sc[k], inter[k]) for k in inter if k in sc}
+        pytest.fail(f"rel RMS {err:.3e}; per-layer rel RMS: {report}")
+    assert abs_rms <= 1e-4 * max(1.0, float(np.sqrt(np.mean(ref ** 2)))), abs_rms
+
+
+def test_forward_fp32_fused_normalizer(gpu):
+    got, ref, inter, dw = run_case(gpu, 4, "float32", seed=7, normalize=True)
+    assert rel_rms(got, ref) <= 1e-5
+
+
+@pytest.mark.parametrize("N", [2, 130])
+def test_forward_bf16_matches_oracle(gpu, N):
+    got, ref, inter, dw = run_case(gpu, N, "bfloat16", seed=11 + N, normalize=True)
+    err = rel_rms(got, ref)
+    if err > 3e-2:
+        sc = scratch(dw, N)
+        report = {k: rel_rms(sc[k], inter[k]) for k in inter if k in sc}
+        pytest.fail(f"rel RMS {err:.3e}; per-layer rel RMS: {report}")
+
+
+def test_intermediates_fp32(gpu):
+    """Every layer's activation, not only the output, matches the oracle (catches compensating bugs)."""
+    got, ref, inter, dw = run_case(gpu, 2, "float32", seed=21)
+    sc = scratch(dw, 2)
+    for k in inter:
+        if k in sc:
+            assert rel_rms(sc[k], inter[k]) <= 1e-5, (k, rel_rms(sc[k], inter[k]))
+
+
+def test_mse_matches(gpu):
+    from avse_amd import ops
+    rng = np.random.default_rng(0)
+    a = rng.normal(size=(5, 80, 20)).astype(np.float32)
+    b = rng.normal(size=(5, 80, 20)).astype(np.float32)
+    got = float(ops.mse(ops.to_device(a), ops.to_device(b)).item())
+    assert abs(got - K.mse(a, b)) <= 1e-6 * K.mse(a, b)
+
+
+def test_network_api_shapes(gpu):
+    from avse_amd.network import SpeechEnhancementNetwork
+    net = SpeechEnhancementNetwork.build((80, 20), (128, 128, 5))
+    mel, video = make_inputs(3, 5)
+    assert net.predict(mel, video).shape == (3, 80, 20)
+    assert net.predict(mel[:1], video[:1]).shape == (80, 20)      # np.squeeze quirk (network.py:212)
+    loss = net.evaluate(mel, video, mel)
+    assert isinstance(loss, float) and np.isfinite(loss)

@@ -1,0 +1,122 @@
+"""CPU tests of the host side: the C-ABI library loads and exports what include/avse.h declares,
+the weight container / blob layout, persistence, and the mediaio stand-in.  No GPU compute."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_functions():
+    src = open(os.path.join(ROOT, "include", "avse.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(avse_[a-z_0-9]+)\s*\(", src)))
+
+
+def test_header_declares_expected_entry_points():
+    fns = declared_functions()
+    for f in ["avse_ctx_create", "avse_spectrogram", "avse_weights_load", "avse_forward", "avse_mse",
+              "avse_video_normalize", "avse_last_error", "avse_forward_profile"]:
+        assert f in fns
+
+
+def test_library_exports_every_declared_symbol():
+    from avse_amd import _lib
+    lib = _lib.load()
+    for f in declared_functions():
+        assert hasattr(lib, f), f"libavse.so does not export {f}"
+        assert f in _lib.SIGNATURES, f"_lib.SIGNATURES lacks {f}"
+
+
+def test_library_is_gfx950_code_object():
+    from avse_amd import _lib
+    data = open(_lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in data
+    assert b"k_spec640" in data and b"k_conv" in data
+
+
+def test_abi_version_and_blob_size():
+    from avse_amd import _lib
+    from avse_amd.model import blob_floats
+    lib = _lib.load()
+    assert lib.avse_abi_version() == 1
+    assert lib.avse_weights_blob_floats() == blob_floats()
+
+
+def test_null_arguments_are_rejected_without_gpu_work():
+    from avse_amd import _lib
+    lib = _lib.load()
+    rc = lib.avse_ctx_create(0, None)
+    assert rc == 1 and b"NULL" in lib.avse_last_error()
+    rc = lib.avse_forward(None, None, None, None, None, None, 1, None, None)
+    assert rc == 1
+
+
+def test_model_init_blob_roundtrip(tmp_path):
+    from avse_amd.model import KerasModel, tensor_names
+    m = KerasModel.init(seed=3, randomize=True)
+    blob = m.to_blob()
+    assert blob.dtype == np.float32 and blob.size == sum(int(np.prod(s)) for _, s in tensor_names())
+    p = str(tmp_path / "model.h5py")
+    m.save(p)
+    m2 = KerasModel.load(p)
+    assert np.array_equal(m2.to_blob(), blob)
+    # Keras-default init: BN identity stats, zero bias
+    d = KerasModel.init(seed=0).layer_dict()
+    assert np.all(d["v_conv1_bn"]["gamma"] == 1) and np.all(d["v_conv1_bn"]["moving_variance"] == 1)
+    assert np.all(d["enc_dense"]["bias"] == 0)
+
+
+def test_keras_layouts():
+    from avse_amd.model import KerasModel
+    d = KerasModel.init(seed=0).layer_dict()
+    assert d["a_conv1"]["kernel"].shape == (5, 5, 1, 64)
+    assert d["v_conv1"]["kernel"].shape == (5, 5, 5, 128)
+    assert d["enc_dense"]["kernel"].shape == (5248, 1312)
+    assert d["d_deconv5"]["kernel"].shape == (5, 5, 64, 64)
+    assert d["d_deconv6"]["kernel"].shape == (1, 1, 1, 64)
+    assert d["dec_dense2_bn"]["gamma"].shape == (128,)
+    # glorot limit respected
+    lim = np.sqrt(6.0 / (5248 + 1312))
+    assert np.abs(d["enc_dense"]["kernel"]).max() <= lim
+
+
+def test_hdf5_is_rejected_with_a_clear_message(tmp_path):
+    from avse_amd.model import KerasModel
+    p = tmp_path / "model.h5py"
+    p.write_bytes(b"\x89HDF\r\n\x1a\n" + b"\0" * 64)
+    with pytest.raises(ValueError, match="HDF5"):
+        KerasModel.load(str(p))
+
+
+def test_audio_signal_pad_truncate_in_place():
+    from avse_amd.audio_io import AudioMixer, AudioSignal
+    s = AudioSignal(np.arange(10, dtype=np.int16), 16000)
+    s.pad_with_zeros(15)
+    assert s.get_number_of_samples() == 15 and s.get_data(0)[-1] == 0
+    s.truncate(4)
+    assert s.get_data(0).tolist() == [0, 1, 2, 3]
+    n = AudioSignal(np.ones(4), 16000)
+    f = AudioMixer.snr_factor(s, n, snr_db=0)
+    assert f == pytest.approx(np.sqrt(np.mean(np.arange(4.0) ** 2)))
+    mix = AudioMixer.mix([s, n], [1, 1])
+    assert mix.get_data(0).tolist() == [1, 2, 3, 4]
+
+
+def test_wav_roundtrip(tmp_path):
+    from avse_amd.audio_io import AudioSignal
+    x = (np.sin(np.arange(1600) / 10) * 1000).astype(np.int16)
+    p = str(tmp_path / "a.wav")
+    AudioSignal(x, 16000).save_to_wav_file(p)
+    y = AudioSignal.from_wav_file(p)
+    assert y.get_sample_rate() == 16000 and np.array_equal(y.get_data(0), x)
+
+
+def test_ops_refuse_cpu_tensors():
+    import torch
+    from avse_amd import ops
+    with pytest.raises(TypeError):
+        ops.spectrogram(torch.zeros(1, 3200))

@@ -1,0 +1,244 @@
+"""CPU tests: the oracle pinned against the reference's own behaviour and analytic known answers.
+
+Golden fixtures (tests/golden/*.json) come from executing the reference's own data_processor.py /
+network.py with stub third-party modules (tests/golden/make_fixtures.py).  The librosa / Keras
+arithmetic itself has no reference test or fixture (parity unpinned); it is checked against
+closed-form answers below.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import keras_ref as K
+from oracle import librosa_ref as R
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def load(name):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)
+
+
+# ---------------------------------------------------------------- slicing (bit-exact integers)
+@pytest.mark.parametrize("case", load("slicing.json")["preprocess_audio_signal"], ids=lambda c: f"{c['n_samples_in']}@{c['fps']}")
+def test_oracle_geometry_matches_reference(case):
+    g = R.frame_geometry(16000, 200, case["n_video_slices"], case["fps"])
+    assert g["signal_length"] == case["signal_length"]
+    assert g["n_fft"] == case["n_fft"] and g["hop_length"] == case["hop_length"]
+    assert g["n_frames"] == case["n_frames"]
+    assert [g["n_slices"], 80, g["spectrogram_samples_per_slice"]] == case["out_shape"]
+    spf = g["spectrogram_samples_per_slice"]
+    ids = np.arange(g["n_frames"])[: g["n_slices"] * spf].reshape(g["n_slices"], spf)
+    assert ids.tolist() == case["frame_ids"]
+    # the oracle's own STFT produces exactly n_frames columns for that signal length
+    assert R.stft(np.zeros(g["signal_length"], np.float32), g["n_fft"], g["hop_length"]).shape[1] == case["n_frames"]
+
+
+@pytest.mark.parametrize("case", load("slicing.json")["preprocess_audio_signal"], ids=lambda c: f"{c['n_samples_in']}@{c['fps']}")
+def test_product_geometry_matches_reference(case):
+    from avse_amd.data_processor import frame_geometry
+    g = frame_geometry(16000, 200, case["n_video_slices"], case["fps"])
+    assert (g["signal_length"], g["n_fft"], g["hop_length"], g["n_frames"]) == \
+        (case["signal_length"], case["n_fft"], case["hop_length"], case["n_frames"])
+    assert [g["n_slices"], 80, g["spectrogram_samples_per_slice"]] == case["out_shape"]
+
+
+def test_reconstruct_call_shapes_match_reference():
+    for rc in load("slicing.json")["reconstruct_speech_signal"]:
+        stft_call, istft_call = rc["calls"]
+        T = stft_call["T"]
+        spf = 20 if rc["fps"] == 25.0 else 24
+        assert istft_call["shape"] == [1 + stft_call["n_fft"] // 2, min(T, rc["n_slices"] * spf)]
+        assert istft_call["hop_length"] == stft_call["hop_length"]
+
+
+def test_oracle_reconstruct_length():
+    rng = np.random.default_rng(0)
+    x = rng.normal(0, 1000, 48000).astype(np.float32)
+    sl = R.preprocess_audio_signal(x, 16000, 200, 15, 25.0)
+    y = R.reconstruct_speech_signal(x, 16000, sl, 25.0)
+    assert y.shape == (160 * (300 - 1),)
+
+
+# ---------------------------------------------------------------- network spec (pinned)
+def test_layer_spec_matches_reference_graph():
+    from avse_amd.model import LAYERS
+    graph = load("network_spec.json")["graph"]
+    convs = [e for e in graph if e["layer"] in ("Conv2D", "Conv2DTranspose", "Dense")]
+    assert len(convs) == len(LAYERS) == 20
+    # reference creation order: audio enc, video enc, enc dense, dec dense x2, deconvs
+    for e, L in zip(convs, LAYERS):
+        kind = {"Conv2D": "conv", "Conv2DTranspose": "deconv", "Dense": "dense"}[e["layer"]]
+        assert kind == L.kind, (e, L)
+        assert e["args"][0] == L.cout
+        if kind != "dense":
+            assert tuple(e["kwargs"]["kernel_size"]) == L.kernel
+            assert tuple(e["kwargs"].get("strides", (1, 1))) == L.strides
+            assert e["kwargs"]["padding"] == "same"
+            cin = e["in"][0][-1]
+            assert cin == L.cin
+        else:
+            assert e["in"][0] == [L.cin]
+    # oracle restatement agrees too
+    oracle_layers = K.AUDIO_ENCODER + K.VIDEO_ENCODER + K.AUDIO_DECODER
+    ref_convs = [e for e in convs if e["layer"] != "Dense"]
+    for e, o in zip(ref_convs, oracle_layers):
+        assert (e["args"][0], tuple(e["kwargs"]["kernel_size"]), tuple(e["kwargs"].get("strides", (1, 1)))) == (o[2], o[3], o[4])
+    # BN after every conv/dense except the last deconv; pooling after every video conv
+    names = [e["layer"] for e in graph]
+    assert names.count("BatchNormalization") == 19
+    assert names.count("MaxPooling2D") == 6
+    comp = [e for e in graph if e["layer"] == "compile"][0]
+    assert comp["loss"] == "mean_squared_error" and comp["optimizer"] == ["adam", 0.0005]
+
+
+def test_shapes_propagate_like_reference():
+    graph = load("network_spec.json")["graph"]
+    cat = [e for e in graph if e["layer"] == "Concatenate"][0]
+    assert cat["in"] == [[3200], [2048]] and cat["out"] == [5248]
+    outs = [e["out"] for e in graph if e["layer"] == "Conv2DTranspose"]
+    assert outs[-1] == [80, 20, 1]
+
+
+def test_param_count():
+    from avse_amd.model import blob_floats
+    # 18,619,073 conv/dense params + 19 BN layers holding 22,272 (4 x 5,568 channels)
+    assert blob_floats() == 18_619_073 + 22_272
+
+
+# ---------------------------------------------------------------- librosa restatement, analytic
+def test_slaney_mel_scale_known_values():
+    assert R.hz_to_mel(0.0) == 0.0
+    assert abs(R.hz_to_mel(1000.0) - 15.0) < 1e-12
+    assert abs(R.hz_to_mel(8000.0) - (15.0 + np.log(8.0) / (np.log(6.4) / 27.0))) < 1e-9
+    f = np.linspace(0, 8000, 97)
+    assert np.allclose(R.mel_to_hz(R.hz_to_mel(f)), f, atol=1e-9)
+
+
+def test_mel_filterbank_structure():
+    fb = R.mel_filterbank(16000, 640, 80, 0, 8000)
+    assert fb.shape == (80, 321)
+    assert (fb >= 0).all()
+    nz = fb > 0
+    assert nz.sum() == 625
+    assert nz.sum(1).max() == 23
+    for m in range(80):
+        idx = np.flatnonzero(nz[m])
+        assert idx.size and np.all(np.diff(idx) == 1)     # one contiguous triangle per band
+    # Slaney area normalisation: each triangle integrates to ~1 over Hz (wide bands, bin width 25 Hz)
+    area = fb.sum(1) * 25.0
+    assert np.allclose(area[40:], 1.0, rtol=0.03)
+
+
+def test_stft_matches_direct_dft():
+    rng = np.random.default_rng(0)
+    x = rng.normal(size=100)
+    n_fft, hop = 16, 4
+    D = R.stft(x, n_fft, hop)
+    xp = np.pad(x, n_fft // 2, mode="reflect")
+    w = 0.5 - 0.5 * np.cos(2 * np.pi * np.arange(n_fft) / n_fft)
+    for t in range(D.shape[1]):
+        fr = xp[t * hop: t * hop + n_fft] * w
+        ref = np.array([np.sum(fr * np.exp(-2j * np.pi * k * np.arange(n_fft) / n_fft)) for k in range(n_fft // 2 + 1)])
+        assert np.allclose(D[:, t], ref, atol=1e-5)
+
+
+def test_stft_of_constant_is_hann_spectrum():
+    D = R.stft(np.ones(3200), 640, 160)
+    mid = D[:, 10]
+    assert abs(mid[0] - 320) < 1e-3 and abs(mid[1] + 160) < 1e-3
+    assert np.abs(mid[2:]).max() < 1e-3
+
+
+def test_amplitude_to_db_floor_and_top_db():
+    assert np.all(R.amplitude_to_db(np.zeros((80, 21))) == -100.0)
+    S = np.array([[1e4, 1.0, 1e-3]])
+    d = R.amplitude_to_db(S)
+    assert d[0, 0] == pytest.approx(80.0)
+    assert d[0, 1] == pytest.approx(0.0)
+    assert d[0, 2] == pytest.approx(0.0)        # clamped at max - 80
+    assert np.allclose(R.db_to_amplitude(R.amplitude_to_db(S, top_db=None)), S)
+
+
+def test_istft_inverts_stft():
+    rng = np.random.default_rng(1)
+    x = rng.normal(0, 1000, 48000)
+    y = R.istft(R.stft(x, 640, 160), 160)
+    assert y.shape == (48000,)
+    assert np.abs(y - x).max() / np.abs(x).max() < 1e-5
+
+
+def test_tone_lands_in_expected_band():
+    t = np.arange(3200) / 16000
+    mel, _ = R.signal_to_spectrogram(10000 * np.sin(2 * np.pi * 1000 * t), 16000, 640, 160)
+    fb = R.mel_filterbank(16000, 640, 80, 0, 8000)
+    assert int(np.argmax(mel[:, 10])) == int(np.argmax(fb[:, 40]))
+
+
+# ---------------------------------------------------------------- Keras restatement, analytic
+def _naive_conv_same(x, k, b, s):
+    """x [H, W, Cin], k (kh, kw, cin, cout) — TF 'SAME' by definition."""
+    H, W, _ = x.shape
+    kh, kw, _, co = k.shape
+    Ho, Wo = -(-H // s[0]), -(-W // s[1])
+    pt = max((Ho - 1) * s[0] + kh - H, 0) // 2
+    pl = max((Wo - 1) * s[1] + kw - W, 0) // 2
+    y = np.tile(b, (Ho, Wo, 1)).astype(np.float64)
+    for oy in range(Ho):
+        for ox in range(Wo):
+            for ky in range(kh):
+                for kx in range(kw):
+                    iy, ix = oy * s[0] + ky - pt, ox * s[1] + kx - pl
+                    if 0 <= iy < H and 0 <= ix < W:
+                        y[oy, ox] += x[iy, ix] @ k[ky, kx]
+    return y
+
+
+def _naive_deconv_same(x, k, b, s):
+    """x [H, W, Cin], k (kh, kw, cout, cin) — TF conv2d_transpose 'SAME' by definition (scatter form)."""
+    H, W, _ = x.shape
+    kh, kw, co, _ = k.shape
+    Ho, Wo = H * s[0], W * s[1]
+    pt, pl = max(kh - s[0], 0) // 2, max(kw - s[1], 0) // 2
+    y = np.tile(b, (Ho, Wo, 1)).astype(np.float64)
+    for iy in range(H):
+        for ix in range(W):
+            for ky in range(kh):
+                for kx in range(kw):
+                    oy, ox = iy * s[0] + ky - pt, ix * s[1] + kx - pl
+                    if 0 <= oy < Ho and 0 <= ox < Wo:
+                        y[oy, ox] += k[ky, kx] @ x[iy, ix]
+    return y
+
+
+@pytest.mark.parametrize("H,W,k,s", [(8, 6, (5, 5), (2, 2)), (8, 6, (4, 4), (1, 1)), (6, 5, (2, 2), (2, 1)), (7, 7, (3, 3), (1, 1))])
+def test_conv_same_semantics(H, W, k, s):
+    rng = np.random.default_rng(0)
+    x = rng.normal(size=(H, W, 3))
+    kern = rng.normal(size=k + (3, 4))
+    b = rng.normal(size=4)
+    got = K.conv_same(torch.from_numpy(x).permute(2, 0, 1)[None], kern, b, s, torch.float64)[0].permute(1, 2, 0).numpy()
+    assert np.allclose(got, _naive_conv_same(x, kern, b, s))
+
+
+@pytest.mark.parametrize("H,W,k,s", [(5, 5, (2, 2), (2, 1)), (4, 3, (4, 4), (2, 2)), (5, 4, (4, 4), (1, 1)), (4, 3, (5, 5), (2, 2))])
+def test_deconv_same_semantics(H, W, k, s):
+    rng = np.random.default_rng(1)
+    x = rng.normal(size=(H, W, 3))
+    kern = rng.normal(size=k + (4, 3))
+    b = rng.normal(size=4)
+    got = K.deconv_same(torch.from_numpy(x).permute(2, 0, 1)[None], kern, b, s, torch.float64)[0].permute(1, 2, 0).numpy()
+    assert np.allclose(got, _naive_deconv_same(x, kern, b, s))
+
+
+def test_forward_shapes_and_mse():
+    from avse_amd.model import KerasModel
+    m = KerasModel.init(seed=0, randomize=True)
+    rng = np.random.default_rng(0)
+    out = K.forward(m.layer_dict(), rng.normal(size=(2, 80, 20)), rng.normal(size=(2, 128, 128, 5)))
+    assert out.shape == (2, 80, 20) and np.isfinite(out).all()
+    assert K.mse(out, out) == 0.0
