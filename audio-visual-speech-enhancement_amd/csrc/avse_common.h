@@ -87,10 +87,41 @@ struct ConvArgs {
     int pool;            // fused 2x2 max pool
     int act;             // 1 = LeakyReLU(0.3)
     int nphase;
+    int ksplit;          // >1: split-K over blockIdx.z, fp32 partials + k_splitk_reduce (nphase == 1)
+    float* partial;      // [ksplit][M][Co] workspace
     ConvPhase ph[MAX_PHASES];
 };
 
 int launch_conv(const ConvArgs& a, int dtype, hipStream_t s);
+
+// ---- halo-tiled video convolutions (conv_halo.hip), bf16 only ----------------------------
+enum HaloVariant { HALO_NONE = -1, HALO_V1 = 0, HALO_K5 = 1, HALO_K3_16 = 2, HALO_K3_8 = 3 };
+
+// K-slices (32 input channels x one tap; V1: 4 taps x 8 channels) processed per barrier step.
+constexpr int HALO_NT = 2;
+// K-slices per 128-channel group: 4 x taps (V1: ceil(taps/4)), taps padded to a multiple of HALO_NT.
+__host__ __device__ constexpr int halo_slices_per_group(int ks, bool v1) {
+    return v1 ? (((ks * ks + 3) / 4 + HALO_NT - 1) / HALO_NT) * HALO_NT
+              : 4 * (((ks * ks + HALO_NT - 1) / HALO_NT) * HALO_NT);
+}
+
+struct HaloArgs {
+    int variant;
+    const void* in;          // bf16 [N][Hc][Wc][Ci]            (not V1)
+    const float* video;      // f32  [N][Hc][Wc][5] raw video   (V1)
+    const float* vmean;      // nullable [Hc][Wc]               (V1)
+    const float* vstd;
+    void* out;               // bf16, pooled [N][Hc/2][Wc/2][Co] at (clip stride, pixel stride, channel offset)
+    const void* w;           // bf16 [step][Co][32]
+    const float* scale;
+    const float* shift;
+    int N, Hc, Wc, Ci, Co;
+    long long out_clip_stride;
+    int out_pix_stride;
+    int out_c_off;
+};
+
+int launch_conv_halo(const HaloArgs& a, hipStream_t s);
 int launch_video_prep(const float* video, const float* mean, const float* stdv, void* out, int64_t N,
                       int dtype, hipStream_t s);
 int launch_audio_prep(const float* audio, void* out, int64_t N, int dtype, hipStream_t s);

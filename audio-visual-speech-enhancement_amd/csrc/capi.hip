@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -159,6 +160,8 @@ struct GpuLayer {
     float* scale = nullptr;
     float* shift = nullptr;
     int2* taps = nullptr;
+    int halo = HALO_NONE;     // halo-tiled kernel variant (bf16 video convs)
+    void* w_halo = nullptr;   // bf16 [step][Cout][32] packing for conv_halo.hip
 };
 
 struct avse_weights {
@@ -198,6 +201,28 @@ const size_t kBufElems[B_COUNT] = {128 * 128 * 8, 80 * 20 * 8, 40 * 10 * 64, 40 
                                    4 * 4 * 512, 5248, 1312, 1312, 3200, 10 * 5 * 128, 20 * 5 * 128,
                                    40 * 10 * 128, 40 * 10 * 64, 80 * 20 * 64};
 
+// Split-K plan for a single-phase GEMM of M rows x Co columns x kpad: double the split while the
+// grid stays <= ~1024 workgroups and every split keeps >= 16 k-slabs (64-byte slabs).
+int choose_ksplit(int64_t M, int Co, int kpad, int dtype) {
+    const int BN = Co <= 64 ? 64 : 128;
+    const int64_t tiles = ((M + 127) / 128) * ((Co + BN - 1) / BN);
+    const int nslab = kpad / (dtype == AVSE_BF16 ? 32 : 16);
+    int ks = 1;
+    while (tiles * ks * 2 <= 1024 && nslab / (ks * 2) >= 16) ks *= 2;
+    return ks;
+}
+
+// fp32 partial-sum workspace needed by the split-K layers (enc/dec dense, v_conv6) at batch N
+size_t split_ws_bytes(int64_t N, int dtype) {
+    const struct { int64_t M; int Co, kpad; } g[4] = {{N, 1312, 5248}, {N, 1312, 1312}, {N, 3200, 1312}, {N * 16, 512, 4608}};
+    size_t mx = 0;
+    for (const auto& x : g) {
+        const int ks = choose_ksplit(x.M, x.Co, x.kpad, dtype);
+        if (ks > 1) mx = std::max(mx, (size_t)ks * (size_t)x.M * (size_t)x.Co * 4);
+    }
+    return mx;
+}
+
 size_t arena_bytes(int64_t clips, int dtype, size_t* offs) {
     const size_t es = dtype == AVSE_BF16 ? 2 : 4;
     size_t off = 0;
@@ -205,6 +230,8 @@ size_t arena_bytes(int64_t clips, int dtype, size_t* offs) {
         if (offs) offs[b] = off;
         off += (kBufElems[b] * es * (size_t)clips + 255) & ~(size_t)255;
     }
+    if (offs) offs[B_COUNT] = off;   // split-K partials
+    off += (split_ws_bytes(clips, dtype) + 255) & ~(size_t)255;
     return off;
 }
 
@@ -372,7 +399,64 @@ int build_layer(avse_weights* W, const LayerDef& L, const float* kernel, const f
     if ((rc = upload(W, scale, &G.scale))) return rc;
     if ((rc = upload(W, shift, &G.shift))) return rc;
     if ((rc = upload(W, taps, &G.taps))) return rc;
+
+    // halo-tiled packing for the bf16 video convs: [step][Cout][32], step = (cg*4 + cc)*KS^2 + tap
+    // (V1: step = group of 4 taps, 8 channels each, channels 5..7 and taps >= 25 zero)
+    const char* no_halo = std::getenv("AVSE_NO_HALO");   // A/B switch: force the generic kernel
+    if (W->dtype == AVSE_BF16 && L.kind == CONV && L.pool && L.hin >= 8 && !(no_halo && no_halo[0] == '1')) {
+        const int ntap = L.kh * L.kw;
+        if (L.cin == 5) G.halo = HALO_V1;
+        else if (L.kh == 5) G.halo = HALO_K5;
+        else if (L.hin >= 16) G.halo = HALO_K3_16;
+        else G.halo = HALO_K3_8;
+        const bool v1 = G.halo == HALO_V1;
+        const int spg = halo_slices_per_group(L.kh, v1);           // slices per 128-channel group
+        const int ntp = spg / 4;                                   // padded taps per 32-channel chunk
+        const int nsteps = v1 ? spg : (L.cin / 128) * spg;
+        std::vector<uint16_t> hp((size_t)nsteps * L.cout * 32, 0);
+        for (int st = 0; st < nsteps; ++st)
+            for (int n = 0; n < L.cout; ++n)
+                for (int kk = 0; kk < 32; ++kk) {
+                    float v = 0.f;
+                    if (v1) {
+                        const int tap = 4 * st + kk / 8, c = kk % 8;
+                        if (tap < ntap && c < L.cin) v = kernel[((size_t)tap * L.cin + c) * L.cout + n];
+                    } else {
+                        const int tap = st % ntp, chunk = st / ntp;   // chunk = cg*4 + cc
+                        const int c = chunk * 32 + kk;
+                        if (tap < ntap) v = kernel[((size_t)tap * L.cin + c) * L.cout + n];
+                    }
+                    hp[((size_t)st * L.cout + n) * 32 + kk] = f2bf(v);
+                }
+        uint16_t* d;
+        if ((rc = upload(W, hp, &d))) return rc;
+        G.w_halo = d;
+    }
     return 0;
+}
+
+HaloArgs halo_args(const GpuLayer& G, const void* in, const float* video, const float* vmean, const float* vstd,
+                   void* out, long long out_clip_stride, int out_pix_stride, int out_c_off, int64_t N) {
+    HaloArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.variant = G.halo;
+    a.in = in;
+    a.video = video;
+    a.vmean = vmean;
+    a.vstd = vstd;
+    a.out = out;
+    a.w = G.w_halo;
+    a.scale = G.scale;
+    a.shift = G.shift;
+    a.N = (int)N;
+    a.Hc = G.def.hin;
+    a.Wc = G.def.win;
+    a.Ci = G.def.cin;
+    a.Co = G.def.cout;
+    a.out_clip_stride = out_clip_stride;
+    a.out_pix_stride = out_pix_stride;
+    a.out_c_off = out_c_off;
+    return a;
 }
 
 ConvArgs conv_args(const GpuLayer& G, const void* in, long long in_clip_stride, void* out, long long out_clip_stride,
@@ -406,6 +490,7 @@ ConvArgs conv_args(const GpuLayer& G, const void* in, long long in_clip_stride, 
     a.pool = L.pool ? 1 : 0;
     a.act = 1;
     a.nphase = G.nphase;
+    a.ksplit = 1;
     for (int p = 0; p < G.nphase; ++p) a.ph[p] = G.ph[p];
     return a;
 }
@@ -559,9 +644,15 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
     int rc = ensure_arena(c, N, W->dtype);
     if (rc) return rc;
     const int dt = W->dtype;
-    size_t off[B_COUNT];
+    size_t off[B_COUNT + 1];
     arena_bytes(N, dt, off);
     auto buf = [&](int b) { return (void*)(c->arena + off[b]); };
+    auto split = [&](ConvArgs& a) {   // dense layers / v_conv6: split-K when the grid is small
+        if (a.nphase != 1) return;
+        const int64_t M = (int64_t)a.N * a.Hq * a.Wq;
+        a.ksplit = choose_ksplit(M, a.Co, a.ph[0].kpad, dt);
+        a.partial = reinterpret_cast<float*>(c->arena + off[B_COUNT]);
+    };
     auto L = [&](int i) -> const GpuLayer& { return W->layers[i]; };
     int stage = 0;
     auto mark = [&]() -> int {
@@ -570,7 +661,9 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
         return 0;
     };
     if ((rc = mark())) return rc;
-    if ((rc = launch_video_prep(video, vmean, vstd, buf(B_VIN), N, dt, s)) || (rc = mark())) return rc;
+    // the halo-tiled v_conv1 reads the raw video and normalises it itself
+    if (L(5).halo == HALO_NONE && (rc = launch_video_prep(video, vmean, vstd, buf(B_VIN), N, dt, s))) return rc;
+    if ((rc = mark())) return rc;
     if ((rc = launch_audio_prep(audio, buf(B_AIN), N, dt, s)) || (rc = mark())) return rc;
     // audio encoder (network.py:88-109)
     const int a_in[5] = {B_AIN, B_A1, B_A2, B_A3, B_A4};
@@ -585,18 +678,29 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
     const int v_in[6] = {B_VIN, B_V1, B_V2, B_V3, B_V4, B_V5};
     for (int i = 0; i < 6; ++i) {
         const GpuLayer& G = L(5 + i);
+        if (G.halo != HALO_NONE) {
+            HaloArgs h = (i < 5) ? halo_args(G, buf(v_in[i]), video, vmean, vstd, buf(v_in[i + 1]),
+                                             (long long)G.ho * G.wo * G.def.cout, G.def.cout, 0, N)
+                                 : halo_args(G, buf(v_in[i]), video, vmean, vstd, buf(B_CAT), 5248, G.def.cout, 3200, N);
+            if ((rc = launch_conv_halo(h, s)) || (rc = mark())) return rc;
+            continue;
+        }
         const long long in_cs = (long long)G.def.hin * G.def.win * (i == 0 ? G.cin_pad : G.def.cin);
         ConvArgs a = (i < 5) ? conv_args(G, buf(v_in[i]), in_cs, buf(v_in[i + 1]), (long long)G.ho * G.wo * G.def.cout, G.def.cout, 0, N)
                              : conv_args(G, buf(v_in[i]), in_cs, buf(B_CAT), 5248, G.def.cout, 3200, N);  // concat[3200:5248]
+        if (i == 5) split(a);
         if ((rc = launch_conv(a, dt, s)) || (rc = mark())) return rc;
     }
     // fusion + decoder dense (network.py:53-58, :66-78)
     {
         ConvArgs a = conv_args(L(11), buf(B_CAT), 5248, buf(B_E1), 1312, 1312, 0, N);
+        split(a);
         if ((rc = launch_conv(a, dt, s)) || (rc = mark())) return rc;
         a = conv_args(L(12), buf(B_E1), 1312, buf(B_E2), 1312, 1312, 0, N);
+        split(a);
         if ((rc = launch_conv(a, dt, s)) || (rc = mark())) return rc;
         a = conv_args(L(13), buf(B_E2), 1312, buf(B_E3), 3200, 3200, 0, N);
+        split(a);
         if ((rc = launch_conv(a, dt, s)) || (rc = mark())) return rc;
     }
     // audio decoder (network.py:112-135)
@@ -656,7 +760,7 @@ int avse_mse(avse_ctx* c, const float* pred, const float* target, int64_t n, flo
 
 int avse_debug_scratch(avse_ctx* c, int64_t N, int dtype, void** base, int64_t* offsets) {
     if (!c || !base || !offsets || N <= 0) return fail(AVSE_ERR_INVALID, "bad debug_scratch args");
-    size_t off[B_COUNT];
+    size_t off[B_COUNT + 1];
     const size_t need = arena_bytes(N, dtype, off);
     if (!c->arena || need > c->arena_bytes) return fail(AVSE_ERR_INVALID, "no forward scratch of that size yet");
     *base = c->arena;

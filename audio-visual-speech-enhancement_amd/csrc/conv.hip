@@ -62,11 +62,16 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
     const int lane = tid & 63;
     const int wid = tid >> 6;
     const int wm = wid >> 1, wn = wid & 1;
-    const ConvPhase ph = a.ph[blockIdx.z];
+    const int zphase = blockIdx.z / a.ksplit, zsplit = blockIdx.z % a.ksplit;
+    const ConvPhase ph = a.ph[zphase];
     const int M = a.N * a.Hq * a.Wq;
     const int m0 = blockIdx.x * BM;
     const int n0 = blockIdx.y * BN;
-    const int nslab = ph.kpad / SLAB;
+    // split-K: this block reduces slabs [s_begin, s_end) of the phase's K
+    const int nslab_all = ph.kpad / SLAB;
+    const int sps = (nslab_all + a.ksplit - 1) / a.ksplit;
+    const int s_begin = zsplit * sps;
+    const int s_end = min(nslab_all, s_begin + sps);
     const int2* __restrict__ taps = a.taps + ph.tap_off;
 
     // ---- per-thread A rows (2 chunks: rows r and r + 64, same chunk column g) ----
@@ -97,8 +102,8 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
         ri[h].ix0 = xq * a.sx;
     }
     // chunk k position: tap j, channel c (incremental across slabs)
-    int kj = (g * CH) / a.Ci;
-    int kc = g * CH - kj * a.Ci;
+    int kj = (s_begin * SLAB + g * CH) / a.Ci;
+    int kc = s_begin * SLAB + g * CH - kj * a.Ci;
 
     const char* wbase = reinterpret_cast<const char*>(a.w) + ph.w_off * sizeof(T);
 
@@ -151,14 +156,15 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
 #pragma unroll
         for (int j = 0; j < NJ; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-    load_slab(0);
+    const int fr = lane & 15, fg = lane >> 4;
+    if (s_begin < s_end) {
+    load_slab(s_begin);
     store_slab(0);
     __syncthreads();
 
-    const int fr = lane & 15, fg = lane >> 4;
-    for (int s = 0; s < nslab; ++s) {
-        const int buf = s & 1;
-        if (s + 1 < nslab) load_slab(s + 1);
+    for (int s = s_begin; s < s_end; ++s) {
+        const int buf = (s - s_begin) & 1;
+        if (s + 1 < s_end) load_slab(s + 1);
         i32x4 fa[NI], fb[NJ];
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
@@ -185,13 +191,30 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
                         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], bv[e], acc[i][j], 0, 0, 0);
                 }
             }
-        if (s + 1 < nslab) store_slab(buf ^ 1);
+        if (s + 1 < s_end) store_slab(buf ^ 1);
         __syncthreads();
+    }
     }
 
 #undef AS
 #undef BS
     // ---- epilogue: scale/shift (bias + BN), [pool], LeakyReLU, strided NHWC store ----
+    if (a.ksplit > 1) {   // raw fp32 partial sums; k_splitk_reduce applies the layer tail
+        float* part = a.partial + (size_t)zsplit * M * a.Co;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int n = n0 + wn * WN + 16 * j + fr;
+            if (n >= a.Co) continue;
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+                const int mb = m0 + wm * 64 + 16 * i + 4 * fg;
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    if (mb + r < M) part[(size_t)(mb + r) * a.Co + n] = acc[i][j][r];
+            }
+        }
+        return;
+    }
     T* out = reinterpret_cast<T*>(a.out);
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
@@ -229,6 +252,43 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
                 }
             }
         }
+    }
+}
+
+// split-K tail: sum the partial slabs, then scale/shift, [2x2 max pool], LeakyReLU, strided store.
+// One thread per (output pixel, channel); single phase (dense layers, forward convs).
+template <typename T>
+__global__ void k_splitk_reduce(ConvArgs a) {
+    const int M = a.N * a.Hq * a.Wq;
+    const int Mo = a.pool ? M / 4 : M;
+    const long long total = (long long)Mo * a.Co;
+    T* out = reinterpret_cast<T*>(a.out);
+    for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total; idx += (long long)gridDim.x * blockDim.x) {
+        const int n = (int)(idx % a.Co);
+        const int p = (int)(idx / a.Co);
+        const float sc = a.scale[n], sh = a.shift[n];
+        float x = -INFINITY;
+        const int nr = a.pool ? 4 : 1;
+        for (int r = 0; r < nr; ++r) {
+            const int m = a.pool ? 4 * p + r : p;
+            float acc = 0.f;
+            for (int z = 0; z < a.ksplit; ++z) acc += a.partial[((size_t)z * M + m) * a.Co + n];
+            x = fmaxf(x, acc * sc + sh);
+        }
+        if (a.act) x = x >= 0.f ? x : LRELU * x;
+        long long o;
+        if (a.pool) {
+            const int pw = a.Wq >> 1, phh = a.Hq >> 1;
+            const int clip = p / (phh * pw);
+            const int rr = p - clip * phh * pw;
+            o = clip * a.out_clip_stride + (long long)rr * a.out_pix_stride + a.out_c_off + n;
+        } else {
+            const int clip = p / (a.Hq * a.Wq);
+            const int rr = p - clip * a.Hq * a.Wq;
+            const int oy = (rr / a.Wq) * a.oys, ox = (rr % a.Wq) * a.oxs;
+            o = clip * a.out_clip_stride + (long long)(oy * a.Wo + ox) * a.out_pix_stride + a.out_c_off + n;
+        }
+        out[o] = from_f<T>(x);
     }
 }
 
@@ -332,7 +392,11 @@ inline unsigned grid_for(long long n, int block) {
 int launch_conv(const ConvArgs& a, int dtype, hipStream_t s) {
     const int M = a.N * a.Hq * a.Wq;
     const int BN = (a.Co <= 64) ? 64 : 128;
-    dim3 grid((M + BM - 1) / BM, (a.Co + BN - 1) / BN, a.nphase);
+    if (a.ksplit < 1 || (a.ksplit > 1 && (a.nphase != 1 || !a.partial))) {
+        set_error("bad split-K configuration");
+        return 1;
+    }
+    dim3 grid((M + BM - 1) / BM, (a.Co + BN - 1) / BN, a.nphase * a.ksplit);
     if (dtype == 1) {
         if (BN == 64) hipLaunchKernelGGL((k_conv<bf16_t, 64>), grid, dim3(256), 0, s, a);
         else hipLaunchKernelGGL((k_conv<bf16_t, 128>), grid, dim3(256), 0, s, a);
@@ -341,6 +405,12 @@ int launch_conv(const ConvArgs& a, int dtype, hipStream_t s) {
         else hipLaunchKernelGGL((k_conv<float, 128>), grid, dim3(256), 0, s, a);
     }
     AVSE_HIP_CHECK(hipGetLastError());
+    if (a.ksplit > 1) {
+        const long long total = (long long)(a.pool ? M / 4 : M) * a.Co;
+        if (dtype == 1) hipLaunchKernelGGL(k_splitk_reduce<bf16_t>, dim3(grid_for(total, 256)), dim3(256), 0, s, a);
+        else hipLaunchKernelGGL(k_splitk_reduce<float>, dim3(grid_for(total, 256)), dim3(256), 0, s, a);
+        AVSE_HIP_CHECK(hipGetLastError());
+    }
     return 0;
 }
 

@@ -112,6 +112,32 @@ def test_forward_bf16_matches_oracle(gpu, N):
         pytest.fail(f"rel RMS {err:.3e}; per-layer rel RMS: {report}")
 
 
+@pytest.mark.parametrize("N", [1, 5])
+def test_bf16_halo_video_convs_match_generic_kernel(gpu, N, monkeypatch):
+    """The halo-tiled video convs (conv_halo.hip) against the generic implicit-GEMM kernel and the
+    oracle, layer by layer (N=5 exercises the 4-clip tiles of v_conv5 with a ragged last tile)."""
+    from avse_amd import ops
+    from avse_amd.model import KerasModel
+    model = KerasModel.init(seed=3, randomize=True)
+    mel, video = make_inputs(N, 9)
+    mean, std = R.video_normalizer_fit(video)
+    args = [ops.to_device(mel), ops.to_device(video), ops.to_device(mean), ops.to_device(std)]
+    inter = {}
+    ref = K.forward(model.layer_dict(), mel, R.video_normalize(video, mean, std).astype(np.float32), intermediates=inter)
+    dw_h = ops.DeviceWeights(model, "bfloat16")
+    out_h = ops.forward(dw_h, *args).cpu().numpy()
+    sc_h = scratch(dw_h, N)
+    monkeypatch.setenv("AVSE_NO_HALO", "1")
+    dw_g = ops.DeviceWeights(model, "bfloat16")
+    out_g = ops.forward(dw_g, *args).cpu().numpy()
+    sc_g = scratch(dw_g, N)
+    for k in ["v_conv1", "v_conv2", "v_conv3", "v_conv4", "v_conv5"]:
+        assert rel_rms(sc_h[k], inter[k]) <= 1.5e-2, (k, rel_rms(sc_h[k], inter[k]))
+        assert rel_rms(sc_h[k], sc_g[k]) <= 1.5e-2, (k, rel_rms(sc_h[k], sc_g[k]))
+    assert rel_rms(out_h, ref) <= 3e-2
+    assert rel_rms(out_h, out_g) <= 3e-2
+
+
 def test_intermediates_fp32(gpu):
     """Every layer's activation, not only the output, matches the oracle (catches compensating bugs)."""
     got, ref, inter, dw = run_case(gpu, 2, "float32", seed=21)
