@@ -48,6 +48,22 @@ def synth(rng, B):
     return audio, video
 
 
+def pmc_traffic(B, dtype):
+    """HBM bytes per launch of the dominant kernel from the newest committed PMC summary
+    (profiles/<round>_pmc_traffic.json, written by tools/profile.sh from separate FETCH_SIZE /
+    WRITE_SIZE rocprofv3 passes at this batch), or None when no matching profile exists."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+        except ValueError:
+            continue
+        if d.get("batch") == B and dtype == "bf16" and "traffic_bytes_per_launch" in d:
+            return int(d["traffic_bytes_per_launch"])
+    return None
+
+
 def cpu_baseline(audio, video, mean, std, model, budget_s=12.0, max_s=30.0):
     """The CPU oracle (numpy librosa restatement + torch-CPU fp32 Keras graph) on a bounded sample."""
     from oracle import keras_ref, librosa_ref
@@ -161,6 +177,7 @@ def main():
     dom = "v_conv2"
     achieved = FLOP_V_CONV2 * B / (stage_ms[dom] * 1e-3) / 1e12
     peak = PEAK_TFLOPS[args.dtype]
+    traffic = pmc_traffic(B, args.dtype)
     fwd_ms = sum(stage_ms.values())
     result = {
         "metric": METRIC,
@@ -179,9 +196,11 @@ def main():
         "config": {"workload": "STFT (n_fft 640, hop 160, 80 mel, dB) + full audio-visual fusion forward "
                                "(BASELINE configs[3]) on 200-ms@16kHz clips",
                    "global_batch": world * B, "per_gpu_batch": B, "parallelism": f"dp{world}"},
-        "roofline": {"kernel": f"{dom} (k_conv implicit GEMM, M=4096/clip N=128 K=3200, fused BN+LReLU+maxpool)",
+        "roofline": {"kernel": f"{dom} (k_conv_halo<5,16,16,1>: halo-tiled implicit GEMM M=4096/clip N=128 "
+                               "K=3200, fused BN+LReLU+2x2 maxpool)" if args.dtype == "bf16" else
+                               f"{dom} (k_conv<float,128> implicit GEMM, exact-fp32 MFMA)",
                      "bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
-                     "frac": round(achieved / peak, 4), "traffic": None,
+                     "frac": round(achieved / peak, 4), "traffic": traffic,
                      "per_launch_flop": FLOP_V_CONV2 * B, "avg_launch_ms": round(stage_ms[dom], 4)},
         "breakdown": {
             "stft_ms": round(stft_ms, 4),
