@@ -37,6 +37,8 @@ SIGNATURES = {
     "avse_ctx_reserve": (_int, [_c_void_p, _i64, _int]),
     "avse_spectrogram": (_int, [_c_void_p, _c_void_p, _i64, _i64, _int, _int, _int, _int, _flt, _flt, _flt, _flt,
                                 _int, _int, _c_void_p, _c_void_p, _c_void_p]),
+    "avse_istft": (_int, [_c_void_p, _c_void_p, _c_void_p, _i64, _int, _int, _int, _int, _int, _int, _int, _flt, _flt,
+                          _c_void_p, _c_void_p]),
     "avse_weights_blob_floats": (_i64, []),
     "avse_weights_load": (_int, [_c_void_p, _c_void_p, _i64, _int, ctypes.POINTER(_c_void_p)]),
     "avse_weights_destroy": (None, [_c_void_p]),

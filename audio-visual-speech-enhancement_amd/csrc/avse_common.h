@@ -55,6 +55,26 @@ struct SpecArgs {
 
 int launch_spectrogram(const SpecArgs& a, hipStream_t s);
 
+struct IstftArgs {
+    const float* mel_db;      // spf > 0: [n_utt][n_slices][n_mels][spf], else [n_utt][n_mels][T]
+    int spf, n_slices;
+    const float2* stft;       // mixture STFT [n_utt][nb][stft_frames] (phase source)
+    int stft_frames;
+    int64_t n_utt;
+    int T;                    // frames reconstructed
+    int nb;                   // bins = 1 + n_fft_analysis / 2
+    int N;                    // inverse size = 2 (nb - 1)
+    int hop;
+    int n_mels;
+    const float* pinvT;       // [n_mels][nb] pinv(mel)^T
+    const float2* twiddle;    // [N] e^{-2 pi i k / N}
+    const float* window;      // [N] periodic Hann
+    float* frames;            // scratch [n_utt][T][N]
+    float* sig;               // [n_utt][hop (T - 1)]
+};
+
+int launch_istft(const IstftArgs& a, hipStream_t s);
+
 // ---- implicit-GEMM convolution ----------------------------------------------------------
 constexpr int MAX_TAPS = 25;
 constexpr int MAX_PHASES = 4;

@@ -140,9 +140,20 @@ uint16_t f2bf(float f) {
 
 }  // namespace
 
+struct IstftTables {
+    int sr = -1, n_fft = -1, n_mels = -1;
+    double fmin = 0, fmax = 0;
+    float* pinvT = nullptr;     // [n_mels][nb]
+    float2* twiddle = nullptr;  // [N]
+    float* window = nullptr;    // [N]
+};
+
 struct avse_ctx {
     int device = 0;
     SpecTables spec;
+    IstftTables istft;
+    float* frames = nullptr;    // ISTFT frame scratch
+    size_t frames_bytes = 0;
     unsigned* umax = nullptr;
     int64_t umax_cap = 0;
     float* mse_partial = nullptr;
@@ -285,6 +296,71 @@ int ensure_spec_tables(avse_ctx* c, int sr, int n_fft, int n_mels, double fmin, 
     AVSE_HIP_CHECK(hipMemcpy(t.mel.weight, wt.data(), sizeof(float) * wt.size(), hipMemcpyHostToDevice));
     t.sr = sr; t.n_fft = n_fft; t.n_mels = n_mels; t.fmin = fmin; t.fmax = fmax;
     t.mel.n_mels = n_mels; t.mel.n_bins = nb; t.mel.max_width = maxw;
+    return 0;
+}
+
+// pinv(mel) = M^T (M M^T)^{-1} in double (M is full row rank, cond ~4.5 for the reference's
+// filterbanks; equal to np.linalg.pinv's SVD form to ~1e-13), plus the inverse-DFT tables.
+int ensure_istft_tables(avse_ctx* c, int sr, int n_fft, int n_mels, double fmin, double fmax) {
+    IstftTables& t = c->istft;
+    if (t.sr == sr && t.n_fft == n_fft && t.n_mels == n_mels && t.fmin == fmin && t.fmax == fmax) return 0;
+    (void)hipFree(t.pinvT); (void)hipFree(t.twiddle); (void)hipFree(t.window);
+    t = IstftTables();
+    const int nb = 1 + n_fft / 2, N = 2 * (nb - 1);
+    const std::vector<double> M = mel_filterbank(sr, n_fft, n_mels, fmin, fmax);
+    // G = M M^T, then Gauss-Jordan inverse with partial pivoting
+    std::vector<double> G((size_t)n_mels * n_mels), Gi((size_t)n_mels * n_mels, 0.0);
+    for (int i = 0; i < n_mels; ++i)
+        for (int j = 0; j < n_mels; ++j) {
+            double s = 0;
+            for (int k = 0; k < nb; ++k) s += M[(size_t)i * nb + k] * M[(size_t)j * nb + k];
+            G[(size_t)i * n_mels + j] = s;
+        }
+    for (int i = 0; i < n_mels; ++i) Gi[(size_t)i * n_mels + i] = 1.0;
+    for (int col = 0; col < n_mels; ++col) {
+        int piv = col;
+        for (int r = col + 1; r < n_mels; ++r)
+            if (std::fabs(G[(size_t)r * n_mels + col]) > std::fabs(G[(size_t)piv * n_mels + col])) piv = r;
+        if (std::fabs(G[(size_t)piv * n_mels + col]) < 1e-300) return fail(AVSE_ERR_UNSUPPORTED, "mel filterbank is rank deficient");
+        if (piv != col)
+            for (int j = 0; j < n_mels; ++j) {
+                std::swap(G[(size_t)piv * n_mels + j], G[(size_t)col * n_mels + j]);
+                std::swap(Gi[(size_t)piv * n_mels + j], Gi[(size_t)col * n_mels + j]);
+            }
+        const double d = G[(size_t)col * n_mels + col];
+        for (int j = 0; j < n_mels; ++j) { G[(size_t)col * n_mels + j] /= d; Gi[(size_t)col * n_mels + j] /= d; }
+        for (int r = 0; r < n_mels; ++r) {
+            if (r == col) continue;
+            const double f = G[(size_t)r * n_mels + col];
+            if (f == 0) continue;
+            for (int j = 0; j < n_mels; ++j) {
+                G[(size_t)r * n_mels + j] -= f * G[(size_t)col * n_mels + j];
+                Gi[(size_t)r * n_mels + j] -= f * Gi[(size_t)col * n_mels + j];
+            }
+        }
+    }
+    // pinv[k][m] = sum_j M[j][k] Gi[j][m]; stored transposed [m][k]
+    std::vector<float> pinvT((size_t)n_mels * nb);
+    for (int m = 0; m < n_mels; ++m)
+        for (int k = 0; k < nb; ++k) {
+            double s = 0;
+            for (int j = 0; j < n_mels; ++j) s += M[(size_t)j * nb + k] * Gi[(size_t)j * n_mels + m];
+            pinvT[(size_t)m * nb + k] = (float)s;
+        }
+    std::vector<float2> tw(N);
+    std::vector<float> win(N);
+    for (int k = 0; k < N; ++k) {
+        const double ang = -2.0 * M_PI * (double)k / (double)N;
+        tw[k] = make_float2((float)std::cos(ang), (float)std::sin(ang));
+        win[k] = (float)(0.5 - 0.5 * std::cos(2.0 * M_PI * (double)k / (double)N));
+    }
+    AVSE_HIP_CHECK(hipMalloc(&t.pinvT, sizeof(float) * pinvT.size()));
+    AVSE_HIP_CHECK(hipMalloc(&t.twiddle, sizeof(float2) * N));
+    AVSE_HIP_CHECK(hipMalloc(&t.window, sizeof(float) * N));
+    AVSE_HIP_CHECK(hipMemcpy(t.pinvT, pinvT.data(), sizeof(float) * pinvT.size(), hipMemcpyHostToDevice));
+    AVSE_HIP_CHECK(hipMemcpy(t.twiddle, tw.data(), sizeof(float2) * N, hipMemcpyHostToDevice));
+    AVSE_HIP_CHECK(hipMemcpy(t.window, win.data(), sizeof(float) * N, hipMemcpyHostToDevice));
+    t.sr = sr; t.n_fft = n_fft; t.n_mels = n_mels; t.fmin = fmin; t.fmax = fmax;
     return 0;
 }
 
@@ -526,6 +602,8 @@ void avse_ctx_destroy(avse_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)hipFree(c->spec.twiddle); (void)hipFree(c->spec.window);
     (void)hipFree(c->spec.mel.start); (void)hipFree(c->spec.mel.width); (void)hipFree(c->spec.mel.weight);
+    (void)hipFree(c->istft.pinvT); (void)hipFree(c->istft.twiddle); (void)hipFree(c->istft.window);
+    (void)hipFree(c->frames);
     (void)hipFree(c->umax);
     (void)hipFree(c->mse_partial);
     (void)hipFree(c->arena);
@@ -583,6 +661,49 @@ int avse_spectrogram(avse_ctx* c, const float* sig, int64_t n_utt, int64_t n_sam
     a.mel_max_width = c->spec.mel.max_width;
     a.umax = c->umax;
     return launch_spectrogram(a, (hipStream_t)stream);
+}
+
+int avse_istft(avse_ctx* c, const float* mel_db, const float* stft_ri, int64_t n_utt, int n_frames, int stft_frames,
+               int frames_per_slice, int sr, int n_fft, int hop, int n_mels, float fmin, float fmax, float* sig,
+               void* stream) {
+    if (!c || !mel_db || !stft_ri || !sig) return fail(AVSE_ERR_INVALID, "NULL argument");
+    if (n_utt < 0 || n_frames < 1 || stft_frames < n_frames || hop <= 0 || sr <= 0 || n_fft < 2)
+        return fail(AVSE_ERR_INVALID, "bad istft geometry (need 1 <= n_frames <= stft_frames)");
+    if (n_fft > 2048) return fail(AVSE_ERR_UNSUPPORTED, "n_fft > 2048 not supported");
+    if (n_mels < 1 || n_mels > 80) return fail(AVSE_ERR_UNSUPPORTED, "n_mels must be in [1, 80]");
+    if (frames_per_slice < 0 || (frames_per_slice > 0 && n_frames % frames_per_slice))
+        return fail(AVSE_ERR_INVALID, "n_frames must be a multiple of frames_per_slice");
+    if (n_utt == 0) return 0;
+    AVSE_HIP_CHECK(hipSetDevice(c->device));
+    int rc = ensure_istft_tables(c, sr, n_fft, n_mels, fmin, fmax);
+    if (rc) return rc;
+    const int nb = 1 + n_fft / 2, N = 2 * (nb - 1);
+    const size_t need = sizeof(float) * (size_t)n_utt * n_frames * N;
+    if (need > c->frames_bytes) {
+        (void)hipFree(c->frames);
+        c->frames = nullptr;
+        c->frames_bytes = 0;
+        if (hipMalloc((void**)&c->frames, need) != hipSuccess) return fail(AVSE_ERR_OOM, "hipMalloc failed (istft scratch)");
+        c->frames_bytes = need;
+    }
+    IstftArgs a;
+    a.mel_db = mel_db;
+    a.spf = frames_per_slice;
+    a.n_slices = frames_per_slice > 0 ? n_frames / frames_per_slice : 0;
+    a.stft = reinterpret_cast<const float2*>(stft_ri);
+    a.stft_frames = stft_frames;
+    a.n_utt = n_utt;
+    a.T = n_frames;
+    a.nb = nb;
+    a.N = N;
+    a.hop = hop;
+    a.n_mels = n_mels;
+    a.pinvT = c->istft.pinvT;
+    a.twiddle = c->istft.twiddle;
+    a.window = c->istft.window;
+    a.frames = c->frames;
+    a.sig = sig;
+    return launch_istft(a, (hipStream_t)stream);
 }
 
 int64_t avse_weights_blob_floats(void) { return blob_floats(); }

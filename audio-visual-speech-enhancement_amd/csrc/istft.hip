@@ -1,0 +1,203 @@
+// K6: mel-dB -> amplitude -> pinv(mel) -> x phase -> inverse real FFT -> Hann overlap-add ->
+// window-sum-square normalisation -> centre trim, for gfx950.
+//
+// Replaces reconstruct_signal_from_spectrogram (/root/reference/data_processor.py:99-116):
+//   librosa.db_to_amplitude (:101), np.dot(np.linalg.pinv(mel), .) (:112), librosa.istft (:114),
+// fed by reconstruct_speech_signal (:60-74) with the mixture's complex STFT from K1 (the phase
+// exp(i angle D) = D / |D| is taken in-kernel, so the mixture is not re-analysed).
+//
+// k_istft640 (n_fft 640): one 64-lane block per 3 frames of one utterance.  The 321-bin one-sided
+// spectrum is folded into a 320-point complex sequence (E[k] + i O[k]) and inverted with the same
+// in-register 20 x 16 DFTs as K1 through the conjugation identity IDFT(Z) = conj(DFT(conj Z)) / 320;
+// each lane then writes two windowed output samples per frame.  k_istft_dft handles other sizes
+// (n_fft = 2 (n_bins - 1), e.g. 532 at 29.97 fps) with a direct inverse DFT.  k_ola sums the <= 4
+// overlapping frames of each output sample in increasing frame order (librosa's order), divides by
+// the window sum-square where it exceeds float32 tiny, and drops n_fft/2 samples at both ends.
+#include "avse_common.h"
+#include "fft_common.h"
+
+namespace avse {
+namespace {
+
+constexpr int FPG = 3;
+constexpr int ZS = 340;
+
+__device__ __forceinline__ float mel_at(const IstftArgs& a, long long u, int m, int t) {
+    if (a.spf > 0) {
+        const int sl = t / a.spf;
+        return a.mel_db[((u * a.n_slices + sl) * a.n_mels + m) * (long long)a.spf + (t - sl * a.spf)];
+    }
+    return a.mel_db[(u * a.n_mels + m) * (long long)a.T + t];
+}
+
+__device__ __forceinline__ float2 unit_phase(float2 d) {
+    const float r = sqrtf(d.x * d.x + d.y * d.y);
+    return r > 0.f ? make_float2(d.x / r, d.y / r) : make_float2(1.f, 0.f);
+}
+
+// X[k] = (pinv(mel) @ 10^(dB/20))[k] * D[k]/|D[k]| for one frame, k in [0, nb)
+__device__ __forceinline__ float2 spectrum_bin(const IstftArgs& a, const float* amp, long long u, int k, int t) {
+    float acc = 0.f;
+    for (int m = 0; m < a.n_mels; ++m) acc = fmaf(a.pinvT[m * a.nb + k], amp[m], acc);
+    const float2 d = a.stft[(u * a.nb + k) * (long long)a.stft_frames + t];
+    const float2 ph = unit_phase(d);
+    return make_float2(acc * ph.x, acc * ph.y);
+}
+
+__global__ __launch_bounds__(64) void k_istft640(IstftArgs a) {
+    __shared__ float amp[FPG][80];
+    __shared__ float2 xb[FPG][324];
+    __shared__ float2 zbuf[FPG * ZS];
+    const int lane = threadIdx.x;
+    const long long u = blockIdx.y;
+    const int t0 = blockIdx.x * FPG;
+    const int ng = min(FPG, a.T - t0);
+    const float2* __restrict__ tw = a.twiddle;   // W640^k
+
+    // db_to_amplitude: (10^(0.1 S))^0.5
+    for (int it = lane; it < ng * a.n_mels; it += 64) {
+        const int f = it / a.n_mels, m = it - f * a.n_mels;
+        amp[f][m] = sqrtf(exp10f(0.1f * mel_at(a, u, m, t0 + f)));
+    }
+    __syncthreads();
+    for (int it = lane; it < ng * 321; it += 64) {
+        const int f = it / 321, k = it - f * 321;
+        float2 x = spectrum_bin(a, amp[f], u, k, t0 + f);
+        if (k == 0 || k == 320) x.y = 0.f;            // irfft ignores the DC / Nyquist imaginary parts
+        xb[f][k] = x;
+    }
+    __syncthreads();
+    // fold into Z'[k] = conj(E[k] + i O[k]), k in [0,320):
+    //   E = (X[k] + conj X[320-k]) / 2,  O = (X[k] - conj X[320-k]) W640^{-k} / 2
+    for (int it = lane; it < ng * 320; it += 64) {
+        const int f = it / 320, k = it - f * 320;
+        const float2 xk = xb[f][k], xm = cconj(xb[f][320 - k]);
+        const float2 E = make_float2(0.5f * (xk.x + xm.x), 0.5f * (xk.y + xm.y));
+        const float2 O = cmul(make_float2(0.5f * (xk.x - xm.x), 0.5f * (xk.y - xm.y)), cconj(tw[k]));
+        const float2 Z = make_float2(E.x - O.y, E.y + O.x);   // E + i O
+        zbuf[f * ZS + k] = cconj(Z);
+    }
+    __syncthreads();
+    // forward 320-point DFT of Z' (step 1: 20-point over n2 of z[n1 + 16 n2], lane = (f, n1))
+    {
+        const int f = lane >> 4, n1 = lane & 15;
+        float2 v[20];
+        const bool act = f < ng;
+        if (act) {
+#pragma unroll
+            for (int n2 = 0; n2 < 20; ++n2) v[n2] = zbuf[f * ZS + n1 + 16 * n2];
+        }
+        __syncthreads();
+        if (act) {
+            dft20(v, tw);
+            float2* zf = zbuf + f * ZS;
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+#pragma unroll
+                for (int d = 0; d < 5; ++d) {
+                    const int k2 = c + 4 * d;
+                    float2 y = v[5 * c + d];
+                    if (k2) y = cmul(y, tw[(2 * n1 * k2) % 640]);
+                    zf[k2 * 17 + n1] = y;
+                }
+        }
+    }
+    __syncthreads();
+    // step 2: 16-point DFT over n1, lane = (f, k2); write the time samples
+    {
+        const int f = lane / 20, k2 = lane - 20 * (lane / 20);
+        if (f < ng) {
+            float2 v[16];
+            const float2* zf = zbuf + f * ZS;
+#pragma unroll
+            for (int n1 = 0; n1 < 16; ++n1) v[n1] = zf[k2 * 17 + n1];
+            dft16(v, tw);
+            float* fr = a.frames + ((u * a.T) + t0 + f) * 640LL;
+            const float s = 1.0f / 320.0f;
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    const int n = k2 + 20 * (c + 4 * d);       // z[n] = conj(out[n]) / 320
+                    const float2 o = v[4 * c + d];
+                    fr[2 * n] = o.x * s * a.window[2 * n];
+                    fr[2 * n + 1] = -o.y * s * a.window[2 * n + 1];
+                }
+        }
+    }
+}
+
+// direct inverse real DFT, one 256-thread block per (frame, utterance); N = 2 (nb - 1)
+__global__ __launch_bounds__(256) void k_istft_dft(IstftArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    float* amp = sm;                                        // [n_mels]
+    float2* xs = reinterpret_cast<float2*>(sm + 80);        // [nb]
+    const int t = blockIdx.x;
+    const long long u = blockIdx.y;
+    const int N = a.N, nb = a.nb;
+    for (int m = threadIdx.x; m < a.n_mels; m += 256) amp[m] = sqrtf(exp10f(0.1f * mel_at(a, u, m, t)));
+    __syncthreads();
+    for (int k = threadIdx.x; k < nb; k += 256) xs[k] = spectrum_bin(a, amp, u, k, t);
+    __syncthreads();
+    float* fr = a.frames + ((u * a.T) + t) * (long long)N;
+    for (int n = threadIdx.x; n < N; n += 256) {
+        // x[n] = (1/N) (Re X0 + (-1)^n Re X[N/2] + 2 sum_{k=1}^{N/2-1} Re(X_k e^{+2 pi i k n / N}))
+        float acc = xs[0].x + ((n & 1) ? -xs[nb - 1].x : xs[nb - 1].x);
+        float part = 0.f;
+        int idx = n;
+        for (int k = 1; k < nb - 1; ++k) {
+            const float2 w = a.twiddle[idx];                // e^{-2 pi i idx / N}; conj for the inverse
+            part = fmaf(xs[k].x, w.x, part);
+            part = fmaf(xs[k].y, w.y, part);                // Re(X (cos + i sin)) = Xr cos - Xi sin, sin = -w.y
+            idx += n;
+            if (idx >= N) idx -= N;
+        }
+        fr[n] = (acc + 2.f * part) / (float)N * a.window[n];
+    }
+}
+
+// overlap-add + window-sum-square normalisation + centre trim
+__global__ void k_ola(IstftArgs a) {
+    const long long L = (long long)a.hop * (a.T - 1);
+    const long long total = L * a.n_utt;
+    const int N = a.N;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+        const long long u = i / L;
+        const long long p = i - u * L + N / 2;            // position in the untrimmed signal
+        // frames t with t*hop <= p <= t*hop + N - 1
+        const long long tlo = (p - N + 1 <= 0) ? 0 : (p - N + 1 + a.hop - 1) / a.hop;
+        const long long thi = min((long long)a.T - 1, p / a.hop);
+        float y = 0.f, wss = 0.f;
+        for (long long t = tlo; t <= thi; ++t) {
+            const int o = (int)(p - t * a.hop);
+            y += a.frames[(u * a.T + t) * (long long)N + o];
+            const float w = a.window[o];
+            wss += w * w;
+        }
+        if (wss > 1.17549435e-38f) y /= wss;
+        a.sig[i] = y;
+    }
+}
+
+}  // namespace
+
+int launch_istft(const IstftArgs& a, hipStream_t s) {
+    if (a.n_utt <= 0 || a.T <= 0) return 0;
+    if (a.N == 640) {
+        hipLaunchKernelGGL(k_istft640, dim3((a.T + FPG - 1) / FPG, (unsigned)a.n_utt), dim3(64), 0, s, a);
+    } else {
+        const size_t shm = sizeof(float) * 80 + sizeof(float2) * a.nb;
+        hipLaunchKernelGGL(k_istft_dft, dim3(a.T, (unsigned)a.n_utt), dim3(256), shm, s, a);
+    }
+    AVSE_HIP_CHECK(hipGetLastError());
+    if (a.T > 1) {
+        const long long total = (long long)a.hop * (a.T - 1) * a.n_utt;
+        long long g = (total + 255) / 256;
+        if (g > 8192) g = 8192;
+        hipLaunchKernelGGL(k_ola, dim3((unsigned)(g < 1 ? 1 : g)), dim3(256), 0, s, a);
+        AVSE_HIP_CHECK(hipGetLastError());
+    }
+    return 0;
+}
+
+}  // namespace avse

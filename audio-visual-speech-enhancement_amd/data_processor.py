@@ -73,8 +73,31 @@ def preprocess_audio_batch(signals, sample_rate, slice_duration_ms, n_video_slic
 
 
 def reconstruct_speech_signal(mixed_signal, speech_spectrograms, video_frame_rate):
-    """data_processor.py:60-74 (needs the K6 ISTFT kernel)."""
-    raise NotImplementedError("reconstruct_speech_signal: the ISTFT kernel (K6) is not built yet")
+    """data_processor.py:60-74: phase of the mixture's STFT + predicted speech mel-dB slices
+    [n_slices, 80, spf] -> AudioSignal (K1 for the phase, K6 for the inverse)."""
+    sr = mixed_signal.get_sample_rate()
+    n_fft = int(float(sr) / video_frame_rate)
+    hop_length = int(n_fft / 4)
+    sig = ops.to_device(np.asarray(_channel0(mixed_signal))[None, :])
+    _, D = ops.spectrogram(sig, sample_rate=sr, n_fft=n_fft, hop_length=hop_length, n_mels=N_MELS, fmin=MEL_FMIN,
+                           fmax=MEL_FMAX, return_stft=True)
+    spec = ops.to_device(speech_spectrograms, sig.device)
+    if spec.dim() == 2:                      # predict() squeezes a single slice to [80, spf]
+        spec = spec[None]
+    y = ops.istft(spec[None].contiguous(), D, sample_rate=sr, n_fft=n_fft, hop_length=hop_length, n_mels=N_MELS,
+                  fmin=MEL_FMIN, fmax=MEL_FMAX)
+    return AudioSignal(y[0].cpu().numpy(), sr)
+
+
+def reconstruct_signal_from_spectrogram(magnitude, phase, sample_rate, n_fft, hop_length, mel=True, db=True):
+    """data_processor.py:99-116 for mel-dB `magnitude` [80, T] and unit `phase` [n_fft//2+1, T]."""
+    if not (mel and db):
+        raise NotImplementedError("the reference calls it with mel=True, db=True only (data_processor.py:72-74)")
+    m = ops.to_device(magnitude)[None].contiguous()
+    ph = torch.from_numpy(np.ascontiguousarray(phase, dtype=np.complex64)).to(m.device)[None]
+    y = ops.istft(m, ph, sample_rate=sample_rate, n_fft=n_fft, hop_length=hop_length, n_mels=N_MELS, fmin=MEL_FMIN,
+                  fmax=MEL_FMAX)
+    return AudioSignal(y[0].cpu().numpy(), sample_rate)
 
 
 class VideoNormalizer(object):

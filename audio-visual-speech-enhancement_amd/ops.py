@@ -61,6 +61,43 @@ def spectrogram(sig, sample_rate=16000, n_fft=640, hop_length=160, n_mels=80, fm
     return out
 
 
+def istft(mel_db, stft, sample_rate=16000, n_fft=640, hop_length=160, n_mels=80, fmin=0.0, fmax=8000.0,
+          n_frames=None):
+    """K6: speech mel-dB + mixture STFT -> time signal (reconstruct_signal_from_spectrogram).
+
+    mel_db: [U, n_slices, n_mels, spf] (network output of consecutive slices) or [U, n_mels, T];
+    stft: complex64 [U, n_fft//2+1, T_stft] (or its float32 [..., 2] view) from spectrogram(return_stft=True).
+    Uses the first n_frames = min(T_pred, T_stft) frames (data_processor.py:68-70).
+    Returns [U, hop * (n_frames - 1)] float32."""
+    _dev_f32(mel_db, "mel_db")
+    if stft.dtype == torch.complex64:
+        stft = torch.view_as_real(stft)
+    _dev_f32(stft, "stft")
+    if mel_db.dim() == 4:
+        U, ns, nm, spf = mel_db.shape
+        T_pred = ns * spf
+    else:
+        U, nm, T_pred = mel_db.shape
+        spf = 0
+    if nm != n_mels or stft.shape[0] != U or stft.shape[1] != n_fft // 2 + 1:
+        raise ValueError("mel_db / stft shapes do not match")
+    T_stft = stft.shape[2]
+    T = min(T_pred, T_stft) if n_frames is None else n_frames
+    if T != T_pred:
+        # min() cut the prediction: use the [U, n_mels, T] layout of the concatenated, trimmed slices
+        if spf:
+            mel_db = mel_db.permute(0, 2, 1, 3).reshape(U, nm, T_pred)
+        mel_db = mel_db[:, :, :T].contiguous()
+        spf = 0
+    out = torch.empty((U, hop_length * (T - 1)), dtype=torch.float32, device=mel_db.device)
+    ctx = _lib.context(mel_db.device)
+    with torch.cuda.device(mel_db.device):
+        _lib.check(_lib.load().avse_istft(ctx.handle, _lib.ptr(mel_db), _lib.ptr(stft), U, int(T), int(T_stft), int(spf),
+                                          int(sample_rate), int(n_fft), int(hop_length), int(n_mels), float(fmin),
+                                          float(fmax), _lib.ptr(out), _lib.stream_handle(mel_db.device)), "avse_istft")
+    return out
+
+
 class DeviceWeights:
     """avse_weights: BN-folded, GEMM-packed weights resident on one device."""
 

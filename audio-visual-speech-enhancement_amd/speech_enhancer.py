@@ -1,0 +1,275 @@
+"""preprocess / train / predict CLI with the flags of /root/reference/speech_enhancer.py:265-293.
+
+    python -m avse_amd.speech_enhancer -bd BASE preprocess -dn NAME -ds DATASET -n NOISE_DIR [-s SPK ...]
+    python -m avse_amd.speech_enhancer -bd BASE train -mn MODEL -tdn NAME ... -vdn NAME ... --init-only
+    python -m avse_amd.speech_enhancer -bd BASE predict -mn MODEL -dn NAME [-g GPUS]
+
+Same cache / output layout as the reference (AssetManager :91-142, PredictionStorage :145-184).
+Differences (host plumbing outside the hot path):
+  * video: the reference decodes with ffmpeg and crops the mouth with dlib (data_processor.py:12-32);
+    this build reads pre-cropped mouth stacks <name>.npy [frames, 128, 128] (25 fps unless a
+    <name>.fps text file says otherwise);
+  * train: fitting (network.py:177-206) is out of scope; `--init-only` writes the files the reference's
+    train produces (model.h5py from a Keras-default initialisation, normalization.pkl fitted on the
+    training video) so that predict runs end to end;
+  * the enhanced/mixture .mp4 muxing (mediaio.ffmpeg.merge) runs only when ffmpeg is installed.
+All spectrogram / network / reconstruction arithmetic goes through libavse (K1, forward, K6).
+"""
+import argparse
+import logging
+import os
+import pickle
+import random
+import shutil
+import subprocess
+from collections import namedtuple
+from datetime import datetime
+from shutil import copy2
+
+import numpy as np
+
+from . import data_processor
+from .audio_io import AudioMixer, AudioSignal
+from .dataset import AudioDataset, AudioVisualDataset
+from .network import SpeechEnhancementNetwork
+
+Sample = namedtuple("Sample", ["speaker_id", "video_file_path", "speech_file_path", "noise_file_path", "video_samples",
+                               "mixed_spectrograms", "speech_spectrograms", "noise_spectrograms", "mixed_signal",
+                               "video_frame_rate"])
+
+
+# ------------------------------------------------------------------------ preprocessing (host side)
+def preprocess_video_sample(video_file_path, slice_duration_ms, mouth_height=128, mouth_width=128):
+    """Stand-in for data_processor.py:12-32 on pre-cropped mouth stacks -> ([S, H, W, frames], fps)."""
+    frames = np.load(video_file_path, allow_pickle=False).astype(np.float32)       # [F, H, W]
+    if frames.shape[1:] != (mouth_height, mouth_width):
+        raise ValueError(f"{video_file_path}: expected [F, {mouth_height}, {mouth_width}] mouth crops")
+    fps_path = os.path.splitext(video_file_path)[0] + ".fps"
+    fps = float(open(fps_path).read()) if os.path.exists(fps_path) else 25.0
+    fps_slice = int((float(slice_duration_ms) / 1000) * fps)
+    n_slices = int(float(frames.shape[0]) / fps_slice)
+    crops = np.transpose(frames, (1, 2, 0))
+    slices = [crops[:, :, i * fps_slice:(i + 1) * fps_slice] for i in range(n_slices)]
+    return np.stack(slices), fps
+
+
+def preprocess_audio_pair(speech_file_path, noise_file_path, slice_duration_ms, n_video_slices, video_frame_rate):
+    """data_processor.py:119-139: tile + truncate the noise, 0 dB SNR, mix [1, 1], three spectrograms."""
+    speech_signal = AudioSignal.from_wav_file(speech_file_path)
+    noise_signal = AudioSignal.from_wav_file(noise_file_path)
+    while noise_signal.get_number_of_samples() < speech_signal.get_number_of_samples():
+        noise_signal = AudioSignal.concat([noise_signal, noise_signal])
+    noise_signal.truncate(speech_signal.get_number_of_samples())
+    factor = AudioMixer.snr_factor(speech_signal, noise_signal, snr_db=0)
+    noise_signal.amplify_by_factor(factor)
+    mixed_signal = AudioMixer.mix([speech_signal, noise_signal], mixing_weights=[1, 1])
+    mixed = data_processor.preprocess_audio_signal(mixed_signal, slice_duration_ms, n_video_slices, video_frame_rate)
+    speech = data_processor.preprocess_audio_signal(speech_signal, slice_duration_ms, n_video_slices, video_frame_rate)
+    noise = data_processor.preprocess_audio_signal(noise_signal, slice_duration_ms, n_video_slices, video_frame_rate)
+    return mixed, speech, noise, mixed_signal
+
+
+def preprocess_sample(speech_entry, noise_file_path, slice_duration_ms=200):
+    """data_processor.py:156-177."""
+    video_samples, fps = preprocess_video_sample(speech_entry.video_path, slice_duration_ms)
+    mixed, speech, noise, mixed_signal = preprocess_audio_pair(speech_entry.audio_path, noise_file_path,
+                                                               slice_duration_ms, video_samples.shape[0], fps)
+    n = min(video_samples.shape[0], mixed.shape[0])
+    return Sample(speech_entry.speaker_id, speech_entry.video_path, speech_entry.audio_path, noise_file_path,
+                  video_samples[:n], mixed[:n], speech[:n], noise[:n], mixed_signal, fps)
+
+
+def preprocess_data(speech_entries, noise_file_paths):
+    """data_processor.py:180-198 (catch-and-skip per sample; the GPU does the spectrograms, so no Pool)."""
+    samples = []
+    for entry, noise in zip(speech_entries, noise_file_paths):
+        try:
+            samples.append(preprocess_sample(entry, noise))
+        except Exception as e:  # noqa: BLE001 — mirrors try_preprocess_sample
+            print("failed to preprocess %s (%s)" % ((entry, noise), e))
+    return samples
+
+
+# ------------------------------------------------------------------------ asset layout
+class AssetManager:
+    def __init__(self, base_dir):
+        self.__base_dir = base_dir
+        self.__cache_dir = os.path.join(base_dir, "cache")
+        self.__preprocessed_dir = os.path.join(self.__cache_dir, "preprocessed")
+        self.__models_dir = os.path.join(self.__cache_dir, "models")
+        self.__out_dir = os.path.join(base_dir, "out")
+        for d in (self.__cache_dir, self.__preprocessed_dir, self.__models_dir, self.__out_dir):
+            os.makedirs(d, exist_ok=True)
+
+    def get_preprocessed_blob_path(self, data_name):
+        return os.path.join(self.__preprocessed_dir, data_name + ".pkl")
+
+    def create_model(self, model_name):
+        os.makedirs(os.path.join(self.__models_dir, model_name), exist_ok=True)
+
+    def get_model_cache_path(self, model_name):
+        return os.path.join(self.__models_dir, model_name, "model.h5py")
+
+    def get_normalization_cache_path(self, model_name):
+        return os.path.join(self.__models_dir, model_name, "normalization.pkl")
+
+    def create_prediction_storage(self, model_name, data_name):
+        d = os.path.join(self.__out_dir, model_name, data_name)
+        os.makedirs(d, exist_ok=True)
+        return d
+
+
+class PredictionStorage(object):
+    def __init__(self, storage_dir):
+        self.__base_dir = os.path.join(storage_dir, "{:%Y-%m-%d_%H-%M-%S}".format(datetime.now()))
+        os.makedirs(self.__base_dir)
+
+    def save_prediction(self, sample, predicted_speech_signal):
+        speaker_dir = os.path.join(self.__base_dir, sample.speaker_id)
+        os.makedirs(speaker_dir, exist_ok=True)
+        speech_name = os.path.splitext(os.path.basename(sample.video_file_path))[0]
+        noise_name = os.path.splitext(os.path.basename(sample.noise_file_path))[0]
+        d = os.path.join(speaker_dir, speech_name + "_" + noise_name)
+        os.mkdir(d)
+        copy2(sample.speech_file_path, os.path.join(d, "source.wav"))
+        copy2(sample.noise_file_path, os.path.join(d, "noise.wav"))
+        sample.mixed_signal.save_to_wav_file(os.path.join(d, "mixture.wav"))
+        predicted_speech_signal.save_to_wav_file(os.path.join(d, "enhanced.wav"))
+        if shutil.which("ffmpeg") and not sample.video_file_path.endswith(".npy"):
+            ext = os.path.splitext(sample.video_file_path)[1]
+            for name in ("mixture", "enhanced"):
+                subprocess.run(["ffmpeg", "-y", "-loglevel", "error", "-i", sample.video_file_path, "-i",
+                                os.path.join(d, name + ".wav"), "-c:v", "copy", "-map", "0:v:0", "-map", "1:a:0",
+                                os.path.join(d, name + ext)], check=False)
+        return d
+
+
+# ------------------------------------------------------------------------ listing
+def list_speakers(args):
+    speaker_ids = AudioVisualDataset(args.dataset_dir).list_speakers() if args.speakers is None else list(args.speakers)
+    if args.ignored_speakers is not None:
+        for speaker_id in args.ignored_speakers:
+            speaker_ids.remove(speaker_id)
+    return speaker_ids
+
+
+def list_data(dataset_dir, speaker_ids, noise_dirs, max_files=None, shuffle=True, augmentation_factor=1):
+    """speech_enhancer.py:201-220 (speech/noise zipped and truncated to the shorter list)."""
+    speech_subset = AudioVisualDataset(dataset_dir).subset(speaker_ids, max_files, shuffle)
+    noise_file_paths = AudioDataset(noise_dirs).subset(max_files, shuffle)
+    n_files = min(len(speech_subset), len(noise_file_paths))
+    speech_entries = speech_subset[:n_files]
+    noise_file_paths = noise_file_paths[:n_files]
+    all_speech, all_noise = list(speech_entries), list(noise_file_paths)
+    for _ in range(augmentation_factor - 1):
+        all_speech += speech_entries
+        all_noise += random.sample(noise_file_paths, len(noise_file_paths))
+    return all_speech, all_noise
+
+
+def load_preprocessed_blob(path):
+    print("loading preprocessed samples from %s" % path)
+    with open(path, "rb") as fd:   # a file this CLI's preprocess wrote
+        return pickle.load(fd)
+
+
+def load_preprocessed_blobs(paths, max_samples_per_blob=None):
+    out = []
+    for p in paths:
+        out += load_preprocessed_blob(p)[:max_samples_per_blob]
+    return out
+
+
+def make_sample_set(samples, max_samples=None):
+    n = len(samples) if max_samples is None else min(len(samples), max_samples)
+    samples = random.sample(samples, n)
+    video = np.concatenate([s.video_samples for s in samples], axis=0)
+    mixed = np.concatenate([s.mixed_spectrograms for s in samples], axis=0)
+    speech = np.concatenate([s.speech_spectrograms for s in samples], axis=0)
+    perm = np.random.permutation(video.shape[0])
+    return video[perm], mixed[perm], speech[perm]
+
+
+# ------------------------------------------------------------------------ subcommands
+def preprocess(args):
+    assets = AssetManager(args.base_dir)
+    speaker_ids = list_speakers(args)
+    speech_entries, noise_file_paths = list_data(args.dataset_dir, speaker_ids, args.noise_dirs, max_files=1000,
+                                                 shuffle=True, augmentation_factor=1)
+    samples = preprocess_data(speech_entries, noise_file_paths)
+    with open(assets.get_preprocessed_blob_path(args.data_name), "wb") as fd:
+        pickle.dump(samples, fd)
+    print("preprocessed %d samples" % len(samples))
+
+
+def train(args):
+    if not args.init_only:
+        raise NotImplementedError("training (network.py:177-206) is outside this build's hot path; "
+                                  "use --init-only to write an initialised model + normalizer")
+    assets = AssetManager(args.base_dir)
+    assets.create_model(args.model)
+    samples = load_preprocessed_blobs([assets.get_preprocessed_blob_path(d) for d in args.train_data_names])
+    video, mixed, _ = make_sample_set(samples)
+    normalizer = data_processor.VideoNormalizer(video)
+    with open(assets.get_normalization_cache_path(args.model), "wb") as fd:
+        pickle.dump(normalizer, fd)
+    network = SpeechEnhancementNetwork.build(mixed.shape[1:], video.shape[1:], seed=args.seed)
+    network.save(assets.get_model_cache_path(args.model))
+
+
+def predict(args):
+    assets = AssetManager(args.base_dir)
+    storage = PredictionStorage(assets.create_prediction_storage(args.model, args.data_name))
+    network = SpeechEnhancementNetwork.load(assets.get_model_cache_path(args.model), compute_dtype=args.dtype)
+    with open(assets.get_normalization_cache_path(args.model), "rb") as fd:   # written by this CLI's train
+        video_normalizer = pickle.load(fd)
+    samples = load_preprocessed_blob(assets.get_preprocessed_blob_path(args.data_name))
+    for sample in samples:
+        try:
+            print("predicting (%s, %s)..." % (sample.video_file_path, sample.noise_file_path))
+            # normalize + evaluate + predict, with the normaliser fused into the first video conv
+            loss = network.evaluate(sample.mixed_spectrograms, sample.video_samples, sample.speech_spectrograms,
+                                    video_normalizer=video_normalizer)
+            print("loss: %f" % loss)
+            pred = network.predict(sample.mixed_spectrograms, sample.video_samples, video_normalizer=video_normalizer)
+            signal = data_processor.reconstruct_speech_signal(sample.mixed_signal, pred, sample.video_frame_rate)
+            storage.save_prediction(sample, signal)
+        except Exception:  # noqa: BLE001 — mirrors speech_enhancer.py:87-88
+            logging.exception("failed to predict %s. skipping" % sample.video_file_path)
+
+
+def main(argv=None):
+    parser = argparse.ArgumentParser(add_help=False)
+    parser.add_argument("-bd", "--base_dir", type=str, required=True)
+    sub = parser.add_subparsers()
+
+    p = sub.add_parser("preprocess")
+    p.add_argument("-dn", "--data_name", type=str, required=True)
+    p.add_argument("-ds", "--dataset_dir", type=str, required=True)
+    p.add_argument("-n", "--noise_dirs", nargs="+", type=str, required=True)
+    p.add_argument("-s", "--speakers", nargs="+", type=str)
+    p.add_argument("-is", "--ignored_speakers", nargs="+", type=str)
+    p.set_defaults(func=preprocess)
+
+    t = sub.add_parser("train")
+    t.add_argument("-mn", "--model", type=str, required=True)
+    t.add_argument("-tdn", "--train_data_names", nargs="+", type=str, required=True)
+    t.add_argument("-vdn", "--validation_data_names", nargs="+", type=str, required=True)
+    t.add_argument("-g", "--gpus", type=int, default=1)
+    t.add_argument("--init-only", action="store_true")
+    t.add_argument("--seed", type=int, default=0)
+    t.set_defaults(func=train)
+
+    q = sub.add_parser("predict")
+    q.add_argument("-mn", "--model", type=str, required=True)
+    q.add_argument("-dn", "--data_name", type=str, required=True)
+    q.add_argument("-g", "--gpus", type=int, default=1)
+    q.add_argument("--dtype", default="float32", choices=["float32", "bfloat16"])
+    q.set_defaults(func=predict)
+
+    args = parser.parse_args(argv)
+    args.func(args)
+
+
+if __name__ == "__main__":
+    main()

@@ -81,6 +81,21 @@ int avse_spectrogram(avse_ctx* ctx, const float* sig, int64_t n_utt, int64_t n_s
                      float amin, float top_db, int pad_mode, int frames_per_slice,
                      float* mel_db, float* stft_ri, void* stream);
 
+/* Replaces reconstruct_signal_from_spectrogram (data_processor.py:99-116) as called by
+ * reconstruct_speech_signal (:60-74): db_to_amplitude (:101) -> np.dot(pinv(mel), .) (:112) ->
+ * x exp(i angle D) of the mixture STFT -> librosa.istft(hop_length=hop) (:114: periodic Hann,
+ * window-sum-square normalisation, n_fft/2 trimmed at both ends).
+ *   mel_db   frames_per_slice > 0: [n_utt][n_frames/frames_per_slice][n_mels][frames_per_slice]
+ *            (the network's [N][80][20] output of consecutive slices = np.concatenate(..., axis=1))
+ *            frames_per_slice == 0: [n_utt][n_mels][n_frames]
+ *   stft_ri  [n_utt][n_fft/2+1][stft_frames][2] complex STFT of the mixture (avse_spectrogram's
+ *            stft_ri output); the first n_frames frames are used (min(T_pred, T_phase), :68-70)
+ *   sig      [n_utt][hop * (n_frames - 1)]
+ * n_fft is the ANALYSIS size (int(sr / fps)); the inverse size is 2 * (n_fft/2), like librosa. */
+int avse_istft(avse_ctx* ctx, const float* mel_db, const float* stft_ri, int64_t n_utt, int n_frames,
+               int stft_frames, int frames_per_slice, int sr, int n_fft, int hop, int n_mels,
+               float fmin, float fmax, float* sig, void* stream);
+
 /* ---- network --------------------------------------------------------------------------- */
 
 /* Number of float32 values in a canonical weight blob (see avse_weights_load). */

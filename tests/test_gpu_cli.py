@@ -1,0 +1,58 @@
+"""Config 1 (BASELINE.json configs[0]): preprocess -> train --init-only -> predict through the CLI on a
+synthetic 2-speaker x 2-clip dataset with one noise file (list_data zips to min(4, 1) = 1 sample,
+speech_enhancer.py:208)."""
+import glob
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def make_dataset(tmp):
+    from scipy.io import wavfile
+    rng = np.random.default_rng(0)
+    ds = os.path.join(tmp, "dataset")
+    for spk in ("s1", "s2"):
+        os.makedirs(os.path.join(ds, spk, "audio"))
+        os.makedirs(os.path.join(ds, spk, "video"))
+        for clip in ("a", "b"):
+            t = np.arange(48000) / 16000
+            speech = (3000 * np.sin(2 * np.pi * rng.uniform(150, 300) * t) * (1 + np.sin(2 * np.pi * 3 * t)))
+            wavfile.write(os.path.join(ds, spk, "audio", clip + ".wav"), 16000, speech.astype(np.int16))
+            np.save(os.path.join(ds, spk, "video", clip + ".npy"), rng.integers(0, 256, (75, 128, 128), dtype=np.uint8))
+    noise = os.path.join(tmp, "noise")
+    os.makedirs(noise)
+    wavfile.write(os.path.join(noise, "n.wav"), 16000, rng.normal(0, 2000, 20000).astype(np.int16))
+    return ds, noise
+
+
+def run(args, cwd):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "speech_enhancer.py")] + args, cwd=cwd,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return r.stdout
+
+
+def test_cli_preprocess_train_predict(gpu, tmp_path):
+    tmp = str(tmp_path)
+    ds, noise = make_dataset(tmp)
+    base = os.path.join(tmp, "base")
+    os.makedirs(base)
+    out = run(["-bd", base, "preprocess", "-dn", "d", "-ds", ds, "-n", noise], tmp)
+    assert "preprocessed 1 samples" in out
+    run(["-bd", base, "train", "-mn", "m", "-tdn", "d", "-vdn", "d", "--init-only"], tmp)
+    assert os.path.exists(os.path.join(base, "cache", "models", "m", "model.h5py"))
+    out = run(["-bd", base, "predict", "-mn", "m", "-dn", "d"], tmp)
+    assert "loss:" in out
+    enhanced = glob.glob(os.path.join(base, "out", "m", "d", "*", "*", "*", "enhanced.wav"))
+    assert len(enhanced) == 1
+    from scipy.io import wavfile
+    sr, y = wavfile.read(enhanced[0])
+    assert sr == 16000 and y.shape == (160 * (300 - 1),)
+    for f in ("mixture.wav", "source.wav", "noise.wav"):
+        assert os.path.exists(os.path.join(os.path.dirname(enhanced[0]), f))

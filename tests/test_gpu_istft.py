@@ -1,0 +1,64 @@
+"""K6 parity: libavse ISTFT reconstruction vs the numpy librosa restatement.
+
+Tolerance (DESIGN.md "Parity"): the reconstructed waveform within relative RMS 1e-4 of the float64
+oracle (fp32 exp10 / pinv dot / inverse FFT / overlap-add); output length exact.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import synth_audio
+from oracle import librosa_ref as R
+
+pytestmark = pytest.mark.gpu
+
+
+def rel_rms(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.sqrt(np.mean((a - b) ** 2)) / np.sqrt(np.mean(b ** 2)))
+
+
+@pytest.mark.parametrize("n_samples,fps,n_slices", [(48000, 25.0, 15), (47000, 25.0, 15), (32000, 29.97, 10)])
+def test_reconstruct_speech_signal_matches_oracle(gpu, n_samples, fps, n_slices):
+    from avse_amd import data_processor as dp
+    from avse_amd.audio_io import AudioSignal
+    rng = np.random.default_rng(7)
+    x = synth_audio(rng, 1, n_samples)[0]
+    sig = AudioSignal(x.copy(), 16000)
+    slices = dp.preprocess_audio_signal(sig, 200, n_slices, fps)            # pads/truncates sig in place
+    # a "prediction": the speech slices perturbed a little (as a network output would be)
+    pred = (slices + rng.normal(0, 1.0, slices.shape)).astype(np.float32)
+    got = dp.reconstruct_speech_signal(sig, pred, fps).get_data(0)
+    ref = R.reconstruct_speech_signal(sig.get_data(0), 16000, pred, fps)
+    assert got.shape == ref.shape
+    g = R.frame_geometry(16000, 200, n_slices, fps)
+    assert got.shape[0] == g["hop_length"] * (n_slices * g["spectrogram_samples_per_slice"] - 1)
+    assert rel_rms(got, ref) < 1e-4, rel_rms(got, ref)
+
+
+def test_batched_istft_matches_oracle(gpu):
+    from avse_amd import ops
+    rng = np.random.default_rng(3)
+    x = synth_audio(rng, 5, 48000)
+    xt = torch.from_numpy(x).to(gpu)
+    mel, D = ops.spectrogram(xt, frames_per_slice=20, return_stft=True)     # [5, 15, 80, 20], [5, 321, 301]
+    y = ops.istft(mel, D).cpu().numpy()
+    assert y.shape == (5, 47840)
+    for u in range(5):
+        sl = R.preprocess_audio_signal(x[u], 16000, 200, 15, 25.0)
+        ref = R.reconstruct_speech_signal(x[u], 16000, sl, 25.0)
+        assert rel_rms(y[u], ref) < 1e-4, (u, rel_rms(y[u], ref))
+
+
+def test_reconstruct_signal_from_spectrogram_api(gpu):
+    from avse_amd import data_processor as dp
+    from avse_amd.audio_io import AudioSignal
+    rng = np.random.default_rng(4)
+    x = synth_audio(rng, 1, 16000)[0]
+    mel, phase = dp.signal_to_spectrogram(AudioSignal(x, 16000), 640, 160)
+    got = dp.reconstruct_signal_from_spectrogram(mel, phase, 16000, 640, 160).get_data(0)
+    mref, pref = R.signal_to_spectrogram(x, 16000, 640, 160)
+    ref = R.reconstruct_signal_from_spectrogram(mref, pref, 16000, 640, 160)
+    assert got.shape == ref.shape == (16000,)
+    assert rel_rms(got, ref) < 1e-4, rel_rms(got, ref)
