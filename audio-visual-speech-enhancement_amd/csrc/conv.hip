@@ -39,10 +39,18 @@ template <> __device__ __forceinline__ bf16_t from_f<bf16_t>(float v) { return (
 template <> __device__ __forceinline__ float from_f<float>(float v) { return v; }
 
 struct RowInfo {
-    const char* base;   // clip base pointer (bytes)
+    int cbase;          // byte offset of the row's clip from the block's first clip
     int iy0, ix0;       // yq*sy, xq*sx
     bool valid;
 };
+
+// Buffer-resource loads: out-of-range offsets return zeros in hardware, so padding / ragged tiles
+// need no branch around the load (a "load or zero" branch makes hipcc drain vmcnt per load).
+constexpr int kOOB = 0x7fffff00;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, long long bytes) {
+    const int nrec = bytes > kOOB ? kOOB : (bytes < 0 ? 0 : (int)bytes);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, nrec, 0x00020000);
+}
 
 template <typename T, int BN>
 __global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
@@ -76,13 +84,17 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
 
     // ---- per-thread A rows (2 chunks: rows r and r + 64, same chunk column g) ----
     const int g = tid & 3;
+    const int clip_first = a.pool ? (m0 >> 2) / ((a.Hq >> 1) * (a.Wq >> 1)) : m0 / (a.Hq * a.Wq);
+    const long long clip_bytes = a.in_clip_stride * (long long)sizeof(T);
+    const __amdgpu_buffer_rsrc_t rsA = make_rsrc(reinterpret_cast<const char*>(a.in) + clip_first * clip_bytes,
+                                                 (a.N - clip_first) * clip_bytes);
     RowInfo ri[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         const int row = (tid >> 2) + 64 * h;
         const int m = m0 + row;
         ri[h].valid = m < M;
-        const int mm = ri[h].valid ? m : 0;
+        const int mm = ri[h].valid ? m : m0;
         int clip, yq, xq;
         if (a.pool) {
             const int p = mm >> 2, q = mm & 3;
@@ -97,7 +109,7 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
             yq = r / a.Wq;
             xq = r % a.Wq;
         }
-        ri[h].base = reinterpret_cast<const char*>(a.in) + (long long)clip * a.in_clip_stride * sizeof(T);
+        ri[h].cbase = (int)((clip - clip_first) * clip_bytes);
         ri[h].iy0 = yq * a.sy;
         ri[h].ix0 = xq * a.sx;
     }
@@ -105,32 +117,29 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
     int kj = (s_begin * SLAB + g * CH) / a.Ci;
     int kc = s_begin * SLAB + g * CH - kj * a.Ci;
 
-    const char* wbase = reinterpret_cast<const char*>(a.w) + ph.w_off * sizeof(T);
+    const __amdgpu_buffer_rsrc_t rsB = make_rsrc(reinterpret_cast<const char*>(a.w) + ph.w_off * sizeof(T),
+                                                 (long long)a.Co * ph.kpad * sizeof(T));
 
     i32x4 ra[2], rb[BCH];
     auto load_slab = [&](int s) {
         // A
-        int2 t = (kj < ph.ntaps) ? taps[kj] : make_int2(0, 0);
+        const bool tap_ok = kj < ph.ntaps;
+        const int2 t = taps[tap_ok ? kj : ph.ntaps - 1];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            i32x4 v = {0, 0, 0, 0};
-            if (ri[h].valid && kj < ph.ntaps) {
-                const int iy = ri[h].iy0 + t.x, ix = ri[h].ix0 + t.y;
-                if (iy >= 0 && iy < a.Hi && ix >= 0 && ix < a.Wi)
-                    v = *reinterpret_cast<const i32x4*>(ri[h].base + ((long long)(iy * a.Wi + ix) * a.Ci + kc) * sizeof(T));
-            }
-            ra[h] = v;
+            const int iy = ri[h].iy0 + t.x, ix = ri[h].ix0 + t.y;
+            const bool ok = ri[h].valid && tap_ok && iy >= 0 && iy < a.Hi && ix >= 0 && ix < a.Wi;
+            const int off = ok ? ri[h].cbase + ((iy * a.Wi + ix) * a.Ci + kc) * (int)sizeof(T) : kOOB;
+            ra[h] = __builtin_amdgcn_raw_buffer_load_b128(rsA, off, 0, 0);
         }
-        // B
+        // B (rows past Cout read zeros)
 #pragma unroll
         for (int h = 0; h < BCH; ++h) {
             const int c = tid + 256 * h;
             const int row = c >> 2, gg = c & 3;
             const int n = n0 + row;
-            i32x4 v = {0, 0, 0, 0};
-            if (n < a.Co)
-                v = *reinterpret_cast<const i32x4*>(wbase + ((long long)n * ph.kpad + s * SLAB + gg * CH) * sizeof(T));
-            rb[h] = v;
+            const int off = n < a.Co ? (n * ph.kpad + s * SLAB + gg * CH) * (int)sizeof(T) : kOOB;
+            rb[h] = __builtin_amdgcn_raw_buffer_load_b128(rsB, off, 0, 0);
         }
         // advance the A chunk position by one slab
         kc += SLAB;
