@@ -122,7 +122,7 @@ constexpr int HALO_NT = 2;
 // K-slices per 128-channel group: 4 x taps (V1: ceil(taps/4)), taps padded to a multiple of HALO_NT.
 __host__ __device__ constexpr int halo_slices_per_group(int ks, bool v1) {
     return v1 ? (((ks * ks + 3) / 4 + HALO_NT - 1) / HALO_NT) * HALO_NT
-              : 4 * (((ks * ks + HALO_NT - 1) / HALO_NT) * HALO_NT);
+              : 4 * ks * ks;   // (4 chunks of 32 channels) x taps; a multiple of HALO_NT for ks = 3, 5
 }
 
 struct HaloArgs {
@@ -142,6 +142,7 @@ struct HaloArgs {
 };
 
 int launch_conv_halo(const HaloArgs& a, hipStream_t s);
+int launch_conv_stream(const HaloArgs& a, hipStream_t s);   // conv_stream.hip (non-V1 variants)
 int launch_video_prep(const float* video, const float* mean, const float* stdv, void* out, int64_t N,
                       int dtype, hipStream_t s);
 int launch_audio_prep(const float* audio, void* out, int64_t N, int dtype, hipStream_t s);

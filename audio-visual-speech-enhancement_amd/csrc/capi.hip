@@ -476,7 +476,7 @@ int build_layer(avse_weights* W, const LayerDef& L, const float* kernel, const f
     if ((rc = upload(W, shift, &G.shift))) return rc;
     if ((rc = upload(W, taps, &G.taps))) return rc;
 
-    // halo-tiled packing for the bf16 video convs: [step][Cout][32], step = (cg*4 + cc)*KS^2 + tap
+    // halo-tiled packing for the bf16 video convs: [slice][Cout][32], slice = (cg*4 + cc)*KS^2 + tap
     // (V1: step = group of 4 taps, 8 channels each, channels 5..7 and taps >= 25 zero)
     const char* no_halo = std::getenv("AVSE_NO_HALO");   // A/B switch: force the generic kernel
     if (W->dtype == AVSE_BF16 && L.kind == CONV && L.pool && L.hin >= 8 && !(no_halo && no_halo[0] == '1')) {
@@ -487,7 +487,6 @@ int build_layer(avse_weights* W, const LayerDef& L, const float* kernel, const f
         else G.halo = HALO_K3_8;
         const bool v1 = G.halo == HALO_V1;
         const int spg = halo_slices_per_group(L.kh, v1);           // slices per 128-channel group
-        const int ntp = spg / 4;                                   // padded taps per 32-channel chunk
         const int nsteps = v1 ? spg : (L.cin / 128) * spg;
         std::vector<uint16_t> hp((size_t)nsteps * L.cout * 32, 0);
         for (int st = 0; st < nsteps; ++st)
@@ -498,9 +497,9 @@ int build_layer(avse_weights* W, const LayerDef& L, const float* kernel, const f
                         const int tap = 4 * st + kk / 8, c = kk % 8;
                         if (tap < ntap && c < L.cin) v = kernel[((size_t)tap * L.cin + c) * L.cout + n];
                     } else {
-                        const int tap = st % ntp, chunk = st / ntp;   // chunk = cg*4 + cc
+                        const int tap = st % ntap, chunk = st / ntap;   // chunk = cg*4 + cc
                         const int c = chunk * 32 + kk;
-                        if (tap < ntap) v = kernel[((size_t)tap * L.cin + c) * L.cout + n];
+                        v = kernel[((size_t)tap * L.cin + c) * L.cout + n];
                     }
                     hp[((size_t)st * L.cout + n) * 32 + kk] = f2bf(v);
                 }

@@ -45,7 +45,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t clip_rsrc(const void* base, in
                                              0x00020000);
 }
 
-template <int KS, int TH, int TW, int NCLIP, bool V1, bool SCHED>
+// ABL: ablation mask for tools/halo_ablate.hip only (0 in the library): 1 = no fragment reads in
+// the K loop, 2 = no per-step barrier, 4 = no halo staging, 8 = no weight streaming, 16 = no MFMAs.
+template <int KS, int TH, int TW, int NCLIP, bool V1, bool SCHED, int ABL = 0>
 __global__ __launch_bounds__(512, 2) void k_conv_halo(HaloArgs a) {
     constexpr int HH = TH + KS - 1, HW = TW + KS - 1;
     constexpr int HPIX = NCLIP * HH * HW;                 // halo pixels
@@ -55,7 +57,8 @@ __global__ __launch_bounds__(512, 2) void k_conv_halo(HaloArgs a) {
     constexpr int BPC = (TH / 4) * BPR;                   // blocks per clip tile
     static_assert(NCLIP * TH * TW == 256, "tile must be 256 conv pixels");
     constexpr int NTAP = KS * KS;
-    constexpr int SPG = halo_slices_per_group(KS, V1);    // K-slices per channel group (padded to HALO_NT)
+    constexpr int SPG = halo_slices_per_group(KS, V1);    // K-slices per channel group
+    static_assert(V1 || SPG == 4 * KS * KS, "non-V1 slices: 4 chunks x KS^2 taps, no padding");
     constexpr int HCH = V1 ? 1 : (HPIX * 16 + 511) / 512; // 16-B halo chunks per thread
     constexpr int WSTEP = HALO_NT * 8192;                 // weight bytes per barrier step
 
@@ -119,7 +122,8 @@ __global__ __launch_bounds__(512, 2) void k_conv_halo(HaloArgs a) {
     for (int cg = 0; cg < ngroups; ++cg) {
         __syncthreads();   // previous group's readers are done with halo / wbuf
         // ---- stage the halo for channel group cg ----
-        if constexpr (V1) {
+        if constexpr ((ABL & 4) != 0) {
+        } else if constexpr (V1) {
             for (int p = tid; p < HPIX; p += 512) {
                 const int cl = p / (HH * HW), rr = p % (HH * HW);
                 const int y = rr / HW, x = rr % HW;
@@ -186,9 +190,7 @@ __global__ __launch_bounds__(512, 2) void k_conv_halo(HaloArgs a) {
 #pragma unroll
                     for (int i = 0; i < 4; ++i) fa[u][i] = *reinterpret_cast<const i32x4*>(halo + abase[i] + toff);
                 } else {
-                    constexpr int NTP = SPG / 4;                     // padded taps per 32-channel chunk
-                    const int cc = slice / NTP, tap0 = slice % NTP;
-                    const int tap = tap0 < NTAP ? tap0 : NTAP - 1;
+                    const int cc = slice / NTAP, tap = slice % NTAP;   // slice = 32-channel chunk x tap
                     const int ky = tap / KS, kx = tap % KS;
                     // slot swizzle of this lane's pixels at this tap: identical for its 4 fragments
                     const int m = ((((xm + kx) & 3) << 1) | (((ym + ky) & 1) << 3)) ^ (cc * 4 + fg);
@@ -203,23 +205,32 @@ __global__ __launch_bounds__(512, 2) void k_conv_halo(HaloArgs a) {
         i32x4 wv[HALO_NT];
         gload(0, wv);
         lstore(0, wv);
-        if (steps_per_group > 1) {
-            gload(1, wv);
-            lstore(1, wv);
-        }
+        gload(min(1, steps_per_group - 1), wv);
+        lstore(1, wv);
         __syncthreads();
         if constexpr (SCHED) {
-            // Branch-free steps (prefetch indices clamped; stores past the end hit a slot nobody reads
-            // again), two steps per iteration so the fragment registers swap roles without copies, and
-            // an explicit interleave: the next step's weight loads first, then each MFMA pair shares its
-            // issue gaps with one fragment ds_read and the address VALU, so both waves of a SIMD keep the
-            // matrix pipe fed instead of serialising their address math before a solid MFMA block.
+            // Software pipeline, one barrier per step st (ring slot = step % 3):
+            //   1. store the weights of step st+2 (global-loaded one step ago) into the slot step st-1
+            //      used — its fragment reads completed before the previous barrier;
+            //   2. issue the global weight loads of step st+3 (a whole step of latency budget);
+            //   3. issue the fragment reads of step st+1 (slot written before the previous barrier);
+            //   4. the 8*HALO_NT MFMAs of step st on fragments already in registers.
+            // The DS store precedes the reads, so lgkmcnt (in order for LDS) never makes the barrier wait
+            // on anything but reads that have had the whole MFMA block to land, and sched_barrier keeps
+            // the compiler from sinking the reads below the MFMAs.  Branch-free: prefetch indices are
+            // clamped; a store past the end lands in a slot nobody reads again in this group.
             i32x4 fa[HALO_NT][4], fb[HALO_NT][4], na[HALO_NT][4], nb[HALO_NT][4];
             frags(0, fa, fb);
+            if constexpr ((ABL & 1) != 0) frags(0, na, nb);
+            gload(min(2, steps_per_group - 1), wv);
             auto step = [&](int st, i32x4 (&ca)[HALO_NT][4], i32x4 (&cb)[HALO_NT][4], i32x4 (&xa)[HALO_NT][4],
                             i32x4 (&xb)[HALO_NT][4]) {
-                gload(min(st + 2, steps_per_group - 1), wv);
-                frags(min(st + 1, steps_per_group - 1), xa, xb);
+                if constexpr (!(ABL & 8)) {
+                    lstore(st + 2, wv);
+                    gload(min(st + 3, steps_per_group - 1), wv);
+                }
+                if constexpr (!(ABL & 1)) frags(min(st + 1, steps_per_group - 1), xa, xb);
+                if constexpr (!(ABL & 16)) {
 #pragma unroll
                 for (int u = 0; u < HALO_NT; ++u)
 #pragma unroll
@@ -228,17 +239,19 @@ __global__ __launch_bounds__(512, 2) void k_conv_halo(HaloArgs a) {
                         for (int j = 0; j < 4; ++j)
                             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
                                 __builtin_bit_cast(bf16x8, ca[u][i]), __builtin_bit_cast(bf16x8, cb[u][j]), acc[i][j], 0, 0, 0);
-                __builtin_amdgcn_sched_group_barrier(0x020, HALO_NT, 0);      // VMEM_READ: weight prefetch
+                }
+                // issue order: the LDS stores and weight loads, then one fragment read per MFMA pair, so
+                // neither wave of a SIMD blocks in-order issue behind a full LDS queue while the matrix
+                // pipe idles
+                __builtin_amdgcn_sched_group_barrier(0x200, HALO_NT, 0);          // DS write
+                __builtin_amdgcn_sched_group_barrier(0x020, HALO_NT, 0);          // VMEM read
 #pragma unroll
                 for (int k = 0; k < 8 * HALO_NT; ++k) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);        // MFMA
-                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);        // DS_READ (next fragments)
-                    __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);        // VALU (addresses)
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);        // MFMA
-                    __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);        // VALU
+                    __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);            // MFMA
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);            // DS read
                 }
-                lstore(st + 2, wv);                                           // slot last read two steps ago
-                __syncthreads();
+                __builtin_amdgcn_sched_barrier(0);
+                if constexpr (!(ABL & 2)) __syncthreads();
             };
             for (int st = 0; st < steps_per_group; st += 2) {
                 step(st, fa, fb, na, nb);
@@ -297,251 +310,6 @@ __global__ __launch_bounds__(512, 2) void k_conv_halo(HaloArgs a) {
     }
 }
 
-// Persistent variant (non-V1): gridDim.x workgroups per 128-channel output block walk the tiles
-// tile = blockIdx.x + k * gridDim.x.  A tile's K loop is split into P = 4 x (Ci / 128) phases of
-// 32 input channels; the halo holds one 64-byte chunk per phase slot (p % 4).  While phase G (global
-// over the workgroup's tiles) computes, each thread loads its share of the input chunk of phase G + 3
-// into registers and writes it at the end of phase G into the slot phase G - 1 has just released,
-// so after the prologue no tile ever waits for its input window.
-template <int KS, int TH, int TW, int NCLIP, int NG>
-__global__ __launch_bounds__(512, 2) void k_conv_halo_p(HaloArgs a) {
-    constexpr int HH = TH + KS - 1, HW = TW + KS - 1;
-    constexpr int HPIX = NCLIP * HH * HW;
-    constexpr int HBYTES = HPIX * 256;
-    constexpr int BPR = TW / 4;
-    constexpr int BPC = (TH / 4) * BPR;
-    static_assert(NCLIP * TH * TW == 256, "tile must be 256 conv pixels");
-    constexpr int NTAP = KS * KS;
-    constexpr int SPG = halo_slices_per_group(KS, false);
-    constexpr int NTP = SPG / 4;                          // padded taps per 32-channel chunk
-    constexpr int SPP = NTP / HALO_NT;                    // barrier steps per phase
-    constexpr int PCH = (HPIX * 4 + 511) / 512;           // 16-B halo pieces per thread per phase
-    constexpr int WSTEP = HALO_NT * 8192;
-    constexpr int PAD = (KS - 1) / 2;
-
-    extern __shared__ __attribute__((aligned(16))) char lds[];
-    char* halo = lds;
-    char* wbuf = lds + HBYTES + 256;                     // after the halo's 256-byte slack row
-
-    const int tid = threadIdx.x;
-    const int lane = tid & 63, wid = tid >> 6;
-    const int wm = wid & 3, wn = wid >> 2;
-    const int fr = lane & 15, fg = lane >> 4;
-    const int co0 = blockIdx.y * 128;
-    const int tiles_x = a.Wc / TW, tiles_y = a.Hc / TH;
-    const int ntiles = ((a.N + NCLIP - 1) / NCLIP) * tiles_x * tiles_y;
-    const int nmine = (ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
-    if (nmine <= 0) return;
-    constexpr int P = 4 * NG;                             // phases per tile
-    const int G_total = nmine * P;
-
-    auto tile_origin = [&](int k, int& clip0, int& oy0, int& ox0) {
-        const int t = (int)blockIdx.x + k * (int)gridDim.x;
-        clip0 = (t / (tiles_x * tiles_y)) * NCLIP;
-        const int tt = t % (tiles_x * tiles_y);
-        oy0 = (tt / tiles_x) * TH;
-        ox0 = (tt % tiles_x) * TW;
-    };
-
-    // per-lane fragment geometry (as in k_conv_halo)
-    int abase[4];
-    int xm = 0, ym = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int F = wm * 4 + i;
-        const int cl = F / BPC, b = F % BPC;
-        const int q = fr >> 2;
-        const int fy = 4 * (b / BPR) + 2 * (q >> 1) + ((fr >> 1) & 1);
-        const int fx = 4 * (b % BPR) + 2 * (q & 1) + (fr & 1);
-        abase[i] = ((cl * HH + fy) * HW + fx) * 256;
-        if (i == 0) { xm = fx & 3; ym = fy & 1; }
-    }
-    int boff[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int row = wn * 64 + 16 * j + fr;
-        boff[j] = row * 64 + ((fg ^ wswz(row)) << 4);
-    }
-    const char* wsrc = reinterpret_cast<const char*>(a.w) + (size_t)co0 * 64;
-    const size_t wslice = (size_t)a.Co * 64;
-    const int wrow = tid >> 2, wgp = tid & 3;
-    const int woff = wrow * 64 + ((wgp ^ wswz(wrow)) << 4);
-
-    // ---- halo chunk streaming: the PCH pieces of phase G + 3 are loaded at the first step of
-    //      phase G and stored at its last step (a whole phase of HBM latency budget) ----
-    i32x4 hreg[PCH];
-    const long long clip_bytes = (long long)a.Hc * a.Wc * a.Ci * 2;
-    auto halo_load = [&](int G) {
-        int clip0, oy0, ox0;
-        tile_origin(G / P, clip0, oy0, ox0);
-        const int p = G % P, cg = p >> 2, cc = p & 3;
-        const __amdgpu_buffer_rsrc_t rs = clip_rsrc(a.in, clip0, clip_bytes, a.N);
-#pragma unroll
-        for (int k = 0; k < PCH; ++k) {
-            const int c = tid + 512 * k;
-            const int pix = min(c >> 2, HPIX - 1), g = c & 3;
-            const int cl = pix / (HH * HW), rr = pix % (HH * HW);
-            const int y = rr / HW, x = rr % HW;
-            const int iy = oy0 + y - PAD, ix = ox0 + x - PAD;
-            const bool ok = (c >> 2) < HPIX && iy >= 0 && iy < a.Hc && ix >= 0 && ix < a.Wc;
-            const int off = ok ? (((cl * a.Hc + iy) * a.Wc + ix) * a.Ci + cg * 128 + cc * 32 + g * 8) * 2 : kOOB;
-            hreg[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
-        }
-    };
-    auto halo_store = [&](int G) {
-        const int cc = (G % P) & 3;
-#pragma unroll
-        for (int k = 0; k < PCH; ++k) {
-            const int c = tid + 512 * k;
-            const int pix = c >> 2, g = c & 3;
-            const int rr = pix % (HH * HW);
-            const int y = rr / HW, x = rr % HW;
-            const int dst = pix < HPIX ? pix * 256 + (((cc * 4 + g) ^ hswz(y, x)) << 4) : HBYTES;   // slack row
-            *reinterpret_cast<i32x4*>(halo + dst) = hreg[k];
-        }
-    };
-    // ---- weight ring (3 LDS slots of HALO_NT slices), global step gst -> tile-local step ----
-    i32x4 wv[HALO_NT];
-    auto gload = [&](int ls) {
-#pragma unroll
-        for (int u = 0; u < HALO_NT; ++u)
-            wv[u] = *reinterpret_cast<const i32x4*>(wsrc + (size_t)(ls * HALO_NT + u) * wslice + tid * 16);
-    };
-    auto lstore = [&](int slot) {
-#pragma unroll
-        for (int u = 0; u < HALO_NT; ++u)
-            *reinterpret_cast<i32x4*>(wbuf + slot * WSTEP + u * 8192 + woff) = wv[u];
-    };
-    // fragments of tile-local step (phase p, step sp) from ring slot `slot`
-    auto frags = [&](int p, int sp, int slot, i32x4 (&fa)[HALO_NT][4], i32x4 (&fb)[HALO_NT][4]) {
-        const char* wb = wbuf + slot * WSTEP;
-        const int cc = p & 3;
-#pragma unroll
-        for (int u = 0; u < HALO_NT; ++u) {
-            const int tap0 = sp * HALO_NT + u;
-            const int tap = tap0 < NTAP ? tap0 : NTAP - 1;
-            const int ky = tap / KS, kx = tap % KS;
-            const int m = ((((xm + kx) & 3) << 1) | (((ym + ky) & 1) << 3)) ^ (cc * 4 + fg);
-            const int off = (ky * HW + kx) * 256 + (m << 4);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) fa[u][i] = *reinterpret_cast<const i32x4*>(halo + abase[i] + off);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) fb[u][j] = *reinterpret_cast<const i32x4*>(wb + u * 8192 + boff[j]);
-        }
-    };
-
-    // ---- prologue: input chunks of phases 0..2, weights of steps 0..1 ----
-    for (int G = 0; G < 3 && G < G_total; ++G) {
-        halo_load(G);
-        halo_store(G);
-    }
-    gload(0);
-    lstore(0);
-    gload(1);          // steps_per_tile >= 2: the next step always exists within a tile
-    lstore(1);
-    __syncthreads();
-
-    f32x4 acc[4][4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    i32x4 fa[HALO_NT][4], fb[HALO_NT][4];
-    frags(0, 0, 0, fa, fb);
-    bf16_t* out = reinterpret_cast<bf16_t*>(a.out);
-    const int Wp = a.Wc / 2;
-
-    int slot = 0;          // ring slot of the current step's weights (global step mod 3)
-    int G = 0;             // global phase index
-    for (int k = 0; k < nmine; ++k) {
-#pragma unroll 1
-        for (int p = 0; p < P; ++p, ++G) {
-            const bool pf = G + 3 < G_total;
-#pragma unroll 1
-            for (int sp = 0; sp < SPP; ++sp) {
-                // tile-local index of the step two ahead (wraps into the next tile's weights)
-                int p2 = p, sp2 = sp + 2;
-                if (sp2 >= SPP) { sp2 -= SPP; if (++p2 == P) p2 = 0; }
-                int p1 = p, sp1 = sp + 1;
-                if (sp1 == SPP) { sp1 = 0; if (++p1 == P) p1 = 0; }
-                const int slot1 = slot == 2 ? 0 : slot + 1, slot2 = slot1 == 2 ? 0 : slot1 + 1;
-                // weight loads first: vmcnt retires in issue order, so the (L2-hit) weights must not
-                // queue behind the (HBM) halo loads their end-of-step LDS store waits for
-                gload(p2 * SPP + sp2);            // past the last step this loads/stores unused slices
-                if (pf && sp == 0) halo_load(G + 3);
-                i32x4 na[HALO_NT][4], nb[HALO_NT][4];
-                frags(p1, sp1, slot1, na, nb);
-#pragma unroll
-                for (int u = 0; u < HALO_NT; ++u)
-#pragma unroll
-                    for (int i = 0; i < 4; ++i)
-#pragma unroll
-                        for (int j = 0; j < 4; ++j)
-                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                                __builtin_bit_cast(bf16x8, fa[u][i]), __builtin_bit_cast(bf16x8, fb[u][j]), acc[i][j], 0, 0, 0);
-                lstore(slot2);
-                if (pf && sp == SPP - 1) halo_store(G + 3);      // slot of phase G - 1: free during phase G
-                __syncthreads();
-#pragma unroll
-                for (int u = 0; u < HALO_NT; ++u)
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        fa[u][i] = na[u][i];
-                        fb[u][i] = nb[u][i];
-                    }
-                slot = slot1;
-            }
-        }
-        // ---- tile epilogue: BN scale/shift -> 2x2 max pool (in-lane quad) -> LeakyReLU -> store ----
-        int clip0, oy0, ox0;
-        tile_origin(k, clip0, oy0, ox0);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int co = co0 + wn * 64 + 16 * j + fr;
-            const float sc = a.scale[co], sh = a.shift[co];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int F = wm * 4 + i;
-                const int cl = F / BPC, b = F % BPC;
-                const int clip = clip0 + cl;
-                const int py = (oy0 + 4 * (b / BPR)) / 2 + (fg >> 1);
-                const int px = (ox0 + 4 * (b % BPR)) / 2 + (fg & 1);
-                float v0 = acc[i][j][0] * sc + sh, v1 = acc[i][j][1] * sc + sh;
-                float v2 = acc[i][j][2] * sc + sh, v3 = acc[i][j][3] * sc + sh;
-                float x = fmaxf(fmaxf(v0, v1), fmaxf(v2, v3));
-                x = x >= 0.f ? x : LRELU * x;
-                if (clip < a.N)
-                    out[(size_t)clip * a.out_clip_stride + (size_t)(py * Wp + px) * a.out_pix_stride + a.out_c_off + co] = (bf16_t)x;
-                acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-            }
-        }
-    }
-}
-
-template <int KS, int TH, int TW, int NCLIP, int NG>
-int launch_halo_p(const HaloArgs& a, hipStream_t s) {
-    constexpr int HPIX = NCLIP * (TH + KS - 1) * (TW + KS - 1);
-    const size_t shm = HPIX * 256 + 256 + 3 * HALO_NT * 8192;
-    static bool attr = false;
-    if (!attr) {
-        AVSE_HIP_CHECK(hipFuncSetAttribute((const void*)k_conv_halo_p<KS, TH, TW, NCLIP, NG>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
-        attr = true;
-    }
-    if (a.Hc % TH || a.Wc % TW || a.Co % 128 || a.Ci != 128 * NG) { set_error("halo conv: tile does not divide the layer"); return 3; }
-    int dev = 0, ncu = 256;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    const int tiles = ((a.N + NCLIP - 1) / NCLIP) * (a.Hc / TH) * (a.Wc / TW);
-    const int cob = a.Co / 128;
-    int gx = ncu / cob;                       // one workgroup per CU (LDS-limited)
-    if (gx < 1) gx = 1;
-    if (gx > tiles) gx = tiles;
-    hipLaunchKernelGGL((k_conv_halo_p<KS, TH, TW, NCLIP, NG>), dim3(gx, cob), dim3(512), shm, s, a);
-    AVSE_HIP_CHECK(hipGetLastError());
-    return 0;
-}
-
 template <int KS, int TH, int TW, int NCLIP, bool V1, bool SCHED>
 int launch_halo_t(const HaloArgs& a, hipStream_t s) {
     constexpr int HH = TH + KS - 1, HW = TW + KS - 1;
@@ -565,26 +333,24 @@ int launch_halo_t(const HaloArgs& a, hipStream_t s) {
 }  // namespace
 
 int launch_conv_halo(const HaloArgs& a, hipStream_t s) {
-    // AVSE_HALO_MODE = tile (default: one tile per workgroup, compiler schedule)
-    //                | sched (same, explicit MFMA/DS/VALU interleave)  | persist (persistent, streamed halo)
-    // Measured at B=512 on MI355X (v_conv2): tile 1.50-1.59 ms, persist 1.58-1.61, sched 1.64.
+    // AVSE_HALO_MODE = stream (default: persistent LDS-DMA kernel, conv_stream.hip)
+    //                | pipe (8-wave halo kernel, explicit pipeline) | tile (8-wave, compiler schedule)
     static const int mode = [] {
         const char* e = std::getenv("AVSE_HALO_MODE");
-        if (e && e[0] == 's') return 1;
-        if (e && e[0] == 'p') return 2;
-        return 0;
+        if (e && e[0] == 't') return 0;
+        if (e && e[0] == 'p') return 1;
+        return 2;
     }();
+    const bool pipe = mode == 1;
+    if (mode == 2 && a.variant != HALO_V1) return launch_conv_stream(a, s);
     switch (a.variant) {
         case HALO_V1: return launch_halo_t<5, 16, 16, 1, true, false>(a, s);
         case HALO_K5:
-            if (mode == 2 && a.Ci == 128) return launch_halo_p<5, 16, 16, 1, 1>(a, s);
-            return mode == 1 ? launch_halo_t<5, 16, 16, 1, false, true>(a, s) : launch_halo_t<5, 16, 16, 1, false, false>(a, s);
+            return pipe ? launch_halo_t<5, 16, 16, 1, false, true>(a, s) : launch_halo_t<5, 16, 16, 1, false, false>(a, s);
         case HALO_K3_16:
-            if (mode == 2) return a.Ci == 128 ? launch_halo_p<3, 16, 16, 1, 1>(a, s) : launch_halo_p<3, 16, 16, 1, 2>(a, s);
-            return mode == 1 ? launch_halo_t<3, 16, 16, 1, false, true>(a, s) : launch_halo_t<3, 16, 16, 1, false, false>(a, s);
+            return pipe ? launch_halo_t<3, 16, 16, 1, false, true>(a, s) : launch_halo_t<3, 16, 16, 1, false, false>(a, s);
         case HALO_K3_8:
-            if (mode == 2 && a.Ci == 256) return launch_halo_p<3, 8, 8, 4, 2>(a, s);
-            return mode == 1 ? launch_halo_t<3, 8, 8, 4, false, true>(a, s) : launch_halo_t<3, 8, 8, 4, false, false>(a, s);
+            return pipe ? launch_halo_t<3, 8, 8, 4, false, true>(a, s) : launch_halo_t<3, 8, 8, 4, false, false>(a, s);
     }
     set_error("bad halo variant");
     return 3;

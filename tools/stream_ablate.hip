@@ -1,0 +1,83 @@
+// Ablation timing of the persistent warp-specialised kernel (k_conv_stream<5,16,16,1,ABL>, conv_stream.hip) at
+// the v_conv2 bench shape (N=512, 64x64x128 -> 128, 5x5).  Timing only: outputs are meaningless for
+// ABL != 0.   hipcc --offload-arch=gfx950 -O3 -std=c++20 -o _stream_ablate stream_ablate.hip
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "../audio-visual-speech-enhancement_amd/csrc/conv_stream.hip"
+
+namespace avse {
+void set_error(const std::string& msg) { std::fprintf(stderr, "error: %s\n", msg.c_str()); }
+}  // namespace avse
+
+using namespace avse;
+
+template <int ABL, int LAT = 4>
+float run(const HaloArgs& a, int reps) {
+    using G = StreamGeom<5, 16, 16, 1, LAT>;
+    (void)hipFuncSetAttribute((const void*)k_conv_stream<5, 16, 16, 1, LAT, ABL>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              G::LDS);
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    for (int r = 0; r < 2; ++r)
+        hipLaunchKernelGGL((k_conv_stream<5, 16, 16, 1, LAT, ABL>), dim3(256, 1), dim3(512), G::LDS, 0, a);
+    (void)hipEventRecord(e0, 0);
+    for (int r = 0; r < reps; ++r)
+        hipLaunchKernelGGL((k_conv_stream<5, 16, 16, 1, LAT, ABL>), dim3(256, 1), dim3(512), G::LDS, 0, a);
+    (void)hipEventRecord(e1, 0);
+    (void)hipEventSynchronize(e1);
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    return ms / reps;
+}
+
+int main() {
+    const int N = 512, H = 64, C = 128;
+    HaloArgs a{};
+    a.variant = HALO_K5;
+    a.N = N; a.Hc = H; a.Wc = H; a.Ci = C; a.Co = C;
+    a.out_clip_stride = (long long)(H / 2) * (H / 2) * C;
+    a.out_pix_stride = C;
+    void *in, *out, *w;
+    float *sc, *sh;
+    (void)hipMalloc(&in, (size_t)N * H * H * C * 2);
+    (void)hipMalloc(&out, (size_t)N * (H / 2) * (H / 2) * C * 2);
+    (void)hipMalloc(&w, (size_t)100 * C * 64);
+    (void)hipMalloc(&sc, C * 4);
+    (void)hipMalloc(&sh, C * 4);
+    // AVSE_ABL_RANDOM=1: random bf16 activations / weights (MFMA power, hence clock, depends on data)
+    const char* rnd = std::getenv("AVSE_ABL_RANDOM");
+    if (rnd && rnd[0] == '1') {
+        std::vector<uint16_t> h((size_t)N * H * H * C);
+        uint32_t st = 12345;
+        auto next = [&] { st = st * 1664525u + 1013904223u; return st; };
+        for (auto& v : h) v = (uint16_t)(0x3c00 + (next() >> 22)) ^ (uint16_t)((next() >> 31) << 15);   // +-[0.0078, 0.03)
+        (void)hipMemcpy(in, h.data(), h.size() * 2, hipMemcpyHostToDevice);
+        (void)hipMemcpy(w, h.data(), (size_t)100 * C * 64, hipMemcpyHostToDevice);
+    } else {
+        (void)hipMemset(in, 0, (size_t)N * H * H * C * 2);
+        (void)hipMemset(w, 0, (size_t)100 * C * 64);
+    }
+    (void)hipMemset(sc, 0, C * 4);
+    (void)hipMemset(sh, 0, C * 4);
+    a.in = in; a.out = out; a.w = w; a.scale = sc; a.shift = sh;
+    const double flop = 2.0 * N * H * H * C * C * 25;
+    const int reps = 10;
+    auto rep = [&](const char* name, float ms) {
+        std::printf("%-34s %8.4f ms  %7.1f TF/s\n", name, ms, flop / (ms * 1e-3) / 1e12);
+    };
+    rep("full", run<0, 10>(a, reps));
+    rep("no halo pieces (1)", run<1, 10>(a, reps));
+    rep("no weight streaming (2)", run<2, 10>(a, reps));
+    rep("no loads at all (3)", run<3, 10>(a, reps));
+    rep("no wait/barrier (4)", run<4, 10>(a, reps));
+    rep("no frag reads (8)", run<8, 10>(a, reps));
+    rep("MFMA only (15)", run<15, 10>(a, reps));
+    rep("L2-resident input (64)", run<64, 10>(a, reps));
+    rep("LAT5", run<0, 5>(a, reps));
+    return 0;
+}
