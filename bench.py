@@ -196,8 +196,8 @@ def main():
         "config": {"workload": "STFT (n_fft 640, hop 160, 80 mel, dB) + full audio-visual fusion forward "
                                "(BASELINE configs[3]) on 200-ms@16kHz clips",
                    "global_batch": world * B, "per_gpu_batch": B, "parallelism": f"dp{world}"},
-        "roofline": {"kernel": f"{dom} (k_conv_halo<5,16,16,1>: halo-tiled implicit GEMM M=4096/clip N=128 "
-                               "K=3200, fused BN+LReLU+2x2 maxpool)" if args.dtype == "bf16" else
+        "roofline": {"kernel": f"{dom} (k_conv_stream<5,16,16,1>: persistent warp-specialised implicit GEMM "
+                               "M=4096/clip N=128 K=3200, fused BN+LReLU+2x2 maxpool)" if args.dtype == "bf16" else
                                f"{dom} (k_conv<float,128> implicit GEMM, exact-fp32 MFMA)",
                      "bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4), "traffic": traffic,

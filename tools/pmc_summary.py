@@ -34,7 +34,7 @@ def main():
         shutil.copy(stats[0], os.path.join(prof, f"{tag}_kernel_stats.csv"))
     fetch = counter(os.path.join(out, f"pmc_{tag}_fetch"), "FETCH_SIZE")
     write = counter(os.path.join(out, f"pmc_{tag}_write"), "WRITE_SIZE")
-    res = {"kernel": "k_conv_halo<5, 16, 16, 1, false, false> (v_conv2)", "batch": 512,
+    res = {"kernel": "k_conv_stream<5, 16, 16, 1, 10, 0> (v_conv2)", "batch": 512,
            "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, tools/fwd_loop.py (B=512 bf16)",
            "dispatches": [len(fetch), len(write)]}
     if fetch and write:
