@@ -143,6 +143,7 @@ struct HaloArgs {
 
 int launch_conv_halo(const HaloArgs& a, hipStream_t s);
 int launch_conv_stream(const HaloArgs& a, hipStream_t s);   // conv_stream.hip (non-V1 variants)
+int launch_conv_v1(const HaloArgs& a, hipStream_t s);       // conv_v1.hip (v_conv1)
 int launch_video_prep(const float* video, const float* mean, const float* stdv, void* out, int64_t N,
                       int dtype, hipStream_t s);
 int launch_audio_prep(const float* audio, void* out, int64_t N, int dtype, hipStream_t s);

@@ -172,7 +172,8 @@ struct GpuLayer {
     float* shift = nullptr;
     int2* taps = nullptr;
     int halo = HALO_NONE;     // halo-tiled kernel variant (bf16 video convs)
-    void* w_halo = nullptr;   // bf16 [step][Cout][32] packing for conv_halo.hip
+    void* w_halo = nullptr;   // bf16 packing for conv_stream.hip / conv_v1.hip (see build_layer)
+    float* scale_h = nullptr; // |scale| for w_halo: channels with a negative BN scale have negated weights
 };
 
 struct avse_weights {
@@ -476,8 +477,8 @@ int build_layer(avse_weights* W, const LayerDef& L, const float* kernel, const f
     if ((rc = upload(W, shift, &G.shift))) return rc;
     if ((rc = upload(W, taps, &G.taps))) return rc;
 
-    // halo-tiled packing for the bf16 video convs: [slice][Cout][32], slice = (cg*4 + cc)*KS^2 + tap
-    // (V1: step = group of 4 taps, 8 channels each, channels 5..7 and taps >= 25 zero)
+    // packing for the bf16 video conv kernels: conv_stream.hip [slice][Cout][32], slice = (cg*4 + cc)*KS^2
+    // + tap; conv_v1.hip (v_conv1) [Cout][128] in im2col order
     const char* no_halo = std::getenv("AVSE_NO_HALO");   // A/B switch: force the generic kernel
     if (W->dtype == AVSE_BF16 && L.kind == CONV && L.pool && L.hin >= 8 && !(no_halo && no_halo[0] == '1')) {
         const int ntap = L.kh * L.kw;
@@ -485,24 +486,34 @@ int build_layer(avse_weights* W, const LayerDef& L, const float* kernel, const f
         else if (L.kh == 5) G.halo = HALO_K5;
         else if (L.hin >= 16) G.halo = HALO_K3_16;
         else G.halo = HALO_K3_8;
-        const bool v1 = G.halo == HALO_V1;
-        const int spg = halo_slices_per_group(L.kh, v1);           // slices per 128-channel group
-        const int nsteps = v1 ? spg : (L.cin / 128) * spg;
-        std::vector<uint16_t> hp((size_t)nsteps * L.cout * 32, 0);
-        for (int st = 0; st < nsteps; ++st)
+        // Sign fold: a channel whose folded BN scale is negative gets negated weights and |scale|, so
+        // every epilogue scale is >= 0 and 2x2 max pooling commutes exactly with scale/shift (the kernels
+        // pool the raw accumulators, then apply one FMA).  bf16 negation and fp32 sums are exact.
+        std::vector<float> sgn(L.cout), scale_h(L.cout);
+        for (int n = 0; n < L.cout; ++n) {
+            sgn[n] = scale[n] < 0.f ? -1.f : 1.f;
+            scale_h[n] = std::fabs(scale[n]);
+        }
+        if ((rc = upload(W, scale_h, &G.scale_h))) return rc;
+        std::vector<uint16_t> hp;
+        if (G.halo == HALO_V1) {
+            // conv_v1.hip: [Cout][128], dense im2col order k = tap * Cin + frame (125 real, zeros after)
+            hp.assign((size_t)L.cout * 128, 0);
             for (int n = 0; n < L.cout; ++n)
-                for (int kk = 0; kk < 32; ++kk) {
-                    float v = 0.f;
-                    if (v1) {
-                        const int tap = 4 * st + kk / 8, c = kk % 8;
-                        if (tap < ntap && c < L.cin) v = kernel[((size_t)tap * L.cin + c) * L.cout + n];
-                    } else {
+                for (int k = 0; k < ntap * L.cin; ++k)
+                    hp[(size_t)n * 128 + k] = f2bf(sgn[n] * kernel[(size_t)k * L.cout + n]);
+        } else {
+            const int nsteps = (L.cin / 128) * halo_slices_per_group(L.kh, false);
+            hp.assign((size_t)nsteps * L.cout * 32, 0);
+            for (int st = 0; st < nsteps; ++st)
+                for (int n = 0; n < L.cout; ++n)
+                    for (int kk = 0; kk < 32; ++kk) {
                         const int tap = st % ntap, chunk = st / ntap;   // chunk = cg*4 + cc
                         const int c = chunk * 32 + kk;
-                        v = kernel[((size_t)tap * L.cin + c) * L.cout + n];
+                        hp[((size_t)st * L.cout + n) * 32 + kk] =
+                            f2bf(sgn[n] * kernel[((size_t)tap * L.cin + c) * L.cout + n]);
                     }
-                    hp[((size_t)st * L.cout + n) * 32 + kk] = f2bf(v);
-                }
+        }
         uint16_t* d;
         if ((rc = upload(W, hp, &d))) return rc;
         G.w_halo = d;
@@ -521,7 +532,7 @@ HaloArgs halo_args(const GpuLayer& G, const void* in, const float* video, const 
     a.vstd = vstd;
     a.out = out;
     a.w = G.w_halo;
-    a.scale = G.scale;
+    a.scale = G.scale_h;
     a.shift = G.shift;
     a.N = (int)N;
     a.Hc = G.def.hin;

@@ -344,7 +344,7 @@ int launch_conv_halo(const HaloArgs& a, hipStream_t s) {
     const bool pipe = mode == 1;
     if (mode == 2 && a.variant != HALO_V1) return launch_conv_stream(a, s);
     switch (a.variant) {
-        case HALO_V1: return launch_halo_t<5, 16, 16, 1, true, false>(a, s);
+        case HALO_V1: return launch_conv_v1(a, s);
         case HALO_K5:
             return pipe ? launch_halo_t<5, 16, 16, 1, false, true>(a, s) : launch_halo_t<5, 16, 16, 1, false, false>(a, s);
         case HALO_K3_16:

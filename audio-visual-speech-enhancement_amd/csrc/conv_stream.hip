@@ -313,30 +313,34 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
     // never assigned a constant: a tile's first step accumulates onto the MFMA's inline zero instead,
     // so the register allocator keeps each accumulator in place across the whole MFMA chain
     f32x16 acc[2][4];
-    bf16_t* out = reinterpret_cast<bf16_t*>(a.out);
     const int Wp = a.Wc / 2;
-    // accumulator register 4g + e of block i, column block jb = row 8g + 4 hi + e = pool window 2g + hi
+    // scale >= 0 (host sign fold), so pooling the raw accumulators then one FMA equals BN-then-pool
+    // exactly; LeakyReLU(0.3) = max(x, 0.3 x); 32-bit offsets into a buffer resource over the tile's
+    // clips (stores past the last clip of a ragged 4-clip tile fall outside it and are dropped).
+    // Accumulator register 4g + e of block i, column block jb = row 8g + 4 hi + e = pool window 2g + hi.
     auto epilogue = [&](int clip0, int oy0, int ox0) {
+        const long long cb = a.out_clip_stride * 2;
+        const __amdgpu_buffer_rsrc_t ors =
+            make_rsrc(reinterpret_cast<const char*>(a.out) + (long long)clip0 * cb, (long long)(a.N - clip0) * cb);
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             const int b = 2 * w + i;
             const int cl = b / BPC, bb = b % BPC;
-            const int clip = clip0 + cl;
             const int py0 = (oy0 + 4 * (bb / BPR)) / 2, px0 = (ox0 + 8 * (bb % BPR)) / 2;
+            const int cbase = cl * (int)a.out_clip_stride + a.out_c_off + co0;
 #pragma unroll
             for (int jb = 0; jb < 4; ++jb) {
-                const int co = co0 + 32 * jb + r32;
+                const int co = 32 * jb + r32;
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
                     const int q = 2 * g + hi;
                     const int py = py0 + (q >> 2), px = px0 + (q & 3);
-                    const float v0 = acc[i][jb][4 * g] * sc[jb] + sh[jb], v1 = acc[i][jb][4 * g + 1] * sc[jb] + sh[jb];
-                    const float v2 = acc[i][jb][4 * g + 2] * sc[jb] + sh[jb], v3 = acc[i][jb][4 * g + 3] * sc[jb] + sh[jb];
-                    float x = fmaxf(fmaxf(v0, v1), fmaxf(v2, v3));
-                    x = x >= 0.f ? x : LRELU * x;
-                    if (clip < a.N)
-                        out[(size_t)clip * a.out_clip_stride + (size_t)(py * Wp + px) * a.out_pix_stride + a.out_c_off + co] =
-                            (bf16_t)x;
+                    const float mx = fmaxf(fmaxf(acc[i][jb][4 * g], acc[i][jb][4 * g + 1]),
+                                           fmaxf(acc[i][jb][4 * g + 2], acc[i][jb][4 * g + 3]));
+                    float x = fmaf(mx, sc[jb], sh[jb]);
+                    x = fmaxf(x, LRELU * x);
+                    __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (bf16_t)x), ors,
+                                                          (cbase + (py * Wp + px) * a.out_pix_stride + co) * 2, 0, 0);
                 }
             }
         }
@@ -369,7 +373,8 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
         __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (!(ABL & 4)) {
-            wait_vm_lgkm0<0>();
+            // LDS reads only: the epilogue's global stores (vmcnt on gfx9) are never waited for
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             barrier_raw();
         }
         if (++tap1 == NTAP) {
