@@ -113,6 +113,9 @@ struct ConvArgs {
 };
 
 int launch_conv(const ConvArgs& a, int dtype, hipStream_t s);
+int launch_splitk_reduce(const ConvArgs& a, int dtype, hipStream_t s);   // conv.hip: split-K tail
+int launch_igemm(const ConvArgs& a, hipStream_t s);                      // igemm.hip (bf16)
+int choose_ksplit_ws(long long M, int Co, int kpad);                     // igemm.hip split-K choice
 
 // ---- halo-tiled video convolutions (conv_halo.hip), bf16 only ----------------------------
 enum HaloVariant { HALO_NONE = -1, HALO_V1 = 0, HALO_K5 = 1, HALO_K3_16 = 2, HALO_K3_8 = 3 };

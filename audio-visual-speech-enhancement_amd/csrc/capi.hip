@@ -215,7 +215,22 @@ const size_t kBufElems[B_COUNT] = {128 * 128 * 8, 80 * 20 * 8, 40 * 10 * 64, 40 
 
 // Split-K plan for a single-phase GEMM of M rows x Co columns x kpad: double the split while the
 // grid stays <= ~1024 workgroups and every split keeps >= 16 k-slabs (64-byte slabs).
+// AVSE_IGEMM=1: run the bf16 generic layers on k_igemm (igemm.hip) instead of k_conv (conv.hip).
+// Opt-in while k_igemm's loader-bound K-slab is slower than k_conv on these shapes (r01 measurements).
+bool no_igemm() {
+    static const bool v = [] {
+        const char* e = std::getenv("AVSE_IGEMM");
+        return !(e && e[0] == '1');
+    }();
+    return v;
+}
+int run_conv(const ConvArgs& a, int dtype, hipStream_t s) {
+    if (dtype == AVSE_BF16 && !no_igemm()) return launch_igemm(a, s);
+    return launch_conv(a, dtype, s);
+}
+
 int choose_ksplit(int64_t M, int Co, int kpad, int dtype) {
+    if (dtype == AVSE_BF16 && !no_igemm()) return choose_ksplit_ws(M, Co, kpad);
     const int BN = Co <= 64 ? 64 : 128;
     const int64_t tiles = ((M + 127) / 128) * ((Co + BN - 1) / BN);
     const int nslab = kpad / (dtype == AVSE_BF16 ? 32 : 16);
@@ -803,7 +818,7 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
         const long long in_cs = (long long)G.def.hin * G.def.win * (i == 0 ? G.cin_pad : G.def.cin);
         ConvArgs a = (i < 4) ? conv_args(G, buf(a_in[i]), in_cs, buf(a_in[i + 1]), (long long)G.ho * G.wo * G.def.cout, G.def.cout, 0, N)
                              : conv_args(G, buf(a_in[i]), in_cs, buf(B_CAT), 5248, G.def.cout, 0, N);   // Flatten -> concat[0:3200]
-        if ((rc = launch_conv(a, dt, s)) || (rc = mark())) return rc;
+        if ((rc = run_conv(a, dt, s)) || (rc = mark())) return rc;
     }
     // video encoder (network.py:138-175)
     const int v_in[6] = {B_VIN, B_V1, B_V2, B_V3, B_V4, B_V5};
@@ -820,19 +835,19 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
         ConvArgs a = (i < 5) ? conv_args(G, buf(v_in[i]), in_cs, buf(v_in[i + 1]), (long long)G.ho * G.wo * G.def.cout, G.def.cout, 0, N)
                              : conv_args(G, buf(v_in[i]), in_cs, buf(B_CAT), 5248, G.def.cout, 3200, N);  // concat[3200:5248]
         if (i == 5) split(a);
-        if ((rc = launch_conv(a, dt, s)) || (rc = mark())) return rc;
+        if ((rc = run_conv(a, dt, s)) || (rc = mark())) return rc;
     }
     // fusion + decoder dense (network.py:53-58, :66-78)
     {
         ConvArgs a = conv_args(L(11), buf(B_CAT), 5248, buf(B_E1), 1312, 1312, 0, N);
         split(a);
-        if ((rc = launch_conv(a, dt, s)) || (rc = mark())) return rc;
+        if ((rc = run_conv(a, dt, s)) || (rc = mark())) return rc;
         a = conv_args(L(12), buf(B_E1), 1312, buf(B_E2), 1312, 1312, 0, N);
         split(a);
-        if ((rc = launch_conv(a, dt, s)) || (rc = mark())) return rc;
+        if ((rc = run_conv(a, dt, s)) || (rc = mark())) return rc;
         a = conv_args(L(13), buf(B_E2), 1312, buf(B_E3), 3200, 3200, 0, N);
         split(a);
-        if ((rc = launch_conv(a, dt, s)) || (rc = mark())) return rc;
+        if ((rc = run_conv(a, dt, s)) || (rc = mark())) return rc;
     }
     // audio decoder (network.py:112-135)
     const int d_in[6] = {B_E3, B_D1, B_D2, B_D3, B_D4, B_D5};
@@ -840,7 +855,7 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
         const GpuLayer& G = L(14 + i);
         const long long in_cs = (long long)G.def.hin * G.def.win * G.def.cin;
         ConvArgs a = conv_args(G, buf(d_in[i]), in_cs, buf(d_in[i + 1]), (long long)G.ho * G.wo * G.def.cout, G.def.cout, 0, N);
-        if ((rc = launch_conv(a, dt, s)) || (rc = mark())) return rc;
+        if ((rc = run_conv(a, dt, s)) || (rc = mark())) return rc;
     }
     if ((rc = launch_out_conv(buf(B_D5), W->d6_w, W->d6_bias, out, N * 80 * 20, dt, s)) || (rc = mark())) return rc;
     return 0;

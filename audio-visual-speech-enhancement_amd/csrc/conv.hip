@@ -414,12 +414,16 @@ int launch_conv(const ConvArgs& a, int dtype, hipStream_t s) {
         else hipLaunchKernelGGL((k_conv<float, 128>), grid, dim3(256), 0, s, a);
     }
     AVSE_HIP_CHECK(hipGetLastError());
-    if (a.ksplit > 1) {
-        const long long total = (long long)(a.pool ? M / 4 : M) * a.Co;
-        if (dtype == 1) hipLaunchKernelGGL(k_splitk_reduce<bf16_t>, dim3(grid_for(total, 256)), dim3(256), 0, s, a);
-        else hipLaunchKernelGGL(k_splitk_reduce<float>, dim3(grid_for(total, 256)), dim3(256), 0, s, a);
-        AVSE_HIP_CHECK(hipGetLastError());
-    }
+    if (a.ksplit > 1) return launch_splitk_reduce(a, dtype, s);
+    return 0;
+}
+
+int launch_splitk_reduce(const ConvArgs& a, int dtype, hipStream_t s) {
+    const int M = a.N * a.Hq * a.Wq;
+    const long long total = (long long)(a.pool ? M / 4 : M) * a.Co;
+    if (dtype == 1) hipLaunchKernelGGL(k_splitk_reduce<bf16_t>, dim3(grid_for(total, 256)), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(k_splitk_reduce<float>, dim3(grid_for(total, 256)), dim3(256), 0, s, a);
+    AVSE_HIP_CHECK(hipGetLastError());
     return 0;
 }
 

@@ -202,6 +202,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
         }
         wait_vm_lgkm0<0>();
         barrier_raw();
+        barrier_raw();   // the compute waves have read slice 0 (weight slot 0 is overwritten at step 0)
 
         // state of the step being issued: its slice (k, c, tap) in halo slot hs; wsa = weight slice
         // loaded by it (step + WD, mod spt)
@@ -351,6 +352,8 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
     i32x4 fa[4], fb[8], na[4], nb[8];
     frags(0, 0, 0, fa, fb);
     if constexpr ((ABL & 8) != 0) frags(0, 0, 0, na, nb);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    barrier_raw();   // slice 0 read: the loaders may now overwrite weight slot 0
 
     auto cstep = [&](auto first, int t, i32x4 (&ca)[4], i32x4 (&cb)[8], i32x4 (&xa)[4], i32x4 (&xb)[8]) {
         // fragments of the next slice (weights in ring slot (t+1)&1), interleaved with the 16 MFMAs
