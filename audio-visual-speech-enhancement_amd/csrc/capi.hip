@@ -225,7 +225,7 @@ bool no_igemm() {
     return v;
 }
 int run_conv(const ConvArgs& a, int dtype, hipStream_t s) {
-    if (dtype == AVSE_BF16 && !no_igemm()) return launch_igemm(a, s);
+    if (dtype == AVSE_BF16 && !no_igemm() && a.Ci % 32 == 0) return launch_igemm(a, s);
     return launch_conv(a, dtype, s);
 }
 

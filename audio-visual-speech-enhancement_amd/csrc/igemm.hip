@@ -1,5 +1,5 @@
 // Persistent, warp-specialised implicit-GEMM for the bf16 layers outside the video trunk's big convs:
-// audio encoder a_conv1..5 (network.py:88-109), v_conv6 (:169), the three Dense layers (:56, :69,
+// audio encoder a_conv2..5 (network.py:92-109), v_conv6 (:169), the three Dense layers (:56, :69,
 // :75-78) and the deconvolution decoder d_deconv1..5 (:112-133).  Same layer semantics and argument
 // block (ConvArgs) as the generic k_conv in conv.hip — TF 'SAME' zero padding, deconvolution as
 // sub-pixel phases with per-phase tap tables, folded bias/BN scale-shift, LeakyReLU(0.3), fused 2x2 max
@@ -7,13 +7,18 @@
 // partials — re-organised the way conv_stream.hip is (see its header for the measurements):
 //   * 512 threads: 4 compute waves (one per SIMD, tile 64 x BN each, v_mfma_f32_32x32x16_bf16,
 //     issue priority) + 4 loader waves (all address arithmetic, im2col gathers, LDS stores);
-//   * persistent over work items (phase, K-split, M-tile of 256 rows, N-tile of BN); each item's K loop
-//     runs in 32-element slabs, one slab and one barrier per step, padded to an even step count;
-//   * loaders issue every load LAT + 2 steps ahead of its slab into a ring of LAT register sets and
-//     store the set loaded LAT steps earlier into a 2-slot LDS ring (vmcnt retires in order; the
-//     ring gives the im2col gathers LAT-1 whole steps of latency budget).
-// LDS images (conflict-free for the 32x32x16 operand reads): A row r / B row n is 64 B, 16-B chunk j
-// at position j ^ ((row >> 2) & 3).
+//   * persistent over work items (phase, K-split, M-tile of 256 rows, N-tile of BN), numbered so each
+//     XCD walks a contiguous block (its L2 keeps the shared im2col window); one barrier per
+//     64-deep K step, which the compute waves run as two 32-deep halves (fragments of the next half
+//     are read while the current half's MFMAs run);
+//   * a loader lane owns 64 contiguous bytes (32 channels of one tap, Ci % 32 == 0) of two A rows per
+//     step: one bounds/address computation feeds four 16-byte loads (the 32-deep first version spent
+//     its loader issue on per-chunk address arithmetic and was slower than k_conv);
+//   * loads run LAT + 2 steps ahead of their step into a ring of LAT register sets; the set loaded LAT
+//     steps earlier is stored into a 3-slot LDS ring (vmcnt retires in order; the ring gives the
+//     gathers LAT - 1 whole steps of latency budget).
+// LDS images (conflict-free for the 32x32x16 operand reads): A row r / B row n is 128 B, 16-B chunk j
+// at position j ^ ((row >> 1) & 7).
 #include <type_traits>
 
 #include "avse_common.h"
@@ -25,7 +30,9 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr float LRELU = 0.3f;
 constexpr int kOOB = 0x7fffff00;
 constexpr int BM = 256;         // rows per work item (4 compute waves x 64)
+constexpr int BK = 64;          // K elements per step
 constexpr int LAT = 4;          // load -> LDS store distance in steps
+constexpr int NS = 3;           // LDS slots
 constexpr int MAXTAPS = 128;    // tap table entries staged in LDS
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, long long bytes) {
@@ -37,50 +44,65 @@ __device__ __forceinline__ void wait_vm_lgkm0() {
     asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(N) : "memory");
 }
 __device__ __forceinline__ void barrier_raw() { asm volatile("s_barrier" ::: "memory"); }
-__device__ __forceinline__ int swz(int row) { return (row >> 2) & 3; }
+__device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
+__device__ __forceinline__ i32x4 ld16(__amdgpu_buffer_rsrc_t rs, int off) {
+    return __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+}
 
 // work-item geometry (identical in both roles)
 struct Item {
     int ph, ks, m0, n0;
-    int sb;       // first slab of this K-split
-    int nreal;    // slabs with data
-    int steps;    // max(nreal, 1) rounded up to even
+    int k0;       // first K element of this split
+    int kend;     // one past its last K element
+    int steps;    // max(ceil((kend - k0) / BK), 1)
+};
+
+template <int BN>
+struct Geo {
+    static constexpr int NB = BN / 32;                    // 32-wide N blocks per compute wave
+    static constexpr int ASLOT = BM * 128, BSLOT = BN * 128;
+    static constexpr int SLOT = ASLOT + BSLOT;
+    static constexpr int BLD = BN == 128 ? 4 : 2;         // B loads per loader lane per step
+    static constexpr int NLD = 8 + BLD;                   // loads per loader lane per step
+    static constexpr int LDS = NS * SLOT + MAXTAPS * 8;
 };
 
 template <int BN>
 __global__ __launch_bounds__(512, 1) void k_igemm(ConvArgs a, int mtiles, int ntiles, int nitems) {
-    constexpr int NB = BN / 32;                       // 32-wide N blocks per compute wave
-    constexpr int ASLOT = BM * 64, BSLOT = BN * 64;   // one slab of A / B
-    constexpr int NBL = BN * 4 / 256;                 // B loads per loader lane per step
-    constexpr int NLD = 4 + NBL;                      // loads per loader lane per step
+    using G = Geo<BN>;
+    constexpr int NB = G::NB, ASLOT = G::ASLOT, SLOT = G::SLOT, BLD = G::BLD, NLD = G::NLD;
 
-    extern __shared__ __attribute__((aligned(1024))) char lds[];   // launch: > 80 KB, one workgroup per CU
-    char* const ring = lds;                                        // [2][ASLOT + BSLOT]
-    int2* const tapl = reinterpret_cast<int2*>(lds + 2 * (ASLOT + BSLOT));
+    extern __shared__ __attribute__((aligned(1024))) char lds[];
+    char* const ring = lds;                                        // [NS][ASLOT + BSLOT]
+    int2* const tapl = reinterpret_cast<int2*>(lds + NS * SLOT);
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int w = wave & 3;
-    const int nmine = (nitems - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+    // XCD-aware numbering: workgroups are dealt round-robin to the 8 XCDs (b % 8); renumber so each XCD
+    // walks a contiguous block of work items and its 4 MB L2 holds the im2col window they share
+    const int gx = (int)gridDim.x, b = (int)blockIdx.x;
+    const int vb = gx % 8 == 0 ? (b % 8) * (gx / 8) + b / 8 : b;
+    const int nmine = (nitems - vb + gx - 1) / gx;
     if (nmine <= 0) return;
     const int M = a.N * a.Hq * a.Wq;
 
     auto item = [&](int k) {
         Item it;
-        const int id = (int)blockIdx.x + k * (int)gridDim.x;
+        const int id = vb + k * gx;
         const int nt = id % ntiles, r1 = id / ntiles;
         const int mt = r1 % mtiles, r2 = r1 / mtiles;
         it.ks = r2 % a.ksplit;
         it.ph = r2 / a.ksplit;
         it.m0 = mt * BM;
         it.n0 = nt * BN;
-        const int nslab = a.ph[it.ph].kpad / 32;
-        const int sps = (nslab + a.ksplit - 1) / a.ksplit;
-        it.sb = it.ks * sps;
-        const int se = min(nslab, it.sb + sps);
-        it.nreal = max(se - it.sb, 0);
-        it.steps = (max(it.nreal, 1) + 1) & ~1;
+        const int K = a.ph[it.ph].kpad;
+        const int nst = (K + BK - 1) / BK;
+        const int sps = (nst + a.ksplit - 1) / a.ksplit;
+        it.k0 = min(K, it.ks * sps * BK);
+        it.kend = min(K, it.k0 + sps * BK);
+        it.steps = max((it.kend - it.k0 + BK - 1) / BK, 1);
         return it;
     };
     // total steps of this workgroup, padded to a multiple of LAT (extra steps: barriers only)
@@ -91,7 +113,6 @@ __global__ __launch_bounds__(512, 1) void k_igemm(ConvArgs a, int mtiles, int nt
     if (wave >= 4) {
         // =============================== loader waves ===============================
         const int L = w * 64 + lane;
-        // stage every phase's tap table
         {
             int ntap = 0;
             for (int p = 0; p < a.nphase; ++p) ntap = max(ntap, a.ph[p].tap_off + a.ph[p].ntaps);
@@ -102,17 +123,21 @@ __global__ __launch_bounds__(512, 1) void k_igemm(ConvArgs a, int mtiles, int nt
 
         const __amdgpu_buffer_rsrc_t rsA = make_rsrc(a.in, (long long)a.N * a.in_clip_stride * 2);
         const __amdgpu_buffer_rsrc_t rsB = make_rsrc(a.w, 0x7fffffffLL);
-        const int g = L & 3;               // this lane's 16-B chunk column (A)
+        const int h = L & 1;                // A: which 64-byte half of the 128-byte row
         const int ci = a.Ci;
-        // cursor: the slab being loaded (WD steps ahead of the computing step)
-        int ck = 0, cs = 0;                 // local item, step within item
+        // B lanes: BN = 128: row L >> 1, 64 B at (L & 1) * 64; BN = 64: row L >> 2, 32 B at (L & 3) * 32
+        const int brow = BN == 128 ? (L >> 1) : (L >> 2);
+        const int bbyte = BN == 128 ? (L & 1) * 64 : (L & 3) * 32;
+        // cursor: the step being loaded
+        int ck = 0, cs = 0;
         Item cit = item(0);
-        int rcb[4], riy[4], rix[4];          // A rows r = L/4 + 64u: clip byte base, iy0, ix0 (row < M: rcb >= 0)
-        int kj = 0, kc = 0;                 // tap / channel of this lane's chunk in the current slab
+        int rcb[2], riy[2], rix[2];          // A rows r = L/2 + 128u: clip byte base (< 0: past M), iy0, ix0
+        int kj = 0, kc = 0;                 // tap / channel of this lane's 32 elements in the step
+        int ke = 0;                         // their K index (>= kend: zeros)
         auto set_rows = [&]() {
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int m = cit.m0 + (L >> 2) + 64 * u;
+            for (int u = 0; u < 2; ++u) {
+                const int m = cit.m0 + (L >> 1) + 128 * u;
                 const int mm = m < M ? m : 0;
                 int clip, yq, xq;
                 if (a.pool) {
@@ -131,13 +156,14 @@ __global__ __launch_bounds__(512, 1) void k_igemm(ConvArgs a, int mtiles, int nt
                 riy[u] = yq * a.sy;
                 rix[u] = xq * a.sx;
             }
-            const int e = cit.sb * 32 + g * 8;
-            kj = e / ci;
-            kc = e - kj * ci;
+            ke = cit.k0 + 32 * h;
+            kj = ke / ci;
+            kc = ke - kj * ci;
         };
         set_rows();
         auto advance = [&]() {
-            kc += 32;
+            ke += BK;
+            kc += BK;
             while (kc >= ci) { kc -= ci; ++kj; }
             if (++cs == cit.steps) {
                 cs = 0;
@@ -147,48 +173,46 @@ __global__ __launch_bounds__(512, 1) void k_igemm(ConvArgs a, int mtiles, int nt
                 }
             }
         };
-        // loads of the cursor's slab into a register set (zeros past the item's data / the last item)
-        auto load = [&](i32x4 (&ra)[4], i32x4 (&rb)[NBL]) {
-            const bool live = ck < nmine && cs < cit.nreal;
+        auto load = [&](i32x4 (&ra)[8], i32x4 (&rb)[BLD]) {
+            const int live = (int)(ck < nmine);
             const ConvPhase& ph = a.ph[live ? cit.ph : 0];
             const int2 t = tapl[ph.tap_off + min(kj, ph.ntaps - 1)];
+            const int kok = live & (int)(ke < cit.kend) & (int)(kj < ph.ntaps);
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
+            for (int u = 0; u < 2; ++u) {
                 const int iy = riy[u] + t.x, ix = rix[u] + t.y;
-                const int ok = (int)live & (int)(rcb[u] >= 0) & (int)(kj < ph.ntaps) & (int)((unsigned)iy < (unsigned)a.Hi) &
+                const int ok = kok & (int)(rcb[u] >= 0) & (int)((unsigned)iy < (unsigned)a.Hi) &
                                (int)((unsigned)ix < (unsigned)a.Wi);
-                const int off = rcb[u] + ((iy * a.Wi + ix) * ci + kc) * 2;
-                const int mask = -ok;
-                ra[u] = __builtin_amdgcn_raw_buffer_load_b128(rsA, (off & mask) | (kOOB & ~mask), 0, 0);
-            }
-            const int slab = cit.sb + cs;
+                const int off = rcb[u] + ((iy * a.Wi + ix) * ci + kc) * 2, mask = -ok;
+                const int o = (off & mask) | (kOOB & ~mask);
 #pragma unroll
-            for (int v = 0; v < NBL; ++v) {
-                const int idx = L + 256 * v, row = idx >> 2, gg = idx & 3;
-                const int n = cit.n0 + row;
-                const int ok = (int)live & (int)(n < a.Co);
-                const int off = ((int)ph.w_off + n * ph.kpad + slab * 32 + gg * 8) * 2;
-                const int mask = -ok;
-                rb[v] = __builtin_amdgcn_raw_buffer_load_b128(rsB, (off & mask) | (kOOB & ~mask), 0, 0);
+                for (int j = 0; j < 4; ++j) ra[4 * u + j] = ld16(rsA, o + 16 * j);
             }
+            // B: this step's K window [k0 + cs*BK, +BK) of rows n0 + brow (zeros past Co / past kend)
+            const int kb = cit.k0 + cs * BK + bbyte / 2;
+            const int n = cit.n0 + brow;
+            const int okb = live & (int)(n < a.Co) & (int)(kb < cit.kend), maskb = -okb;
+            const int offb = ((((int)ph.w_off + n * ph.kpad + kb) * 2) & maskb) | (kOOB & ~maskb);
+#pragma unroll
+            for (int j = 0; j < BLD; ++j) rb[j] = ld16(rsB, offb + 16 * j);
         };
-        auto store = [&](int slot, const i32x4 (&ra)[4], const i32x4 (&rb)[NBL]) {
-            char* as = ring + slot * (ASLOT + BSLOT);
+        auto store = [&](int slot, const i32x4 (&ra)[8], const i32x4 (&rb)[BLD]) {
+            char* as = ring + slot * SLOT;
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int row = (L >> 2) + 64 * u;
-                *reinterpret_cast<i32x4*>(as + row * 64 + ((g ^ swz(row)) << 4)) = ra[u];
+            for (int u = 0; u < 2; ++u) {
+                const int row = (L >> 1) + 128 * u;
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    *reinterpret_cast<i32x4*>(as + row * 128 + (((4 * h + j) ^ swz(row)) << 4)) = ra[4 * u + j];
             }
 #pragma unroll
-            for (int v = 0; v < NBL; ++v) {
-                const int idx = L + 256 * v, row = idx >> 2, gg = idx & 3;
-                *reinterpret_cast<i32x4*>(as + ASLOT + row * 64 + ((gg ^ swz(row)) << 4)) = rb[v];
-            }
+            for (int j = 0; j < BLD; ++j)
+                *reinterpret_cast<i32x4*>(as + ASLOT + brow * 128 + (((bbyte / 16 + j) ^ swz(brow)) << 4)) = rb[j];
         };
-        // prologue: slabs of steps 0, 1 straight to LDS; steps 2 .. LAT+1 into the register ring
-        i32x4 ra[LAT][4], rb[LAT][NBL];
+        // prologue: steps 0, 1 straight to LDS slots 0, 1; steps 2 .. LAT+1 into the register ring
+        i32x4 ra[LAT][8], rb[LAT][BLD];
         {
-            i32x4 ta[4], tb[NBL];
+            i32x4 ta[8], tb[BLD];
             load(ta, tb);
             advance();
             wait_vm_lgkm0<0>();
@@ -202,15 +226,15 @@ __global__ __launch_bounds__(512, 1) void k_igemm(ConvArgs a, int mtiles, int nt
             std::make_integer_sequence<int, LAT>{});
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         barrier_raw();
-        barrier_raw();   // the compute waves have read slab 0 (slot 0 is overwritten at step 0)
-        // step t: store the set loaded LAT steps ago (slab of step t+2) into ring slot t&1, load the
-        // slab of step t+WD into the same set
+        // step t: store the set loaded LAT steps ago (step t+2) into slot (t+2) % 3 — its previous
+        // contents (step t-1) were read before the last barrier — and load step t+LAT+2 into that set
+        int sl = 2;
         for (int t = 0; t < total_pad; t += LAT)
             [&]<int... S>(std::integer_sequence<int, S...>) {
-                ((store(S & 1, ra[S], rb[S]), load(ra[S], rb[S]), advance(), wait_vm_lgkm0<(LAT - 1) * NLD>(),
-                  barrier_raw()),
+                ((store(sl, ra[S], rb[S]), load(ra[S], rb[S]), advance(), wait_vm_lgkm0<(LAT - 1) * NLD>(),
+                  barrier_raw(), sl = sl == NS - 1 ? 0 : sl + 1),
                  ...);
-            }(std::make_integer_sequence<int, LAT>{});   // LAT even: slot (t + S) & 1 == S & 1
+            }(std::make_integer_sequence<int, LAT>{});
         wait_vm_lgkm0<0>();
         return;
     }
@@ -218,18 +242,19 @@ __global__ __launch_bounds__(512, 1) void k_igemm(ConvArgs a, int mtiles, int nt
     // =============================== compute waves ===============================
     __builtin_amdgcn_s_setprio(2);
     barrier_raw();   // tap tables
-    barrier_raw();   // prologue slabs
+    barrier_raw();   // prologue steps
     const int r32 = lane & 31, hi = lane >> 5;
     const int asw = swz(r32);
-    auto frags = [&](int slot, i32x4 (&fa)[4], i32x4 (&fb)[2 * NB]) {
-        const char* as = ring + slot * (ASLOT + BSLOT);
+    // fragments of half hf (K 32 hf .. 32 hf + 31) of the step in slot `slot`
+    auto frags = [&](int slot, int hf, i32x4 (&fa)[4], i32x4 (&fb)[2 * NB]) {
+        const char* as = ring + slot * SLOT;
 #pragma unroll
         for (int m = 0; m < 2; ++m) {
-            const int pos = ((2 * m + hi) ^ asw) << 4;
+            const int pos = ((4 * hf + 2 * m + hi) ^ asw) << 4;
 #pragma unroll
-            for (int i = 0; i < 2; ++i) fa[2 * i + m] = *reinterpret_cast<const i32x4*>(as + (64 * w + 32 * i + r32) * 64 + pos);
+            for (int i = 0; i < 2; ++i) fa[2 * i + m] = *reinterpret_cast<const i32x4*>(as + (64 * w + 32 * i + r32) * 128 + pos);
 #pragma unroll
-            for (int jb = 0; jb < NB; ++jb) fb[2 * jb + m] = *reinterpret_cast<const i32x4*>(as + ASLOT + (32 * jb + r32) * 64 + pos);
+            for (int jb = 0; jb < NB; ++jb) fb[2 * jb + m] = *reinterpret_cast<const i32x4*>(as + ASLOT + (32 * jb + r32) * 128 + pos);
         }
     };
     f32x16 acc[2][NB];
@@ -296,13 +321,7 @@ __global__ __launch_bounds__(512, 1) void k_igemm(ConvArgs a, int mtiles, int nt
                 }
         }
     };
-    i32x4 fa[4], fb[2 * NB], na[4], nb[2 * NB];
-    frags(0, fa, fb);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    barrier_raw();   // slab 0 read: the loaders may now overwrite slot 0
-    int t = 0;
-    auto cstep = [&](auto first, i32x4 (&ca)[4], i32x4 (&cb)[2 * NB], i32x4 (&xa)[4], i32x4 (&xb)[2 * NB]) {
-        frags((t + 1) & 1, xa, xb);
+    auto mfma_half = [&](auto first, const i32x4 (&ca)[4], const i32x4 (&cb)[2 * NB]) {
 #pragma unroll
         for (int m = 0; m < 2; ++m)
 #pragma unroll
@@ -318,18 +337,27 @@ __global__ __launch_bounds__(512, 1) void k_igemm(ConvArgs a, int mtiles, int nt
             __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
         }
         __builtin_amdgcn_sched_barrier(0);
+    };
+    // X: first half of the current step (read during the previous step), Y: its second half
+    i32x4 xa[4], xb[2 * NB], ya[4], yb[2 * NB];
+    int slot = 0;
+    frags(0, 0, xa, xb);
+    int t = 0;
+    auto cstep = [&](auto first) {
+        const int nslot = slot == NS - 1 ? 0 : slot + 1;
+        frags(slot, 1, ya, yb);
+        mfma_half(first, xa, xb);
+        frags(nslot, 0, xa, xb);
+        mfma_half(std::false_type{}, ya, yb);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         barrier_raw();
+        slot = nslot;
         ++t;
     };
     for (int k = 0; k < nmine; ++k) {
         const Item it = item(k);
-        cstep(std::true_type{}, fa, fb, na, nb);
-        cstep(std::false_type{}, na, nb, fa, fb);
-        for (int s = 2; s < it.steps; s += 2) {
-            cstep(std::false_type{}, fa, fb, na, nb);
-            cstep(std::false_type{}, na, nb, fa, fb);
-        }
+        cstep(std::true_type{});
+        for (int s = 1; s < it.steps; ++s) cstep(std::false_type{});
         epilogue(it);
     }
     for (; t < total_pad; ++t) barrier_raw();   // the loaders' padding steps
@@ -340,9 +368,9 @@ __global__ __launch_bounds__(512, 1) void k_igemm(ConvArgs a, int mtiles, int nt
 int choose_ksplit_ws(long long M, int Co, int kpad) {
     const int BN = Co <= 64 ? 64 : 128;
     const long long items = ((M + BM - 1) / BM) * ((Co + BN - 1) / BN);
-    const int nslab = kpad / 32;
+    const int nstep = (kpad + BK - 1) / BK;
     int ks = 1;
-    while (items * ks < 256 && nslab / (ks * 2) >= 8) ks *= 2;
+    while (items * ks < 256 && nstep / (ks * 2) >= 4) ks *= 2;
     return ks;
 }
 
@@ -352,6 +380,10 @@ int launch_igemm(const ConvArgs& a, hipStream_t s) {
     if (a.ksplit < 1 || (a.ksplit > 1 && (a.nphase != 1 || !a.partial))) {
         set_error("bad split-K configuration");
         return 1;
+    }
+    if (a.Ci % 32) {
+        set_error("igemm: Ci must be a multiple of 32");
+        return 3;
     }
     for (int p = 0; p < a.nphase; ++p)
         if (a.ph[p].tap_off + a.ph[p].ntaps > MAXTAPS || a.ph[p].kpad % 32) {
@@ -369,16 +401,16 @@ int launch_igemm(const ConvArgs& a, hipStream_t s) {
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
     const int gx = nitems < ncu ? nitems : ncu;
-    // 2 x (A + B) slab ring + tap table = 49 KB used; 84 KB requested so a CU never holds two workgroups
-    constexpr int kLds = 84 * 1024;
     static bool attr = false;
     if (!attr) {
-        AVSE_HIP_CHECK(hipFuncSetAttribute((const void*)k_igemm<64>, hipFuncAttributeMaxDynamicSharedMemorySize, kLds));
-        AVSE_HIP_CHECK(hipFuncSetAttribute((const void*)k_igemm<128>, hipFuncAttributeMaxDynamicSharedMemorySize, kLds));
+        AVSE_HIP_CHECK(hipFuncSetAttribute((const void*)k_igemm<64>, hipFuncAttributeMaxDynamicSharedMemorySize, Geo<64>::LDS));
+        AVSE_HIP_CHECK(hipFuncSetAttribute((const void*)k_igemm<128>, hipFuncAttributeMaxDynamicSharedMemorySize, Geo<128>::LDS));
         attr = true;
     }
-    if (BN == 64) hipLaunchKernelGGL(k_igemm<64>, dim3(gx), dim3(512), kLds, s, a, mtiles, ntiles, nitems);
-    else hipLaunchKernelGGL(k_igemm<128>, dim3(gx), dim3(512), kLds, s, a, mtiles, ntiles, nitems);
+    // both sizes exceed 80 KB: one workgroup per CU
+    static_assert(Geo<64>::LDS > 80 * 1024 && Geo<128>::LDS <= 160 * 1024, "igemm LDS budget");
+    if (BN == 64) hipLaunchKernelGGL(k_igemm<64>, dim3(gx), dim3(512), Geo<64>::LDS, s, a, mtiles, ntiles, nitems);
+    else hipLaunchKernelGGL(k_igemm<128>, dim3(gx), dim3(512), Geo<128>::LDS, s, a, mtiles, ntiles, nitems);
     AVSE_HIP_CHECK(hipGetLastError());
     if (a.ksplit > 1) return launch_splitk_reduce(a, 1, s);
     return 0;

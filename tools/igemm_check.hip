@@ -43,14 +43,14 @@ int main() {
     hipDeviceSynchronize();
     std::vector<float> P((size_t)KS * M * Co);
     hipMemcpy(P.data(), dP, P.size() * 4, hipMemcpyDeviceToHost);
-    const int nslab = K / 32, sps = (nslab + KS - 1) / KS;
+    const int nst = (K + 63) / 64, sps = (nst + KS - 1) / KS;   // 64-deep steps per split
     for (int z = 0; z < KS; ++z) {
         double e2 = 0, r2 = 0;
         int bad = 0;
         for (int m = 0; m < M; ++m)
             for (int n = 0; n < Co; ++n) {
                 double ref = 0;
-                for (int k = z * sps * 32; k < std::min(K, (z + 1) * sps * 32); ++k)
+                for (int k = std::min(K, z * sps * 64); k < std::min(K, (z + 1) * sps * 64); ++k)
                     ref += (double)bf2f(A[(size_t)m * K + k]) * bf2f(W[(size_t)n * K + k]);
                 const double got = P[((size_t)z * M + m) * Co + n];
                 e2 += (got - ref) * (got - ref);
@@ -68,7 +68,7 @@ int main() {
             double e = 0;
             for (int n = 0; n < 8; ++n) {
                 double ref = 0;
-                for (int k = 0; k < sps * 32; ++k) ref += (double)bf2f(A[(size_t)mr * K + k]) * bf2f(W[(size_t)n * K + k]);
+                for (int k = 0; k < std::min(K, sps * 64); ++k) ref += (double)bf2f(A[(size_t)mr * K + k]) * bf2f(W[(size_t)n * K + k]);
                 const double d = P[(size_t)m * Co + n] - ref;
                 e += d * d;
             }
