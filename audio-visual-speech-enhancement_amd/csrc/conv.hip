@@ -18,12 +18,15 @@
 // A (im2col gathered on the fly, 16-byte chunks, zero padding = TF 'SAME') and B (packed weights
 // [Cout][Kpad]) are register-staged into a double-buffered, XOR-swizzled LDS tile (one barrier
 // per slab; the next slab's global loads are in flight during the current slab's MFMAs).
+#include <type_traits>
+
 #include "avse_common.h"
 
 namespace avse {
 namespace {
 
 constexpr int BM = 128;
+constexpr int MAX_TAPS_LDS = 64;   // taps of one phase (largest: 25)
 constexpr float LRELU = 0.3f;
 
 template <typename T> struct Vec16;
@@ -62,6 +65,9 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
     constexpr int BCH = BN * 4 / 256;           // B chunks per thread
 
     __shared__ __attribute__((aligned(16))) char lds[2 * (BM + BN) * 64];
+    // this phase's tap table, staged in LDS: a per-lane global tap load feeding the A addresses made every
+    // slab wait for vmcnt — which retires in order, so it also drained all the slabs in flight
+    __shared__ int2 tap_lds[MAX_TAPS_LDS];
     // buffer b: A tile at lds + b*(BM+BN)*64, B tile right after it
 #define AS(b) (lds + (b) * (BM + BN) * 64)
 #define BS(b) (lds + (b) * (BM + BN) * 64 + BM * 64)
@@ -80,7 +86,8 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
     const int sps = (nslab_all + a.ksplit - 1) / a.ksplit;
     const int s_begin = zsplit * sps;
     const int s_end = min(nslab_all, s_begin + sps);
-    const int2* __restrict__ taps = a.taps + ph.tap_off;
+    for (int i = threadIdx.x; i < ph.ntaps && i < MAX_TAPS_LDS; i += 256) tap_lds[i] = a.taps[ph.tap_off + i];
+    __syncthreads();
 
     // ---- per-thread A rows (2 chunks: rows r and r + 64, same chunk column g) ----
     const int g = tid & 3;
@@ -120,11 +127,14 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
     const __amdgpu_buffer_rsrc_t rsB = make_rsrc(reinterpret_cast<const char*>(a.w) + ph.w_off * sizeof(T),
                                                  (long long)a.Co * ph.kpad * sizeof(T));
 
-    i32x4 ra[2], rb[BCH];
-    auto load_slab = [&](int s) {
+    // P register stages: slabs s+1 .. s+P-1 are in flight while slab s computes (a layer with a short K loop
+    // was a serial chain of one global-load latency per slab: ~0.7-1.2 us each, measured at batch 8)
+    constexpr int P = 3;
+    i32x4 ras[P][2], rbs[P][BCH];
+    auto load_slab = [&](int s, i32x4 (&ra)[2], i32x4 (&rb)[BCH]) {
         // A
         const bool tap_ok = kj < ph.ntaps;
-        const int2 t = taps[tap_ok ? kj : ph.ntaps - 1];
+        const int2 t = tap_lds[tap_ok ? kj : ph.ntaps - 1];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const int iy = ri[h].iy0 + t.x, ix = ri[h].ix0 + t.y;
@@ -145,7 +155,7 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
         kc += SLAB;
         while (kc >= a.Ci) { kc -= a.Ci; ++kj; }
     };
-    auto store_slab = [&](int buf) {
+    auto store_slab = [&](int buf, const i32x4 (&ra)[2], const i32x4 (&rb)[BCH]) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const int row = (tid >> 2) + 64 * h;
@@ -167,13 +177,17 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
 
     const int fr = lane & 15, fg = lane >> 4;
     if (s_begin < s_end) {
-    load_slab(s_begin);
-    store_slab(0);
+    // loads past s_end read zeros (taps past ntaps / rows past the phase's weights are out of range)
+#pragma unroll
+    for (int p = 0; p < P; ++p) load_slab(s_begin + p, ras[p], rbs[p]);
+    store_slab(0, ras[0], rbs[0]);
+    load_slab(s_begin + P, ras[0], rbs[0]);   // set of slab x: (x - s_begin) % P
     __syncthreads();
 
-    for (int s = s_begin; s < s_end; ++s) {
+    auto step = [&](auto qidx, int s) {
+        constexpr int q = decltype(qidx)::value;           // (s - s_begin) % P
+        constexpr int qn = (q + 1) % P;
         const int buf = (s - s_begin) & 1;
-        if (s + 1 < s_end) load_slab(s + 1);
         i32x4 fa[NI], fb[NJ];
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
@@ -200,8 +214,16 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
                         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], bv[e], acc[i][j], 0, 0, 0);
                 }
             }
-        if (s + 1 < s_end) store_slab(buf ^ 1);
+        if (s + 1 < s_end) {
+            store_slab(buf ^ 1, ras[qn], rbs[qn]);   // slab s+1, loaded P-1 steps ago
+            load_slab(s + 1 + P, ras[qn], rbs[qn]);  // refill with slab s+1+P (the load cursor is sequential)
+        }
         __syncthreads();
+    };
+    for (int s = s_begin; s < s_end; s += P) {
+        step(std::integral_constant<int, 0>{}, s);
+        if (s + 1 < s_end) step(std::integral_constant<int, 1>{}, s + 1);
+        if (s + 2 < s_end) step(std::integral_constant<int, 2>{}, s + 2);
     }
     }
 
@@ -405,6 +427,11 @@ int launch_conv(const ConvArgs& a, int dtype, hipStream_t s) {
         set_error("bad split-K configuration");
         return 1;
     }
+    for (int p = 0; p < a.nphase; ++p)
+        if (a.ph[p].ntaps > MAX_TAPS_LDS) {
+            set_error("k_conv: too many taps in one phase");
+            return 3;
+        }
     dim3 grid((M + BM - 1) / BM, (a.Co + BN - 1) / BN, a.nphase * a.ksplit);
     if (dtype == 1) {
         if (BN == 64) hipLaunchKernelGGL((k_conv<bf16_t, 64>), grid, dim3(256), 0, s, a);
