@@ -247,6 +247,31 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
         return;
     }
     T* out = reinterpret_cast<T*>(a.out);
+    // output row -> element offset, decomposed once per (fragment, row) instead of per element: the
+    // three runtime integer divisions per stored value used to be the floor of every short-K layer
+    long long orow[NI][4];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+        const int mb = m0 + wm * 64 + 16 * i + 4 * fg;   // first of this lane's 4 rows
+        if (a.pool) {
+            const int p = mb >> 2;
+            const int pw = a.Wq >> 1, phh = a.Hq >> 1;
+            const int clip = p / (phh * pw);
+            const int r = p - clip * phh * pw;
+            orow[i][0] = mb < M ? clip * a.out_clip_stride + (long long)r * a.out_pix_stride + a.out_c_off : -1;
+        } else {
+            const int hw = a.Hq * a.Wq;
+            int clip = mb / hw;
+            int rr = mb - clip * hw;
+            int yq = rr / a.Wq, xq = rr - yq * a.Wq;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int oy = yq * a.oys + ph.py, ox = xq * a.oxs + ph.px;
+                orow[i][r] = mb + r < M ? clip * a.out_clip_stride + (long long)(oy * a.Wo + ox) * a.out_pix_stride + a.out_c_off : -1;
+                if (++xq == a.Wq) { xq = 0; if (++yq == a.Hq) { yq = 0; ++clip; } }
+            }
+        }
+    }
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
         const int n = n0 + wn * WN + 16 * j + fr;
@@ -254,32 +279,21 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
         const float sc = a.scale[n], sh = a.shift[n];
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
-            const int mb = m0 + wm * 64 + 16 * i + 4 * fg;   // first of this lane's 4 rows
-            if (mb >= M) continue;
             float v[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] * sc + sh;
             if (a.pool) {
+                if (orow[i][0] < 0) continue;
                 float x = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
                 if (a.act) x = x >= 0.f ? x : LRELU * x;
-                const int p = mb >> 2;
-                const int pw = a.Wq >> 1, phh = a.Hq >> 1;
-                const int clip = p / (phh * pw);
-                const int r = p - clip * phh * pw;
-                const long long o = clip * a.out_clip_stride + (long long)r * a.out_pix_stride + a.out_c_off + n;
-                out[o] = from_f<T>(x);
+                out[orow[i][0] + n] = from_f<T>(x);
             } else {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const int m = mb + r;
-                    if (m >= M) break;
+                    if (orow[i][r] < 0) continue;
                     float x = v[r];
                     if (a.act) x = x >= 0.f ? x : LRELU * x;
-                    const int clip = m / (a.Hq * a.Wq);
-                    const int rr = m - clip * a.Hq * a.Wq;
-                    const int oy = (rr / a.Wq) * a.oys + ph.py, ox = (rr % a.Wq) * a.oxs + ph.px;
-                    const long long o = clip * a.out_clip_stride + (long long)(oy * a.Wo + ox) * a.out_pix_stride + a.out_c_off + n;
-                    out[o] = from_f<T>(x);
+                    out[orow[i][r] + n] = from_f<T>(x);
                 }
             }
         }
