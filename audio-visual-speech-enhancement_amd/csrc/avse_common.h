@@ -109,6 +109,11 @@ struct ConvArgs {
     int nphase;
     int ksplit;          // >1: split-K over blockIdx.z, fp32 partials + k_splitk_reduce (nphase == 1)
     float* partial;      // [ksplit][M][Co] workspace
+    // fused trailing 1x1 Cout -> 1 layer (d_deconv6, network.py:133): out_f[pixel] = bias + sum_c w[c] * y[c],
+    // y = this layer's output rounded to T; the T output is not stored (Co == 64, ksplit == 1, no pool)
+    const float* fuse_w;
+    float fuse_bias;
+    float* fuse_out;
     ConvPhase ph[MAX_PHASES];
 };
 

@@ -224,6 +224,13 @@ bool no_igemm() {
     }();
     return v;
 }
+// AVSE_UNFUSED_TAIL=1 (read per forward, for the layer-by-layer tests): run d_deconv6 as its own kernel so the
+// 64-channel d_deconv5 activation is materialised in the scratch buffer avse_debug_scratch exposes
+bool unfused_tail() {
+    const char* e = std::getenv("AVSE_UNFUSED_TAIL");
+    return e && e[0] == '1';
+}
+
 int run_conv(const ConvArgs& a, int dtype, hipStream_t s) {
     if (dtype == AVSE_BF16 && !no_igemm() && a.Ci % 32 == 0) return launch_igemm(a, s);
     return launch_conv(a, dtype, s);
@@ -854,10 +861,24 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
     for (int i = 0; i < 5; ++i) {
         const GpuLayer& G = L(14 + i);
         const long long in_cs = (long long)G.def.hin * G.def.win * G.def.cin;
+        if (i == 4 && !unfused_tail()) {
+            // d_deconv5 with d_deconv6 (1x1, 64 -> 1, network.py:133) fused into its epilogue: the 64-channel
+            // [N, 80, 20] activation is never written; orow addresses the float output pixel directly
+            ConvArgs a = conv_args(G, buf(d_in[i]), in_cs, nullptr, (long long)G.ho * G.wo, 1, 0, N);
+            a.fuse_w = W->d6_w;
+            a.fuse_bias = W->d6_bias;
+            a.fuse_out = out;
+            if ((rc = launch_conv(a, dt, s)) || (rc = mark())) return rc;
+            continue;
+        }
         ConvArgs a = conv_args(G, buf(d_in[i]), in_cs, buf(d_in[i + 1]), (long long)G.ho * G.wo * G.def.cout, G.def.cout, 0, N);
         if ((rc = run_conv(a, dt, s)) || (rc = mark())) return rc;
     }
-    if ((rc = launch_out_conv(buf(B_D5), W->d6_w, W->d6_bias, out, N * 80 * 20, dt, s)) || (rc = mark())) return rc;
+    if (unfused_tail()) {
+        if ((rc = launch_out_conv(buf(B_D5), W->d6_w, W->d6_bias, out, N * 80 * 20, dt, s)) || (rc = mark())) return rc;
+    } else if ((rc = mark())) {   // d_deconv6: fused into d_deconv5 above
+        return rc;
+    }
     return 0;
 }
 }  // namespace

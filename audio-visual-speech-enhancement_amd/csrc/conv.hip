@@ -272,6 +272,51 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
             }
         }
     }
+    if constexpr (BN == 64) {
+        if (a.fuse_w) {   // d_deconv5 + d_deconv6: 64 -> 1 dot in the epilogue (all 64 channels are in this tile)
+            float part[NI][4];
+#pragma unroll
+            for (int i = 0; i < NI; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) part[i][r] = 0.f;
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const int n = wn * WN + 16 * j + fr;
+                const float sc = a.scale[n], sh = a.shift[n], wf = a.fuse_w[n];
+#pragma unroll
+                for (int i = 0; i < NI; ++i)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        float x = acc[i][j][r] * sc + sh;
+                        if (a.act) x = x >= 0.f ? x : LRELU * x;
+                        part[i][r] = fmaf(to_f(from_f<T>(x)), wf, part[i][r]);
+                    }
+            }
+            // sum over the 16 lanes holding the same rows (lane bits 0..3 = column within a fragment)
+#pragma unroll
+            for (int i = 0; i < NI; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int o = 1; o < 16; o <<= 1) part[i][r] += __shfl_xor(part[i][r], o);
+            // then over the two column halves (wn = 0, 1) through LDS (the K loop ended on a barrier)
+            float* red = reinterpret_cast<float*>(lds);
+            if (wn == 1 && fr == 0)
+#pragma unroll
+                for (int i = 0; i < NI; ++i)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) red[wm * 64 + 16 * i + 4 * fg + r] = part[i][r];
+            __syncthreads();
+            if (wn == 0 && fr == 0)
+#pragma unroll
+                for (int i = 0; i < NI; ++i)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (orow[i][r] >= 0)
+                            a.fuse_out[orow[i][r]] = part[i][r] + red[wm * 64 + 16 * i + 4 * fg + r] + a.fuse_bias;
+            return;
+        }
+    }
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
         const int n = n0 + wn * WN + 16 * j + fr;
@@ -439,6 +484,10 @@ int launch_conv(const ConvArgs& a, int dtype, hipStream_t s) {
     const int BN = (a.Co <= 64) ? 64 : 128;
     if (a.ksplit < 1 || (a.ksplit > 1 && (a.nphase != 1 || !a.partial))) {
         set_error("bad split-K configuration");
+        return 1;
+    }
+    if (a.fuse_w && (a.Co != 64 || a.ksplit != 1 || a.pool || !a.fuse_out)) {
+        set_error("k_conv: fused 1x1 tail needs Co == 64, no split-K, no pool");
         return 1;
     }
     for (int p = 0; p < a.nphase; ++p)

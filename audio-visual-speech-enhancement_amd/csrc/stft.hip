@@ -12,8 +12,8 @@
 //   step 2: lane (f, k2 in [0,20)) does a 16-point DFT (4 x 4) over n1 -> Z[k2 + 20 k1]
 //   step 3: lane (f, k) untangles X[k], X[320-k] from Z[k], Z[320-k]  -> |X| in LDS
 //   step 4: lane (f, mel band) sparse Slaney dot (<= max_width bins) -> dB
-// Each 64-lane block handles one chunk of up to 21 frames of one utterance, 3 frames per
-// pass (48 / 60 active lanes in steps 1 / 2).  When the chunk covers the whole utterance (the
+// Each 448-lane block handles one chunk of up to 21 frames of one utterance, 3 frames per
+// wave (48 / 60 active lanes in steps 1 / 2).  When the chunk covers the whole utterance (the
 // 200-ms segment case: 3200 samples -> 21 frames) the top_db clamp (max over the WHOLE
 // [80, T] array, including the frame the slicing later drops) happens in-kernel; otherwise each
 // chunk publishes its max with an ordered-uint atomicMax and a clamp kernel follows.
@@ -29,7 +29,6 @@ namespace {
 constexpr int FPG = 3;          // frames per pass
 constexpr int CHUNK = 21;       // frames per block (7 passes)
 constexpr int ZS = 340;         // float2 slots per frame in LDS (20 rows x 17, padded)
-constexpr int MS = 324;         // floats per frame of |X| (321 used)
 
 __device__ __forceinline__ float sample_at(const float* __restrict__ s, long long L, long long i, int pad_mode) {
     if (i < 0) {
@@ -64,124 +63,165 @@ __device__ __forceinline__ long long out_index(int spf, int n_slices, int n_mels
     return (u * n_mels + m) * (long long)T + t;
 }
 
-// One 64-lane block per (chunk of CHUNK frames, utterance).
-__global__ __launch_bounds__(64) void k_spec640(SpecArgs a, int n_chunks) {
-    __shared__ float2 zbuf[FPG * ZS];
-    __shared__ float mbuf[FPG * MS];
-    __shared__ float dbuf[80 * CHUNK];
+// One block per (chunk of CHUNK frames, utterance): wave w owns frames [3w, 3w + 3) of the chunk, so a
+// 21-frame chunk is one pass of 7 waves (was one 64-lane wave walking 7 passes: ~110 us of serial
+// latency per utterance).  Twiddles, window and the Slaney table live in LDS — the per-weight global
+// loads of the mel dot were a dependent-latency chain.  |X| of a frame aliases its FFT buffer.
+constexpr int WAVES = CHUNK / FPG;     // 7
+constexpr int MEL_LDS_CAP = 6144;      // floats of the [n_mels][max_width] table staged in LDS
 
-    const int lane = threadIdx.x;
+template <bool MEL_LDS>
+__global__ __launch_bounds__(64 * WAVES) void k_spec640(SpecArgs a, int n_chunks) {
+    __shared__ float2 zbuf[WAVES * FPG * ZS];
+    __shared__ float dbuf[80 * CHUNK];
+    __shared__ float2 twl[640];
+    __shared__ float2 winl[320];
+    __shared__ float wmax[WAVES];
+    extern __shared__ __attribute__((aligned(16))) float mel_sm[];   // [n_mels * mw] weights, start, width
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int chunk = blockIdx.x;
     const long long u = blockIdx.y;
     const int T = a.n_frames;
     const int t0 = chunk * CHUNK;
     const int nf = min(CHUNK, T - t0);
+    const int g = FPG * wave;                       // this wave's first frame in the chunk
+    const int ng = max(0, min(FPG, nf - g));
     const long long L = a.n_samples;
     const float* __restrict__ sig = a.sig + u * L;
-    const float2* __restrict__ tw = a.twiddle;   // W640^k
-    const float* __restrict__ win = a.window;
-    const int n_mels = a.n_mels;
-    float vmax = -INFINITY;
+    const int n_mels = a.n_mels, mw = a.mel_max_width;
+    float* mel_w = mel_sm;
+    int* mel_st = reinterpret_cast<int*>(mel_sm + (MEL_LDS ? n_mels * mw : 0));
+    int* mel_wd = mel_st + n_mels;
 
-    for (int g = 0; g < nf; g += FPG) {
-        const int ng = min(FPG, nf - g);
-        // ---- step 1: 20-point DFTs over n2, lane = (f, n1) ----
-        {
-            const int f = lane >> 4, n1 = lane & 15;
-            if (f < ng) {
-                const long long s0 = (long long)(t0 + g + f) * a.hop - 320;
-                float2 v[20];
-#pragma unroll
-                for (int n2 = 0; n2 < 20; ++n2) {
-                    const int n = n1 + 16 * n2;
-                    float2 x = sample_pair(sig, L, s0 + 2 * n, a.pad_mode);
-                    float2 w = *reinterpret_cast<const float2*>(win + 2 * n);
-                    v[n2] = make_float2(x.x * w.x, x.y * w.y);
-                }
-                dft20(v, tw);
-                // v[5c + d] = Y[c + 4d]; twiddle W320^{n1 k2} = W640^{2 n1 k2}
-                float2* zf = zbuf + f * ZS;
-#pragma unroll
-                for (int c = 0; c < 4; ++c)
-#pragma unroll
-                    for (int d = 0; d < 5; ++d) {
-                        const int k2 = c + 4 * d;
-                        float2 y = v[5 * c + d];
-                        if (k2) y = cmul(y, tw[(2 * n1 * k2) % 640]);
-                        zf[k2 * 17 + n1] = y;
-                    }
-            }
-        }
-        __syncthreads();
-        // ---- step 2: 16-point DFTs over n1, lane = (f, k2) ----
-        {
-            const int f = lane / 20, k2 = lane - 20 * (lane / 20);
-            const bool act = f < ng;
-            float2 v[16];
-            float2* zf = zbuf + min(f, FPG - 1) * ZS;
-            if (act) {
-#pragma unroll
-                for (int n1 = 0; n1 < 16; ++n1) v[n1] = zf[k2 * 17 + n1];
-            }
-            __syncthreads();
-            if (act) {
-                dft16(v, tw);
-                // v[4c + d] = Z[k2 + 20 (c + 4d)]
-#pragma unroll
-                for (int c = 0; c < 4; ++c)
-#pragma unroll
-                    for (int d = 0; d < 4; ++d) zf[k2 + 20 * (c + 4 * d)] = v[4 * c + d];
-            }
-        }
-        __syncthreads();
-        // ---- step 3: real-FFT untangling + magnitude, item = (f, k), k in [0,160] ----
-        for (int it = lane; it < ng * 161; it += 64) {
-            const int f = it / 161, k = it - 161 * f;
-            const float2* zf = zbuf + f * ZS;
-            const float2 zk = zf[k];
-            const float2 zm = zf[k == 0 ? 0 : 320 - k];
-            // E = (Zk + conj Zm)/2 ; O = -i/2 (Zk - conj Zm)
-            const float2 E = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y));
-            const float2 O = make_float2(0.5f * (zk.y + zm.y), -0.5f * (zk.x - zm.x));
-            const float2 WO = cmul(tw[k], O);
-            const float2 X = cadd(E, WO);
-            const float2 Xm = make_float2(E.x - WO.x, -(E.y - WO.y));   // X[320 - k] = conj(E - W^k O)
-            float* mf = mbuf + f * MS;
-            mf[k] = sqrtf(X.x * X.x + X.y * X.y);
-            mf[320 - k] = sqrtf(Xm.x * Xm.x + Xm.y * Xm.y);
-            if (a.stft_ri) {
-                const long long t = t0 + g + f;
-                float2* o = reinterpret_cast<float2*>(a.stft_ri);
-                o[(u * 321 + k) * T + t] = X;
-                if (k != 160) o[(u * 321 + (320 - k)) * T + t] = Xm;
-            }
-        }
-        __syncthreads();
-        // ---- step 4: Slaney mel + dB, item = (f, m) ----
-        for (int it = lane; it < ng * n_mels; it += 64) {
-            const int f = it / n_mels, m = it - n_mels * f;
-            const float* mf = mbuf + f * MS + a.mel_start[m];
-            const float* wm = a.mel_weight + m * a.mel_max_width;
-            const int wdt = a.mel_width[m];
-            float acc = 0.f;
-            for (int j = 0; j < wdt; ++j) acc = fmaf(mf[j], wm[j], acc);
-            const float db = acc > a.amin ? 20.0f * log10f(acc) : a.db_floor;
-            vmax = fmaxf(vmax, db);
-            dbuf[m * CHUNK + g + f] = db;
-        }
-        __syncthreads();
+    for (int i = tid; i < 640; i += 64 * WAVES) twl[i] = a.twiddle[i];
+    for (int i = tid; i < 320; i += 64 * WAVES) winl[i] = reinterpret_cast<const float2*>(a.window)[i];
+    if (MEL_LDS)
+        for (int i = tid; i < n_mels * mw; i += 64 * WAVES) mel_w[i] = a.mel_weight[i];
+    for (int i = tid; i < n_mels; i += 64 * WAVES) {
+        mel_st[i] = a.mel_start[i];
+        mel_wd[i] = a.mel_width[i];
     }
-    // ---- block max + clamp / publish ----
+    // samples of step 1 (issued before the table barrier so their latency overlaps it)
+    const int f1 = lane >> 4, n1 = lane & 15;
+    float2 x[20];
+    if (f1 < ng) {
+        const long long s0 = (long long)(t0 + g + f1) * a.hop - 320;
+#pragma unroll
+        for (int n2 = 0; n2 < 20; ++n2) x[n2] = sample_pair(sig, L, s0 + 2 * (n1 + 16 * n2), a.pad_mode);
+    }
+    __syncthreads();
+
+    float2* zw = zbuf + wave * FPG * ZS;
+    // ---- step 1: 20-point DFTs over n2, lane = (f, n1) ----
+    if (f1 < ng) {
+        float2 v[20];
+#pragma unroll
+        for (int n2 = 0; n2 < 20; ++n2) {
+            const float2 w = winl[n1 + 16 * n2];
+            v[n2] = make_float2(x[n2].x * w.x, x[n2].y * w.y);
+        }
+        dft20(v, twl);
+        // v[5c + d] = Y[c + 4d]; twiddle W320^{n1 k2} = W640^{2 n1 k2}
+        float2* zf = zw + f1 * ZS;
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int d = 0; d < 5; ++d) {
+                const int k2 = c + 4 * d;
+                float2 y = v[5 * c + d];
+                if (k2) y = cmul(y, twl[(2 * n1 * k2) % 640]);
+                zf[k2 * 17 + n1] = y;
+            }
+    }
+    __syncthreads();
+    // ---- step 2: 16-point DFTs over n1, lane = (f, k2) ----
+    {
+        const int f = lane / 20, k2 = lane - 20 * (lane / 20);
+        const bool act = f < ng;
+        float2 v[16];
+        float2* zf = zw + min(f, FPG - 1) * ZS;
+        if (act) {
+#pragma unroll
+            for (int n = 0; n < 16; ++n) v[n] = zf[k2 * 17 + n];
+        }
+        __syncthreads();
+        if (act) {
+            dft16(v, twl);
+            // v[4c + d] = Z[k2 + 20 (c + 4d)]
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+#pragma unroll
+                for (int d = 0; d < 4; ++d) zf[k2 + 20 * (c + 4 * d)] = v[4 * c + d];
+        }
+    }
+    __syncthreads();
+    // ---- step 3: real-FFT untangling + magnitude, item = (f, k), k in [0,160]; |X| overwrites Z ----
+    constexpr int IT3 = (FPG * 161 + 63) / 64;
+    float mk[IT3], mm[IT3];
+#pragma unroll
+    for (int j = 0; j < IT3; ++j) {
+        const int it = lane + 64 * j;
+        if (it >= ng * 161) break;
+        const int f = it / 161, k = it - 161 * f;
+        const float2* zf = zw + f * ZS;
+        const float2 zk = zf[k];
+        const float2 zm = zf[k == 0 ? 0 : 320 - k];
+        // E = (Zk + conj Zm)/2 ; O = -i/2 (Zk - conj Zm)
+        const float2 E = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y));
+        const float2 O = make_float2(0.5f * (zk.y + zm.y), -0.5f * (zk.x - zm.x));
+        const float2 WO = cmul(twl[k], O);
+        const float2 X = cadd(E, WO);
+        const float2 Xm = make_float2(E.x - WO.x, -(E.y - WO.y));   // X[320 - k] = conj(E - W^k O)
+        mk[j] = sqrtf(X.x * X.x + X.y * X.y);
+        mm[j] = sqrtf(Xm.x * Xm.x + Xm.y * Xm.y);
+        if (a.stft_ri) {
+            const long long t = t0 + g + f;
+            float2* o = reinterpret_cast<float2*>(a.stft_ri);
+            o[(u * 321 + k) * T + t] = X;
+            if (k != 160) o[(u * 321 + (320 - k)) * T + t] = Xm;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < IT3; ++j) {
+        const int it = lane + 64 * j;
+        if (it >= ng * 161) break;
+        const int f = it / 161, k = it - 161 * f;
+        float* mf = reinterpret_cast<float*>(zw + f * ZS);
+        mf[k] = mk[j];
+        mf[320 - k] = mm[j];
+    }
+    __syncthreads();
+    // ---- step 4: Slaney mel + dB, item = (f, m) ----
+    float vmax = -INFINITY;
+    for (int it = lane; it < ng * n_mels; it += 64) {
+        const int f = it / n_mels, m = it - n_mels * f;
+        const float* mf = reinterpret_cast<const float*>(zw + f * ZS) + mel_st[m];
+        const float* wm = MEL_LDS ? mel_w + m * mw : a.mel_weight + m * mw;
+        const int wdt = mel_wd[m];
+        float acc = 0.f;
+        for (int j = 0; j < wdt; ++j) acc = fmaf(mf[j], wm[j], acc);
+        const float db = acc > a.amin ? 20.0f * log10f(acc) : a.db_floor;
+        vmax = fmaxf(vmax, db);
+        dbuf[m * CHUNK + g + f] = db;
+    }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) vmax = fmaxf(vmax, __shfl_xor(vmax, o));
+    if (lane == 0) wmax[wave] = vmax;
+    __syncthreads();
+    vmax = wmax[0];
+#pragma unroll
+    for (int w = 1; w < WAVES; ++w) vmax = fmaxf(vmax, wmax[w]);
+    // ---- clamp / publish ----
     const bool single = (n_chunks == 1);
     const float floor_db = (single && a.top_db >= 0.f) ? vmax - a.top_db : -INFINITY;
-    for (int it = lane; it < n_mels * nf; it += 64) {
+    for (int it = tid; it < n_mels * nf; it += 64 * WAVES) {
         const int m = it / nf, tl = it - nf * m;
         const long long oi = out_index(a.spf, a.n_slices, n_mels, T, u, m, t0 + tl);
         if (oi >= 0) a.mel_db[oi] = fmaxf(dbuf[m * CHUNK + tl], floor_db);
     }
-    if (!single && lane == 0) atomicMax(a.umax + u, f2ord(vmax));
+    if (!single && tid == 0) atomicMax(a.umax + u, f2ord(vmax));
 }
 
 // Direct DFT fallback for n_fft != 640: one 256-thread block per (frame, utterance).
@@ -245,7 +285,12 @@ int launch_spectrogram(const SpecArgs& a, hipStream_t s) {
     if (a.n_fft == 640) {
         const int n_chunks = (a.n_frames + CHUNK - 1) / CHUNK;
         if (n_chunks > 1) AVSE_HIP_CHECK(hipMemsetAsync(a.umax, 0, sizeof(unsigned) * a.n_utt, s));
-        hipLaunchKernelGGL(k_spec640, dim3(n_chunks, (unsigned)a.n_utt), dim3(64), 0, s, a, n_chunks);
+        const bool mel_lds = a.n_mels * a.mel_max_width <= MEL_LDS_CAP;
+        const size_t shm = sizeof(float) * ((mel_lds ? a.n_mels * a.mel_max_width : 0) + 2 * a.n_mels);
+        if (mel_lds)
+            hipLaunchKernelGGL(k_spec640<true>, dim3(n_chunks, (unsigned)a.n_utt), dim3(64 * WAVES), shm, s, a, n_chunks);
+        else
+            hipLaunchKernelGGL(k_spec640<false>, dim3(n_chunks, (unsigned)a.n_utt), dim3(64 * WAVES), shm, s, a, n_chunks);
         AVSE_HIP_CHECK(hipGetLastError());
         if (n_chunks > 1 && need_clamp_pass) {
             hipLaunchKernelGGL(k_spec_clamp, dim3(1024), dim3(256), 0, s, a);

@@ -138,13 +138,32 @@ def test_bf16_halo_video_convs_match_generic_kernel(gpu, N, monkeypatch):
     assert rel_rms(out_h, out_g) <= 3e-2
 
 
-def test_intermediates_fp32(gpu):
-    """Every layer's activation, not only the output, matches the oracle (catches compensating bugs)."""
+def test_intermediates_fp32(gpu, monkeypatch):
+    """Every layer's activation, not only the output, matches the oracle (catches compensating bugs).
+    d_deconv6 runs unfused here so the d_deconv5 activation is materialised; the fused path is covered by
+    every output comparison and by test_fused_tail_matches_unfused."""
+    monkeypatch.setenv("AVSE_UNFUSED_TAIL", "1")
     got, ref, inter, dw = run_case(gpu, 2, "float32", seed=21)
     sc = scratch(dw, 2)
     for k in inter:
         if k in sc:
             assert rel_rms(sc[k], inter[k]) <= 1e-5, (k, rel_rms(sc[k], inter[k]))
+
+
+@pytest.mark.parametrize("dtype,tol", [("float32", 1e-6), ("bfloat16", 2e-3)])
+def test_fused_tail_matches_unfused(gpu, monkeypatch, dtype, tol):
+    """d_deconv5 + d_deconv6 fused (the 64 -> 1 dot in d_deconv5's epilogue) against the two-kernel path;
+    both round the d_deconv5 activation to the compute dtype, only the summation order differs."""
+    from avse_amd import ops
+    from avse_amd.model import KerasModel
+    model = KerasModel.init(seed=4, randomize=True)
+    mel, video = make_inputs(7, 44)
+    args = [ops.to_device(mel), ops.to_device(video)]
+    dw = ops.DeviceWeights(model, dtype)
+    fused = ops.forward(dw, *args).cpu().numpy()
+    monkeypatch.setenv("AVSE_UNFUSED_TAIL", "1")
+    unfused = ops.forward(dw, *args).cpu().numpy()
+    assert rel_rms(fused, unfused) <= tol, rel_rms(fused, unfused)
 
 
 def test_mse_matches(gpu):
