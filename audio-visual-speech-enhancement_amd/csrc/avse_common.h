@@ -147,6 +147,7 @@ struct HaloArgs {
     long long out_clip_stride;
     int out_pix_stride;
     int out_c_off;
+    unsigned long long* prof;   // ablation harness only (ABL & 128): per-wave cycle counters, else unused
 };
 
 int launch_conv_halo(const HaloArgs& a, hipStream_t s);

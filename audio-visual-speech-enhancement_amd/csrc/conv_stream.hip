@@ -12,11 +12,16 @@
 //     32-channel K-slice it reads 4 A + 8 B fragments (12 KB for 16 MFMAs), 25% fewer LDS bytes per
 //     FLOP than 8 waves of 64 x 64, and keeps its 128 accumulators in place for the whole tile;
 //   * the workgroup is persistent over tiles; one K-slice per step, one barrier per step;
-//   * per step each loader lane issues three 16-byte loads — weights of the slice LAT+2 steps ahead,
-//     one 1-KB piece of the input window of the chunk after next — into a ring of LAT register sets and
-//     stores the set loaded LAT steps earlier.  vmcnt retires in issue order, so the input window's HBM
-//     latency would stall the weights behind it with a short ring (LAT 4: +14%); register staging costs a
-//     few issue cycles where an LDS-DMA (buffer_load ... lds) costs its wave 100-200;
+//   * per step each loader lane issues two 16-byte weight loads (the slice LAT+2 steps ahead) and, on
+//     the first HPW taps of a chunk, one 1-KB piece of the input window of the chunk after next, into a
+//     ring of LAT register sets, and stores the set loaded LAT steps earlier.  vmcnt retires in issue
+//     order, so the input window's HBM latency would stall the weights behind it with a short ring (LAT 4:
+//     +14%); register staging costs a few issue cycles where an LDS-DMA (buffer_load ... lds) costs its
+//     wave 100-200;
+//   * the loader is unrolled over a chunk pair (2 x KS^2 steps), so tap, ring set, weight slot and piece
+//     index are compile-time: a wave issues at most one instruction per 4 cycles, and the first loader
+//     (runtime tap: piece address, chunk and tile bookkeeping every step, ~185 instructions per step)
+//     took ~730 cycles per step against ~600 for the compute wave's 16 MFMAs (s_memtime split, ABL 128);
 //   * the input window streams per 32-channel chunk through 3 LDS slots of 64-byte pixel rows: chunk g+2
 //     arrives while chunk g computes, across tile boundaries too.
 //
@@ -69,9 +74,9 @@ __device__ __forceinline__ void wait_vm_lgkm0() {
 }
 __device__ __forceinline__ void barrier_raw() { asm volatile("s_barrier" ::: "memory"); }
 
-// LAT (load -> LDS store distance, steps): 10 for 5x5 (100 slices per 128-channel tile), 6 for 3x3
-// (36 / 72 slices; the halo deadline below caps it at 10).  Measured on v_conv2: LAT 4 / 5 / 10 / 20 =
-// 1.14 / 1.04-1.13 / 1.00 / 1.27 ms (20 spills).
+// LAT (load -> LDS store distance, steps): 10 for 5x5, 6 for 3x3; it divides the unrolled chunk pair
+// (2 KS^2 steps).  Measured on v_conv2 (runtime-tap loader): LAT 4 / 5 / 10 / 20 = 1.14 / 1.04-1.13 / 1.00 /
+// 1.27 ms (20 spills).
 template <int KS, int TH, int TW, int NCLIP, int LAT_ = (KS == 5 ? 10 : 6)>
 struct StreamGeom {
     static constexpr int HH = TH + KS - 1, HW = TW + KS - 1;
@@ -81,27 +86,39 @@ struct StreamGeom {
     static constexpr int NTAP = KS * KS;
     static constexpr int CSLOT = HPIECES * 1024;               // bytes per halo chunk slot
     static constexpr int WSLOT = 8192;                         // one K-slice of 128 co x 32 ci
-    // LAT: steps between a load and its LDS write (the loop is unrolled by LAT); weights are loaded
-    // WD = LAT + 2 steps ahead of their slice and land in a 2-slot LDS ring; 3 halo chunk slots;
-    // + one 1-KB dummy row per wave for the zero pieces of steps without a real one
-    static constexpr int LAT = LAT_, WD = LAT + 2, NHS = 3;
-    static constexpr int LDS = NHS * CSLOT + 2 * WSLOT + 4 * 1024;
-    static_assert(LDS > 80 * 1024 && LDS <= 160 * 1024, "one persistent workgroup per CU");
+    // LAT: steps between a load and its LDS write; weights are loaded WD = LAT + 2 steps ahead of their
+    // slice and land in a 2-slot LDS ring; 3 halo chunk slots
+    static constexpr int LAT = LAT_, WD = LAT + 2, NHS = 3, PAIR = 2 * NTAP;
+    static constexpr int LDS = NHS * CSLOT + 2 * WSLOT;
+    static_assert(LDS <= 160 * 1024, "LDS");   // one workgroup per CU: ~250 VGPRs x 8 waves fill the register file
     static_assert(NCLIP * TH * TW == 256, "tile = 256 conv pixels (4 waves x 4 fragments)");
+    static_assert(PAIR % LAT == 0 && LAT < NTAP, "the ring set of a step is compile-time");
     // chunk g+2's pieces are loaded at taps 0..HPW-1 of chunk g and written LAT steps later, before
     // the first fragment read of chunk g+2 at step NTAP-1 of chunk g+1
     static_assert(HPW <= NTAP && HPW - 1 + LAT <= 2 * NTAP - 2, "halo pieces must land in time");
+    // loads issued by step j (tap j % NTAP): two weight chunks + one piece on the first HPW taps
+    static constexpr int loads(int j, int abl) {
+        const int tap = ((j % NTAP) + NTAP) % NTAP;
+        return ((abl & 2) ? 0 : 2) + ((!(abl & 1) && tap < HPW) ? 1 : 0);
+    }
+    // vmcnt bound at the end of step j: the loads of steps j-LAT+2 .. j may stay in flight (the set of
+    // step j-LAT+1 is stored by step j+1)
+    static constexpr int vm_wait(int j, int abl) {
+        int n = 0;
+        for (int i = j - LAT + 2; i <= j; ++i) n += loads(i, abl);
+        return n;
+    }
 };
 
 // ABL: ablation mask for tools/stream_ablate.hip only (0 in the library): 1 = no halo pieces in the
 // loop, 2 = no weight streaming in the loop, 4 = no barrier/wait, 8 = no fragment reads, 16 = no MFMAs,
-// 32 = every in-loop piece is a zero fill (all piece instructions, no input traffic), 64 = every tile
-// reads clip 0's window (L2-resident input)
+// 64 = every tile reads clip 0's window (L2-resident input), 128 = s_memtime per step: cycles working /
+// waiting (vmcnt, lgkmcnt) / in the barrier, per wave, into a.prof[(block * 8 + wave) * 4 + {0,1,2, 3=steps}]
 template <int KS, int TH, int TW, int NCLIP, int LAT_ = StreamGeom<KS, TH, TW, NCLIP>::LAT, int ABL = 0>
 __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
     using G = StreamGeom<KS, TH, TW, NCLIP, LAT_>;
     constexpr int HH = G::HH, HW = G::HW, HPIX = G::HPIX, HPW = G::HPW, NTAP = G::NTAP;
-    constexpr int CSLOT = G::CSLOT, WSLOT = G::WSLOT, LAT = G::LAT, WD = G::WD;
+    constexpr int CSLOT = G::CSLOT, WSLOT = G::WSLOT, LAT = G::LAT, WD = G::WD, PAIR = G::PAIR;
     constexpr int BPR = TW / 8, BPC = (TH / 4) * BPR;     // 4x8-pixel blocks (32 MFMA rows) per row / clip
     static_assert(TW % 8 == 0 && TH % 4 == 0 && BPC % 2 == 0, "a wave's two blocks share their y origin mod 4");
     constexpr int PAD = (KS - 1) / 2;
@@ -109,14 +126,13 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
     extern __shared__ __attribute__((aligned(1024))) char lds[];
     char* const halo = lds;                    // [NHS][CSLOT]
     char* const wring = lds + G::NHS * CSLOT;  // [2][WSLOT]
-    char* const dummy = wring + 2 * WSLOT;     // [4 loader waves][1 KB]
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int w = wave & 3;                    // index within the role
 
-    const int nch = a.Ci / 32;                 // 32-channel chunks per tile
+    const int nch = a.Ci / 32;                 // 32-channel chunks per tile (even: host check)
     const int spt = nch * NTAP;                // K-slices per tile (a multiple of 4: 4 | nch)
     const int tiles_x = a.Wc / TW, tiles_y = a.Hc / TH;
     const int tiles_per_clip = tiles_x * tiles_y;
@@ -124,7 +140,6 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
     const int nmine = (ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
     if (nmine <= 0) return;
     const int nchunks = nmine * nch;
-    const int total = nmine * spt;
     const int co0 = blockIdx.y * 128;
     const long long clip_bytes = (long long)a.Hc * a.Wc * a.Ci * 2;
 
@@ -141,128 +156,165 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
         // weights: loader w stores bytes [2048 w, 2048 w + 2048) of a slot: rows 32w + 16u + lane/4
         const __amdgpu_buffer_rsrc_t wrs = make_rsrc(reinterpret_cast<const char*>(a.w) + (size_t)co0 * 64,
                                                      (long long)spt * a.Co * 64 - (long long)co0 * 64);
-        const int wslice = a.Co * 64;
+        const int wslice = a.Co * 64, wend = spt * wslice;
         int wvoff[2];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
             const int row = 32 * w + 16 * u + (lane >> 2), sl = lane & 3;
             wvoff[u] = row * 64 + ((sl ^ wswz(row)) << 4);
         }
-        auto wdst = [&](int slot, int u) { return wring + slot * WSLOT + 2048 * w + 1024 * u + lane * 16; };
+        char* const wdst = wring + 2048 * w + lane * 16;   // + slot * WSLOT + 1024 u
         auto tile_rsrc = [&](int clip0) {
             return make_rsrc(reinterpret_cast<const char*>(a.in) + (long long)clip0 * clip_bytes,
                              (long long)(a.N - clip0) * clip_bytes);
         };
-        // source offset (per lane) and LDS destination (uniform) of piece pc of this loader (P = w + 4 pc)
-        // of chunk c of the tile at (oy0, ox0); not real: a zero load bound for this loader's dummy row
+        // piece pc of this loader is P = w + 4 pc (1-KB rows P*1024 .. of a halo slot; lane: 16 B of pixel
+        // P*16 + lane/4).  Its source offset in the tile at (oy0, ox0) for chunk 0, or kOOB (reads zero)
+        // outside the image / past the window — computed once per tile
         const int ci2 = a.Ci * 2, hc = a.Hc, wc = a.Wc;
-        auto piece_addr = [&](bool real, int oy0, int ox0, int c, int slot, int pc, int& voff, char*& dst) {
-            const int P = w + 4 * pc;
-            const int p = P * 16 + (lane >> 2), sl = lane & 3;
-            const int cl = p / (HH * HW), rr = p - cl * (HH * HW);
-            const int y = rr / HW, x = rr - y * HW;
-            const int iy = oy0 + y - PAD, ix = ox0 + x - PAD;
-            const int off = ((cl * hc + iy) * wc + ix) * ci2 + c * 64 + ((sl ^ hsw(y)) << 4);
-            const int ok = (int)real & (int)(p < HPIX) & (int)((unsigned)iy < (unsigned)hc) & (int)((unsigned)ix < (unsigned)wc);
-            const int mask = -ok;
-            voff = (off & mask) | (kOOB & ~mask);
-            dst = (real ? halo + slot * CSLOT + P * 1024 : dummy + w * 1024) + lane * 16;
+        auto tile_voffs = [&](int oy0, int ox0, int (&vo)[HPW]) {
+#pragma unroll
+            for (int pc = 0; pc < HPW; ++pc) {
+                const int P = w + 4 * pc;
+                const int p = P * 16 + (lane >> 2), sl = lane & 3;
+                const int cl = p / (HH * HW), rr = p - cl * (HH * HW);
+                const int y = rr / HW, x = rr - y * HW;
+                const int iy = oy0 + y - PAD, ix = ox0 + x - PAD;
+                const int off = ((cl * hc + iy) * wc + ix) * ci2 + ((sl ^ hsw(y)) << 4);
+                const bool ok = (P < G::HPIECES) & (p < HPIX) & ((unsigned)iy < (unsigned)hc) & ((unsigned)ix < (unsigned)wc);
+                vo[pc] = ok ? off : kOOB;
+            }
+        };
+        // a piece row past the chunk (P >= HPIECES: only for the last pc of some waves) is not stored
+        auto piece_store = [&](auto pcc, char* base, i32x4 v) {
+            constexpr int pc = decltype(pcc)::value;
+            if constexpr (4 * pc + 3 < G::HPIECES) st16(base + pc * 4096, v);
+            else if (w + 4 * pc < G::HPIECES) st16(base + pc * 4096, v);
         };
 
-        // tile origins: the current slice's tile and the next one (chunk g+2 may belong to it)
+        // tiles: k (chunks being computed), k + 1 (chunk g+2 may belong to it)
         int cur_clip0, cur_oy0, cur_ox0, nxt_clip0, nxt_oy0, nxt_ox0;
         tile_origin(0, cur_clip0, cur_oy0, cur_ox0);
         tile_origin(1, nxt_clip0, nxt_oy0, nxt_ox0);
         __amdgpu_buffer_rsrc_t cur_rs = tile_rsrc(cur_clip0), nxt_rs = tile_rsrc(nxt_clip0);
+        int vo_cur[HPW], vo_nxt[HPW];
+        tile_voffs(cur_oy0, cur_ox0, vo_cur);
+        tile_voffs(nxt_oy0, nxt_ox0, vo_nxt);
+        char* const pbase0 = halo + w * 1024 + lane * 16;   // + slot * CSLOT + pc * 4096
 
-        // prologue: chunks 0, 1 of the first tile (nch >= 4) and weight slices 0, 1 straight to LDS;
-        // weight slices 2 .. LAT+1 into the register ring (stored by steps 0 .. LAT-1)
-#pragma unroll
-        for (int cc = 0; cc < 2; ++cc)
-#pragma unroll
-            for (int pc = 0; pc < HPW; ++pc)
-                if (w + 4 * pc < G::HPIECES) {
-                    int voff;
-                    char* dst;
-                    piece_addr(true, cur_oy0, cur_ox0, cc, cc, pc, voff, dst);
-                    st16(dst, ld16(cur_rs, voff, 0));
-                }
+        // prologue: chunk 0 and the pieces of chunk 1 that no virtual step -LAT..-1 loads, weight slices
+        // 0, 1 straight to LDS; the sets of the virtual steps (weights of slices 2 .. LAT+1, pieces of chunk
+        // 1 on taps NTAP-LAT ..) into the register ring — steps 0 .. LAT-1 store them
+        [&]<int... PC>(std::integer_sequence<int, PC...>) {
+            (piece_store(std::integral_constant<int, PC>{}, pbase0, ld16(cur_rs, vo_cur[PC], 0)), ...);
+            ((PC < NTAP - LAT ? piece_store(std::integral_constant<int, PC>{}, pbase0 + CSLOT, ld16(cur_rs, vo_cur[PC], 64))
+                              : (void)0), ...);
+        }(std::make_integer_sequence<int, HPW>{});
 #pragma unroll
         for (int s = 0; s < 2; ++s)
 #pragma unroll
-            for (int u = 0; u < 2; ++u) st16(wdst(s, u), ld16(wrs, wvoff[u], (s % spt) * wslice));
+            for (int u = 0; u < 2; ++u) st16(wdst + s * WSLOT + 1024 * u, ld16(wrs, wvoff[u], (s % spt) * wslice));
         i32x4 rw[LAT][2], rp[LAT];
-        char* pdst[LAT];
-#pragma unroll
-        for (int S = 0; S < LAT; ++S) {
-#pragma unroll
-            for (int u = 0; u < 2; ++u) rw[S][u] = ld16(wrs, wvoff[u], ((S + 2) % spt) * wslice);
-            rp[S] = (i32x4){0, 0, 0, 0};
-            pdst[S] = dummy + w * 1024 + lane * 16;
-        }
+        [&]<int... S>(std::integer_sequence<int, S...>) {
+            ([&] {
+                 rw[S][0] = ld16(wrs, wvoff[0], ((S + 2) % spt) * wslice);
+                 rw[S][1] = ld16(wrs, wvoff[1], ((S + 2) % spt) * wslice);
+                 constexpr int vt = NTAP - LAT + S;   // tap of virtual step S - LAT
+                 if constexpr (vt < HPW && !(ABL & 1)) rp[S] = ld16(cur_rs, vo_cur[vt < HPW ? vt : 0], 64);
+             }(), ...);
+        }(std::make_integer_sequence<int, LAT>{});
         wait_vm_lgkm0<0>();
         barrier_raw();
         barrier_raw();   // the compute waves have read slice 0 (weight slot 0 is overwritten at step 0)
 
-        // state of the step being issued: its slice (k, c, tap) in halo slot hs; wsa = weight slice
-        // loaded by it (step + WD, mod spt)
-        int k = 0, c = 0, tap = 0, hs = 0;
-        int wsa = WD % spt;
-        int pv_voff;
-        char* pv_dst;
-        __amdgpu_buffer_rsrc_t pv_rs;
-        // the piece a step loads: chunk g+2 of its slice's chunk g, piece index = its tap
-        auto piece_prep = [&]() {
-            const bool real = !(ABL & 32) & (w + 4 * tap < G::HPIECES) & (k * nch + c + 2 < nchunks);
+        // per-chunk state of chunk g = k * nch + c: its pieces load chunk g+2 from (prs, vsel[], psoff) and
+        // land at pd_cur; pd_prev = where the pieces loaded during chunk g-1 land
+        int k = 0, c = 0, g = 0, hs2 = 2;           // hs2 = halo slot of chunk g+2
+        int woff = (WD % spt) * wslice;             // weights loaded by the next step: slice step + WD
+        int vsel[HPW];
+        __amdgpu_buffer_rsrc_t prs = cur_rs;
+        int psoff = 0;
+        char* pd_cur = pbase0 + CSLOT;              // virtual steps' pieces: chunk 1
+        char* pd_prev = pd_cur;
+        unsigned long long ptp = (ABL & 128) ? __builtin_amdgcn_s_memtime() : 0, pt0 = 0, pt1 = 0, p_work = 0,
+                           p_wait = 0, p_bar = 0;
+        auto chunk_begin = [&]() {
             const bool nx = c + 2 >= nch;
-            piece_addr(real, nx ? nxt_oy0 : cur_oy0, nx ? nxt_ox0 : cur_ox0, nx ? c + 2 - nch : c + 2,
-                       hs == 0 ? 2 : hs - 1, tap < HPW ? tap : 0, pv_voff, pv_dst);
-            pv_rs = nx ? nxt_rs : cur_rs;
+            const bool real = g + 2 < nchunks;
+#pragma unroll
+            for (int pc = 0; pc < HPW; ++pc) vsel[pc] = !real ? kOOB : nx ? vo_nxt[pc] : vo_cur[pc];
+            prs = nx ? nxt_rs : cur_rs;
+            psoff = (nx ? c + 2 - nch : c + 2) * 64;
+            pd_prev = pd_cur;
+            pd_cur = pbase0 + hs2 * CSLOT;
         };
-        auto lstep = [&](auto sidx, int t) {
-            constexpr int S = decltype(sidx)::value;
-            // 1. LDS stores of the set loaded LAT steps ago: weights of slice t+2 into ring slot t&1
-            //    (slice t's, read during step t-1) and that step's piece
-            if constexpr (!(ABL & 2))
+        auto chunk_end = [&]() {
+            ++g;
+            hs2 = hs2 == 2 ? 0 : hs2 + 1;
+            if (++c == nch) {
+                c = 0;
+                ++k;
+                cur_oy0 = nxt_oy0;
+                cur_ox0 = nxt_ox0;
+                cur_rs = nxt_rs;
 #pragma unroll
-                for (int u = 0; u < 2; ++u) st16(wdst(t & 1, u), rw[S][u]);
-            if constexpr (!(ABL & 1)) st16(pdst[S], rp[S]);
+                for (int pc = 0; pc < HPW; ++pc) vo_cur[pc] = vo_nxt[pc];
+                tile_origin(k + 1, nxt_clip0, nxt_oy0, nxt_ox0);
+                nxt_rs = tile_rsrc(nxt_clip0);
+                tile_voffs(nxt_oy0, nxt_ox0, vo_nxt);
+            }
+        };
+        // step j of a chunk pair (compile-time): tap j % NTAP, ring set j % LAT, weight slot j & 1
+        auto lstep = [&](auto jidx) {
+            constexpr int j = decltype(jidx)::value;
+            constexpr int tap = j % NTAP, S = j % LAT;
+            constexpr int jl = j - LAT;                                 // the step that loaded set S
+            constexpr int tl = ((jl % NTAP) + NTAP) % NTAP;
+            constexpr bool lprev = (jl < 0) || (jl / NTAP != j / NTAP);  // ... during the previous chunk
+            if constexpr (tap == 0) chunk_begin();
+            // 1. LDS stores of set S: weights of slice j+2 (slot j & 1: slice j's, read during step j-1) and
+            //    the piece loaded with them
+            if constexpr (!(ABL & 2)) {
+                st16(wdst + (j & 1) * WSLOT, rw[S][0]);
+                st16(wdst + (j & 1) * WSLOT + 1024, rw[S][1]);
+            }
+            if constexpr (tl < HPW && !(ABL & 1))
+                piece_store(std::integral_constant<int, (tl < HPW ? tl : 0)>{}, lprev ? pd_prev : pd_cur, rp[S]);
             // 2. this step's loads
-            if constexpr (!(ABL & 2))
-#pragma unroll
-                for (int u = 0; u < 2; ++u) rw[S][u] = ld16(wrs, wvoff[u], wsa * wslice);
-            if constexpr (!(ABL & 1)) {
-                piece_prep();
-                rp[S] = ld16(pv_rs, pv_voff, 0);
-                pdst[S] = pv_dst;
+            if constexpr (!(ABL & 2)) {
+                rw[S][0] = ld16(wrs, wvoff[0], woff);
+                rw[S][1] = ld16(wrs, wvoff[1], woff);
             }
-            // 3. loads issued LAT-1 or more steps ago have landed (the next step stores the set loaded
-            //    LAT-1 steps before it); this step's stores are visible after the barrier
+            if constexpr (tap < HPW && !(ABL & 1)) rp[S] = ld16(prs, vsel[tap < HPW ? tap : 0], psoff);
+            woff += wslice;
+            if (woff == wend) woff = 0;
+            // 3. the set of step j-LAT+1 has landed (stored by step j+1); this step's stores are visible
+            //    after the barrier
             if constexpr (!(ABL & 4)) {
-                wait_vm_lgkm0<(ABL & 3) == 3 ? 0 : (ABL & 3) ? (LAT - 1) * ((ABL & 1) ? 2 : 1) : 3 * (LAT - 1)>();
+                if constexpr ((ABL & 128) != 0) pt0 = __builtin_amdgcn_s_memtime();
+                wait_vm_lgkm0<G::vm_wait(j, ABL)>();
+                if constexpr ((ABL & 128) != 0) pt1 = __builtin_amdgcn_s_memtime();
                 barrier_raw();
-            }
-            // 4. advance to the next slice (a new tile moves the tile origins on)
-            if (++wsa == spt) wsa = 0;
-            if (++tap == NTAP) {
-                tap = 0;
-                hs = hs == 2 ? 0 : hs + 1;
-                if (++c == nch) {
-                    c = 0;
-                    ++k;
-                    cur_oy0 = nxt_oy0;
-                    cur_ox0 = nxt_ox0;
-                    cur_rs = nxt_rs;
-                    tile_origin(k + 1, nxt_clip0, nxt_oy0, nxt_ox0);
-                    nxt_rs = tile_rsrc(nxt_clip0);
+                if constexpr ((ABL & 128) != 0) {
+                    const unsigned long long pt2 = __builtin_amdgcn_s_memtime();
+                    p_work += pt0 - ptp;
+                    p_wait += pt1 - pt0;
+                    p_bar += pt2 - pt1;
+                    ptp = pt2;
                 }
             }
+            if constexpr (tap == NTAP - 1) chunk_end();
         };
-        for (int t = 0; t < total; t += LAT)   // total % LAT == 0 (host check)
-            [&]<int... S>(std::integer_sequence<int, S...>) {
-                (lstep(std::integral_constant<int, S>{}, t + S), ...);
-            }(std::make_integer_sequence<int, LAT>{});
+        for (int pr = 0; pr < nchunks; pr += 2)
+            [&]<int... J>(std::integer_sequence<int, J...>) {
+                (lstep(std::integral_constant<int, J>{}), ...);
+            }(std::make_integer_sequence<int, PAIR>{});
         wait_vm_lgkm0<0>();   // loads still in flight target registers and rows nobody reads
+        if constexpr ((ABL & 128) != 0)
+            if (lane == 0) {
+                unsigned long long* pr = a.prof + ((size_t)blockIdx.x * 8 + wave) * 4;
+                pr[0] = p_work; pr[1] = p_wait; pr[2] = p_bar; pr[3] = (unsigned long long)nchunks * NTAP;
+            }
         return;
     }
 
@@ -347,6 +399,8 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
         }
     };
 
+    unsigned long long ptp = (ABL & 128) ? __builtin_amdgcn_s_memtime() : 0, pt0 = 0, pt1 = 0, p_work = 0, p_wait = 0,
+                       p_bar = 0;
     // next slice (tap1 of the chunk in halo slot hs1)
     int tap1 = 1, hs1 = 0;
     i32x4 fa[4], fb[8], na[4], nb[8];
@@ -376,9 +430,18 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
         __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (!(ABL & 4)) {
+            if constexpr ((ABL & 128) != 0) pt0 = __builtin_amdgcn_s_memtime();
             // LDS reads only: the epilogue's global stores (vmcnt on gfx9) are never waited for
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if constexpr ((ABL & 128) != 0) pt1 = __builtin_amdgcn_s_memtime();
             barrier_raw();
+            if constexpr ((ABL & 128) != 0) {
+                const unsigned long long pt2 = __builtin_amdgcn_s_memtime();
+                p_work += pt0 - ptp;
+                p_wait += pt1 - pt0;
+                p_bar += pt2 - pt1;
+                ptp = pt2;
+            }
         }
         if (++tap1 == NTAP) {
             tap1 = 0;
@@ -398,6 +461,11 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
         tile_origin(kt, cur_clip0, cur_oy0, cur_ox0);
         epilogue(cur_clip0, cur_oy0, cur_ox0);
     }
+    if constexpr ((ABL & 128) != 0)
+        if (lane == 0) {
+            unsigned long long* pr = a.prof + ((size_t)blockIdx.x * 8 + wave) * 4;
+            pr[0] = p_work; pr[1] = p_wait; pr[2] = p_bar; pr[3] = (unsigned long long)t;
+        }
 }
 
 template <int KS, int TH, int TW, int NCLIP>
@@ -409,7 +477,7 @@ int launch_stream(const HaloArgs& a, hipStream_t s) {
                                            hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
         attr = true;
     }
-    if (a.Hc % TH || a.Wc % TW || a.Co % 128 || a.Ci % 32 || ((a.Ci / 32) * KS * KS) % G::LAT) {
+    if (a.Hc % TH || a.Wc % TW || a.Co % 128 || a.Ci % 64) {   // an even number of 32-channel chunks
         set_error("stream conv: tile does not divide the layer");
         return 3;
     }

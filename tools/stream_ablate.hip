@@ -15,7 +15,7 @@ void set_error(const std::string& msg) { std::fprintf(stderr, "error: %s\n", msg
 
 using namespace avse;
 
-template <int ABL, int LAT = 4>
+template <int ABL, int LAT = 10>
 float run(const HaloArgs& a, int reps) {
     using G = StreamGeom<5, 16, 16, 1, LAT>;
     (void)hipFuncSetAttribute((const void*)k_conv_stream<5, 16, 16, 1, LAT, ABL>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -23,7 +23,7 @@ float run(const HaloArgs& a, int reps) {
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
-    for (int r = 0; r < 2; ++r)
+    for (int r = 0; r < 10; ++r)   // warm-up long enough for the clock to settle under MFMA load
         hipLaunchKernelGGL((k_conv_stream<5, 16, 16, 1, LAT, ABL>), dim3(256, 1), dim3(512), G::LDS, 0, a);
     (void)hipEventRecord(e0, 0);
     for (int r = 0; r < reps; ++r)
@@ -66,7 +66,7 @@ int main() {
     (void)hipMemset(sh, 0, C * 4);
     a.in = in; a.out = out; a.w = w; a.scale = sc; a.shift = sh;
     const double flop = 2.0 * N * H * H * C * C * 25;
-    const int reps = 10;
+    const int reps = 20;
     auto rep = [&](const char* name, float ms) {
         std::printf("%-34s %8.4f ms  %7.1f TF/s\n", name, ms, flop / (ms * 1e-3) / 1e12);
     };
@@ -79,5 +79,28 @@ int main() {
     rep("MFMA only (15)", run<15, 10>(a, reps));
     rep("L2-resident input (64)", run<64, 10>(a, reps));
     rep("LAT5", run<0, 5>(a, reps));
+    rep("full (again: clock drift check)", run<0, 10>(a, reps));
+    // per-step cycle split (s_memtime; the counters add a few instructions per step)
+    unsigned long long* prof;
+    (void)hipMalloc(&prof, 256 * 8 * 4 * 8);
+    (void)hipMemset(prof, 0, 256 * 8 * 4 * 8);
+    a.prof = prof;
+    rep("instrumented (128)", run<128, 10>(a, reps));
+    auto split = [&](const char* title) {
+    std::vector<unsigned long long> hp(256 * 8 * 4);
+    (void)hipMemcpy(hp.data(), prof, hp.size() * 8, hipMemcpyDeviceToHost);
+    double s[2][3] = {}, steps[2] = {};
+    for (int b = 0; b < 256; ++b)
+        for (int wv = 0; wv < 8; ++wv) {
+            const int role = wv >= 4;
+            for (int k = 0; k < 3; ++k) s[role][k] += (double)hp[(b * 8 + wv) * 4 + k];
+            steps[role] += (double)hp[(b * 8 + wv) * 4 + 3];
+        }
+    const char* names[2] = {"compute", "loader"};
+    for (int r = 0; r < 2; ++r)
+        std::printf("%s %-8s cycles/step: work %7.1f  wait(vm/lgkm) %7.1f  barrier %7.1f\n", title, names[r],
+                    s[r][0] / steps[r], s[r][1] / steps[r], s[r][2] / steps[r]);
+    };
+    split("LAT10");
     return 0;
 }
