@@ -18,6 +18,7 @@
 // A (im2col gathered on the fly, 16-byte chunks, zero padding = TF 'SAME') and B (packed weights
 // [Cout][Kpad]) are register-staged into a double-buffered, XOR-swizzled LDS tile (one barrier
 // per slab; the next slab's global loads are in flight during the current slab's MFMAs).
+#include <cstdlib>
 #include <type_traits>
 
 #include "avse_common.h"
@@ -55,7 +56,12 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, lo
     return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, nrec, 0x00020000);
 }
 
-template <typename T, int BN>
+// FAST (Ci a multiple of the slab, i.e. every layer but a_conv1): a slab never straddles a tap, so the A row
+// offsets are computed once per tap and a slab's channel offset is the buffer load's scalar soffset; three LDS
+// buffers make the buffer of every unrolled step compile-time.  The generic path decoded (tap, channel) and
+// re-checked the bounds of both rows every slab: ~138 instructions per slab against 16 MFMAs of 16 cycles
+// (a wave issues at most one instruction per 4 cycles), so the short-K layers were issue-bound.
+template <typename T, int BN, bool FAST>
 __global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
     constexpr int CH = 16 / sizeof(T);          // elements per 16-byte chunk
     constexpr int SLAB = 64 / sizeof(T);        // elements per 64-byte k-slab
@@ -63,8 +69,9 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
     constexpr int NJ = WN / 16;                 // 16-wide N fragments per wave
     constexpr int NI = 4;                       // 16-high M fragments per wave (64 rows)
     constexpr int BCH = BN * 4 / 256;           // B chunks per thread
+    constexpr int NBUF = FAST ? 3 : 2;          // LDS buffers
 
-    __shared__ __attribute__((aligned(16))) char lds[2 * (BM + BN) * 64];
+    __shared__ __attribute__((aligned(16))) char lds[NBUF * (BM + BN) * 64];
     // this phase's tap table, staged in LDS: a per-lane global tap load feeding the A addresses made every
     // slab wait for vmcnt — which retires in order, so it also drained all the slabs in flight
     __shared__ int2 tap_lds[MAX_TAPS_LDS];
@@ -127,11 +134,50 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
     const __amdgpu_buffer_rsrc_t rsB = make_rsrc(reinterpret_cast<const char*>(a.w) + ph.w_off * sizeof(T),
                                                  (long long)a.Co * ph.kpad * sizeof(T));
 
+    // ---- FAST path state: load cursor (slab lk = tap kjf x chunks-per-tap + csf), per-tap A row offsets ----
+    const int cpt = FAST ? a.Ci / SLAB : 1;
+    int lk = s_begin, kjf = s_begin / cpt, csf = s_begin - kjf * cpt;
+    int aoff[2], boff[BCH];
+    auto tap_offs = [&]() {
+        const bool tap_ok = kjf < ph.ntaps;
+        const int2 t = tap_lds[tap_ok ? kjf : ph.ntaps - 1];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int iy = ri[h].iy0 + t.x, ix = ri[h].ix0 + t.y;
+            const bool ok = ri[h].valid && tap_ok && iy >= 0 && iy < a.Hi && ix >= 0 && ix < a.Wi;
+            aoff[h] = ok ? ri[h].cbase + ((iy * a.Wi + ix) * a.Ci + g * CH) * (int)sizeof(T) : kOOB;
+        }
+    };
+    if constexpr (FAST) {
+        tap_offs();
+#pragma unroll
+        for (int h = 0; h < BCH; ++h) {
+            const int c = tid + 256 * h;
+            const int n = n0 + (c >> 2);
+            boff[h] = n < a.Co ? (n * ph.kpad + (c & 3) * CH) * (int)sizeof(T) : kOOB;
+        }
+    }
+
     // P register stages: slabs s+1 .. s+P-1 are in flight while slab s computes (a layer with a short K loop
     // was a serial chain of one global-load latency per slab: ~0.7-1.2 us each, measured at batch 8)
     constexpr int P = 3;
     i32x4 ras[P][2], rbs[P][BCH];
     auto load_slab = [&](int s, i32x4 (&ra)[2], i32x4 (&rb)[BCH]) {
+        if constexpr (FAST) {
+            // A: the channel chunk is the scalar offset (an out-of-range row offset stays out of range);
+            // B: rows past Cout and slabs past the phase's K read zeros (range-checked voffset)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) ra[h] = __builtin_amdgcn_raw_buffer_load_b128(rsA, aoff[h], csf * 64, 0);
+#pragma unroll
+            for (int h = 0; h < BCH; ++h) rb[h] = __builtin_amdgcn_raw_buffer_load_b128(rsB, boff[h] + lk * 64, 0, 0);
+            ++lk;
+            if (++csf == cpt) {
+                csf = 0;
+                ++kjf;
+                tap_offs();
+            }
+            return;
+        }
         // A
         const bool tap_ok = kj < ph.ntaps;
         const int2 t = tap_lds[tap_ok ? kj : ph.ntaps - 1];
@@ -187,7 +233,7 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
     auto step = [&](auto qidx, int s) {
         constexpr int q = decltype(qidx)::value;           // (s - s_begin) % P
         constexpr int qn = (q + 1) % P;
-        const int buf = (s - s_begin) & 1;
+        const int buf = FAST ? q : (s - s_begin) & 1;      // FAST: three buffers, slab x in buffer (x - s_begin) % 3
         i32x4 fa[NI], fb[NJ];
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
@@ -214,7 +260,12 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
                         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], bv[e], acc[i][j], 0, 0, 0);
                 }
             }
-        if (s + 1 < s_end) {
+        if constexpr (FAST) {
+            // unconditional: past s_end the loads read zeros / unused rows and the buffer is never read
+            // (buffer qn held slab s-2, read before the barrier of step s-2)
+            store_slab(qn, ras[qn], rbs[qn]);
+            load_slab(s + 1 + P, ras[qn], rbs[qn]);
+        } else if (s + 1 < s_end) {
             store_slab(buf ^ 1, ras[qn], rbs[qn]);   // slab s+1, loaded P-1 steps ago
             load_slab(s + 1 + P, ras[qn], rbs[qn]);  // refill with slab s+1+P (the load cursor is sequential)
         }
@@ -479,6 +530,12 @@ inline unsigned grid_for(long long n, int block) {
 
 }  // namespace
 
+// AVSE_SLOW_CONV=1: force the generic (per-slab tap decode) k_conv path — A/B switch and test coverage
+bool no_fast_conv() {
+    const char* e = std::getenv("AVSE_SLOW_CONV");
+    return e && e[0] == '1';
+}
+
 int launch_conv(const ConvArgs& a, int dtype, hipStream_t s) {
     const int M = a.N * a.Hq * a.Wq;
     const int BN = (a.Co <= 64) ? 64 : 128;
@@ -496,12 +553,23 @@ int launch_conv(const ConvArgs& a, int dtype, hipStream_t s) {
             return 3;
         }
     dim3 grid((M + BM - 1) / BM, (a.Co + BN - 1) / BN, a.nphase * a.ksplit);
+    const bool fast = a.Ci % (dtype == 1 ? 32 : 16) == 0 && !no_fast_conv();
     if (dtype == 1) {
-        if (BN == 64) hipLaunchKernelGGL((k_conv<bf16_t, 64>), grid, dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((k_conv<bf16_t, 128>), grid, dim3(256), 0, s, a);
+        if (fast) {
+            if (BN == 64) hipLaunchKernelGGL((k_conv<bf16_t, 64, true>), grid, dim3(256), 0, s, a);
+            else hipLaunchKernelGGL((k_conv<bf16_t, 128, true>), grid, dim3(256), 0, s, a);
+        } else {
+            if (BN == 64) hipLaunchKernelGGL((k_conv<bf16_t, 64, false>), grid, dim3(256), 0, s, a);
+            else hipLaunchKernelGGL((k_conv<bf16_t, 128, false>), grid, dim3(256), 0, s, a);
+        }
     } else {
-        if (BN == 64) hipLaunchKernelGGL((k_conv<float, 64>), grid, dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((k_conv<float, 128>), grid, dim3(256), 0, s, a);
+        if (fast) {
+            if (BN == 64) hipLaunchKernelGGL((k_conv<float, 64, true>), grid, dim3(256), 0, s, a);
+            else hipLaunchKernelGGL((k_conv<float, 128, true>), grid, dim3(256), 0, s, a);
+        } else {
+            if (BN == 64) hipLaunchKernelGGL((k_conv<float, 64, false>), grid, dim3(256), 0, s, a);
+            else hipLaunchKernelGGL((k_conv<float, 128, false>), grid, dim3(256), 0, s, a);
+        }
     }
     AVSE_HIP_CHECK(hipGetLastError());
     if (a.ksplit > 1) return launch_splitk_reduce(a, dtype, s);
