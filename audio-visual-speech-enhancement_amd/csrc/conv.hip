@@ -61,8 +61,12 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, lo
 // buffers make the buffer of every unrolled step compile-time.  The generic path decoded (tap, channel) and
 // re-checked the bounds of both rows every slab: ~138 instructions per slab against 16 MFMAs of 16 cycles
 // (a wave issues at most one instruction per 4 cycles), so the short-K layers were issue-bound.
+// occupancy: more resident workgroups hide the per-tile load latency of the short-K layers (8-18 slabs per
+// tile for the decoder): 4 per CU for BN = 64 (<= 128 VGPRs, 36 KB LDS), 3 for BN = 128 (<= 168, 48 KB)
+template <int BN, bool FAST> constexpr int conv_occupancy() { return !FAST ? 2 : BN == 64 ? 4 : 3; }
+
 template <typename T, int BN, bool FAST>
-__global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
+__global__ __launch_bounds__(256, (conv_occupancy<BN, FAST>())) void k_conv(ConvArgs a) {
     constexpr int CH = 16 / sizeof(T);          // elements per 16-byte chunk
     constexpr int SLAB = 64 / sizeof(T);        // elements per 64-byte k-slab
     constexpr int WN = BN / 2;                  // wave tile N

@@ -118,6 +118,23 @@ class VideoNormalizer(object):
     def std_image(self):
         return self.__std_image
 
+    @classmethod
+    def from_stats(cls, mean_image, std_image):
+        obj = cls.__new__(cls)
+        obj.__mean_image = np.asarray(mean_image, np.float32)
+        obj.__std_image = np.asarray(std_image, np.float32)
+        return obj
+
+    def save(self, path):
+        """The fitted images as .npz (the reference pickles the object: speech_enhancer.py:48-49)."""
+        with open(path, "wb") as fd:
+            np.savez(fd, mean_image=self.__mean_image, std_image=self.__std_image)
+
+    @classmethod
+    def load(cls, path):
+        with np.load(path, allow_pickle=False) as z:
+            return cls.from_stats(z["mean_image"], z["std_image"])
+
     def device_stats(self, device=None):
         return ops.to_device(self.__mean_image, device), ops.to_device(self.__std_image, device)
 

@@ -64,6 +64,16 @@ class SpeechEnhancementNetwork(object):
         target = ops.to_device(speech_spectrograms, pred.device).reshape(pred.shape)
         return float(ops.mse(pred, target).item())
 
+    def predict_and_evaluate(self, mixed_spectrograms, video_samples, speech_spectrograms, video_normalizer=None):
+        """predict() and evaluate() from ONE forward: (squeezed prediction, MSE of that prediction).
+        speech_enhancer.py:76-79 runs the two on the same input; the loss is the same value."""
+        pred = self.predict_device(mixed_spectrograms, video_samples, video_normalizer)
+        target = ops.to_device(speech_spectrograms, pred.device).reshape(pred.shape)
+        loss = float(ops.mse(pred, target).item())
+        if isinstance(mixed_spectrograms, torch.Tensor):
+            return pred.squeeze(), loss
+        return np.squeeze(pred.cpu().numpy()), loss
+
     @staticmethod
     def load(model_cache_path, compute_dtype="float32"):
         """network.py:222-226 (own safetensors format; Keras HDF5 needs the converter)."""

@@ -12,13 +12,20 @@ Differences (host plumbing outside the hot path):
   * train: fitting (network.py:177-206) is out of scope; `--init-only` writes the files the reference's
     train produces (model.h5py from a Keras-default initialisation, normalization.pkl fitted on the
     training video) so that predict runs end to end;
-  * the enhanced/mixture .mp4 muxing (mediaio.ffmpeg.merge) runs only when ffmpeg is installed.
+  * the enhanced/mixture .mp4 muxing (mediaio.ffmpeg.merge) runs only when ffmpeg is installed;
+  * caches hold no pickles: preprocessed samples are <name>.npz (arrays + a JSON metadata string, read with
+    allow_pickle=False), the normaliser normalization.npz, the model model.safetensors (a Keras model.h5py
+    is converted once by tools/keras_h5_to_avse.py); the reference's own .pkl caches are not read (this
+    build never unpickles);
+  * predict runs ONE forward per sample: the printed loss (speech_enhancer.py:76-77, an MSE over the
+    sample like Model.evaluate) is computed from the same prediction that is reconstructed (the reference
+    runs evaluate and predict, two forwards of the same input).
 All spectrogram / network / reconstruction arithmetic goes through libavse (K1, forward, K6).
 """
 import argparse
+import json
 import logging
 import os
-import pickle
 import random
 import shutil
 import subprocess
@@ -102,16 +109,19 @@ class AssetManager:
             os.makedirs(d, exist_ok=True)
 
     def get_preprocessed_blob_path(self, data_name):
-        return os.path.join(self.__preprocessed_dir, data_name + ".pkl")
+        return os.path.join(self.__preprocessed_dir, data_name + ".npz")
 
     def create_model(self, model_name):
         os.makedirs(os.path.join(self.__models_dir, model_name), exist_ok=True)
 
     def get_model_cache_path(self, model_name):
-        return os.path.join(self.__models_dir, model_name, "model.h5py")
+        return os.path.join(self.__models_dir, model_name, "model.safetensors")
+
+    def get_keras_model_path(self, model_name):
+        return os.path.join(self.__models_dir, model_name, "model.h5py")   # the reference's file (speech_enhancer.py:120-122)
 
     def get_normalization_cache_path(self, model_name):
-        return os.path.join(self.__models_dir, model_name, "normalization.pkl")
+        return os.path.join(self.__models_dir, model_name, "normalization.npz")
 
     def create_prediction_storage(self, model_name, data_name):
         d = os.path.join(self.__out_dir, model_name, data_name)
@@ -167,10 +177,37 @@ def list_data(dataset_dir, speaker_ids, noise_dirs, max_files=None, shuffle=True
     return all_speech, all_noise
 
 
+SAMPLE_ARRAYS = ("video_samples", "mixed_spectrograms", "speech_spectrograms", "noise_spectrograms")
+
+
+def save_preprocessed_blob(path, samples):
+    """list[Sample] -> one .npz: per sample its arrays and the mixture's samples, plus a JSON metadata string."""
+    arrays, meta = {}, []
+    for i, smp in enumerate(samples):
+        for f in SAMPLE_ARRAYS:
+            arrays["s%d_%s" % (i, f)] = np.asarray(getattr(smp, f))
+        arrays["s%d_mixed_signal" % i] = np.asarray(smp.mixed_signal.get_data())
+        meta.append({"speaker_id": smp.speaker_id, "video_file_path": smp.video_file_path,
+                     "speech_file_path": smp.speech_file_path, "noise_file_path": smp.noise_file_path,
+                     "video_frame_rate": float(smp.video_frame_rate),
+                     "sample_rate": int(smp.mixed_signal.get_sample_rate())})
+    arrays["meta"] = np.array(json.dumps(meta))
+    with open(path, "wb") as fd:
+        np.savez(fd, **arrays)
+
+
 def load_preprocessed_blob(path):
     print("loading preprocessed samples from %s" % path)
-    with open(path, "rb") as fd:   # a file this CLI's preprocess wrote
-        return pickle.load(fd)
+    with np.load(path, allow_pickle=False) as z:
+        meta = json.loads(str(z["meta"]))
+        out = []
+        for i, m in enumerate(meta):
+            arrs = {f: z["s%d_%s" % (i, f)] for f in SAMPLE_ARRAYS}
+            signal = AudioSignal(z["s%d_mixed_signal" % i], m["sample_rate"])
+            out.append(Sample(m["speaker_id"], m["video_file_path"], m["speech_file_path"], m["noise_file_path"],
+                              arrs["video_samples"], arrs["mixed_spectrograms"], arrs["speech_spectrograms"],
+                              arrs["noise_spectrograms"], signal, m["video_frame_rate"]))
+    return out
 
 
 def load_preprocessed_blobs(paths, max_samples_per_blob=None):
@@ -197,8 +234,7 @@ def preprocess(args):
     speech_entries, noise_file_paths = list_data(args.dataset_dir, speaker_ids, args.noise_dirs, max_files=1000,
                                                  shuffle=True, augmentation_factor=1)
     samples = preprocess_data(speech_entries, noise_file_paths)
-    with open(assets.get_preprocessed_blob_path(args.data_name), "wb") as fd:
-        pickle.dump(samples, fd)
+    save_preprocessed_blob(assets.get_preprocessed_blob_path(args.data_name), samples)
     print("preprocessed %d samples" % len(samples))
 
 
@@ -211,8 +247,7 @@ def train(args):
     samples = load_preprocessed_blobs([assets.get_preprocessed_blob_path(d) for d in args.train_data_names])
     video, mixed, _ = make_sample_set(samples)
     normalizer = data_processor.VideoNormalizer(video)
-    with open(assets.get_normalization_cache_path(args.model), "wb") as fd:
-        pickle.dump(normalizer, fd)
+    normalizer.save(assets.get_normalization_cache_path(args.model))
     network = SpeechEnhancementNetwork.build(mixed.shape[1:], video.shape[1:], seed=args.seed)
     network.save(assets.get_model_cache_path(args.model))
 
@@ -220,18 +255,21 @@ def train(args):
 def predict(args):
     assets = AssetManager(args.base_dir)
     storage = PredictionStorage(assets.create_prediction_storage(args.model, args.data_name))
-    network = SpeechEnhancementNetwork.load(assets.get_model_cache_path(args.model), compute_dtype=args.dtype)
-    with open(assets.get_normalization_cache_path(args.model), "rb") as fd:   # written by this CLI's train
-        video_normalizer = pickle.load(fd)
+    model_path = assets.get_model_cache_path(args.model)
+    if not os.path.exists(model_path) and os.path.exists(assets.get_keras_model_path(args.model)):
+        raise SystemExit("%s is a Keras model: convert it once with\n  /opt/conda/bin/python3.9 tools/keras_h5_to_avse.py "
+                         "%s %s" % (assets.get_keras_model_path(args.model), assets.get_keras_model_path(args.model),
+                                    model_path))
+    network = SpeechEnhancementNetwork.load(model_path, compute_dtype=args.dtype)
+    video_normalizer = data_processor.VideoNormalizer.load(assets.get_normalization_cache_path(args.model))
     samples = load_preprocessed_blob(assets.get_preprocessed_blob_path(args.data_name))
     for sample in samples:
         try:
             print("predicting (%s, %s)..." % (sample.video_file_path, sample.noise_file_path))
-            # normalize + evaluate + predict, with the normaliser fused into the first video conv
-            loss = network.evaluate(sample.mixed_spectrograms, sample.video_samples, sample.speech_spectrograms,
-                                    video_normalizer=video_normalizer)
+            # normalize + evaluate + predict as ONE forward, the normaliser fused into the first video conv
+            pred, loss = network.predict_and_evaluate(sample.mixed_spectrograms, sample.video_samples,
+                                                      sample.speech_spectrograms, video_normalizer=video_normalizer)
             print("loss: %f" % loss)
-            pred = network.predict(sample.mixed_spectrograms, sample.video_samples, video_normalizer=video_normalizer)
             signal = data_processor.reconstruct_speech_signal(sample.mixed_signal, pred, sample.video_frame_rate)
             storage.save_prediction(sample, signal)
         except Exception:  # noqa: BLE001 — mirrors speech_enhancer.py:87-88

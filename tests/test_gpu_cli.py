@@ -46,7 +46,7 @@ def test_cli_preprocess_train_predict(gpu, tmp_path):
     out = run(["-bd", base, "preprocess", "-dn", "d", "-ds", ds, "-n", noise], tmp)
     assert "preprocessed 1 samples" in out
     run(["-bd", base, "train", "-mn", "m", "-tdn", "d", "-vdn", "d", "--init-only"], tmp)
-    assert os.path.exists(os.path.join(base, "cache", "models", "m", "model.h5py"))
+    assert os.path.exists(os.path.join(base, "cache", "models", "m", "model.safetensors"))
     out = run(["-bd", base, "predict", "-mn", "m", "-dn", "d"], tmp)
     assert "loss:" in out
     enhanced = glob.glob(os.path.join(base, "out", "m", "d", "*", "*", "*", "enhanced.wav"))

@@ -166,6 +166,18 @@ def test_fused_tail_matches_unfused(gpu, monkeypatch, dtype, tol):
     assert rel_rms(fused, unfused) <= tol, rel_rms(fused, unfused)
 
 
+def test_predict_and_evaluate_single_forward(gpu):
+    """The CLI's one-forward predict prints the loss evaluate() reports (speech_enhancer.py:76-79)."""
+    from avse_amd.network import SpeechEnhancementNetwork
+    net = SpeechEnhancementNetwork.build((80, 20), (128, 128, 5), seed=3)
+    mel, video = make_inputs(4, 8)
+    target = np.random.default_rng(1).normal(size=mel.shape).astype(np.float32)
+    pred, loss = net.predict_and_evaluate(mel, video, target)
+    assert np.array_equal(pred, net.predict(mel, video))
+    assert abs(loss - net.evaluate(mel, video, target)) <= 1e-6 * abs(loss)
+    assert abs(loss - K.mse(pred[:, :, :], target)) <= 1e-5 * abs(loss)
+
+
 def test_mse_matches(gpu):
     from avse_amd import ops
     rng = np.random.default_rng(0)

@@ -120,3 +120,37 @@ def test_ops_refuse_cpu_tensors():
     from avse_amd import ops
     with pytest.raises(TypeError):
         ops.spectrogram(torch.zeros(1, 3200))
+
+
+def test_preprocessed_blob_and_normalizer_round_trip(tmp_path):
+    """The CLI's caches are pickle-free: list[Sample] as one .npz (+ JSON metadata), the normaliser as .npz;
+    both read back with allow_pickle=False."""
+    from avse_amd import data_processor
+    from avse_amd.audio_io import AudioSignal
+    from avse_amd.speech_enhancer import Sample, load_preprocessed_blob, save_preprocessed_blob
+    rng = np.random.default_rng(0)
+    samples = []
+    for i in range(3):
+        n = 2 + i
+        samples.append(Sample("spk%d" % i, "/v/%d.npy" % i, "/a/%d.wav" % i, "/n/%d.wav" % i,
+                              rng.normal(size=(n, 128, 128, 5)).astype(np.float32),
+                              rng.normal(size=(n, 80, 20)).astype(np.float32),
+                              rng.normal(size=(n, 80, 20)).astype(np.float32),
+                              rng.normal(size=(n, 80, 20)).astype(np.float32),
+                              AudioSignal(rng.normal(size=3200 * n).astype(np.float32), 16000), 25.0 + i))
+    p = str(tmp_path / "d.npz")
+    save_preprocessed_blob(p, samples)
+    got = load_preprocessed_blob(p)
+    assert len(got) == 3
+    for a, b in zip(samples, got):
+        for f in ("speaker_id", "video_file_path", "speech_file_path", "noise_file_path", "video_frame_rate"):
+            assert getattr(a, f) == getattr(b, f)
+        for f in ("video_samples", "mixed_spectrograms", "speech_spectrograms", "noise_spectrograms"):
+            assert np.array_equal(getattr(a, f), getattr(b, f))
+        assert np.array_equal(a.mixed_signal.get_data(), b.mixed_signal.get_data())
+        assert b.mixed_signal.get_sample_rate() == 16000
+    norm = data_processor.VideoNormalizer(samples[0].video_samples)
+    q = str(tmp_path / "normalization.npz")
+    norm.save(q)
+    back = data_processor.VideoNormalizer.load(q)
+    assert np.array_equal(back.mean_image, norm.mean_image) and np.array_equal(back.std_image, norm.std_image)
