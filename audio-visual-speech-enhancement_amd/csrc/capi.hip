@@ -159,6 +159,9 @@ struct avse_ctx {
     float* mse_partial = nullptr;
     char* arena = nullptr;
     size_t arena_bytes = 0;
+    // side stream for the audio branch of the forward (runs concurrently with the video encoder)
+    hipStream_t side = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
 };
 
 struct GpuLayer {
@@ -226,6 +229,12 @@ bool no_igemm() {
 }
 // AVSE_UNFUSED_TAIL=1 (read per forward, for the layer-by-layer tests): run d_deconv6 as its own kernel so the
 // 64-channel d_deconv5 activation is materialised in the scratch buffer avse_debug_scratch exposes
+// AVSE_SERIAL=1 (read per forward): run the audio branch on the caller's stream too
+bool serial_forward() {
+    const char* e = std::getenv("AVSE_SERIAL");
+    return e && e[0] == '1';
+}
+
 bool unfused_tail() {
     const char* e = std::getenv("AVSE_UNFUSED_TAIL");
     return e && e[0] == '1';
@@ -639,6 +648,9 @@ void avse_ctx_destroy(avse_ctx* c) {
     (void)hipFree(c->umax);
     (void)hipFree(c->mse_partial);
     (void)hipFree(c->arena);
+    if (c->side) (void)hipStreamDestroy(c->side);
+    if (c->fork) (void)hipEventDestroy(c->fork);
+    if (c->join) (void)hipEventDestroy(c->join);
     delete c;
 }
 
@@ -817,7 +829,23 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
     // the halo-tiled v_conv1 reads the raw video and normalises it itself
     if (L(5).halo == HALO_NONE && (rc = launch_video_prep(video, vmean, vstd, buf(B_VIN), N, dt, s))) return rc;
     if ((rc = mark())) return rc;
-    if ((rc = launch_audio_prep(audio, buf(B_AIN), N, dt, s)) || (rc = mark())) return rc;
+    // The audio branch (prep + a_conv1..5 -> concat[0:3200]) shares no buffer with the video encoder until the
+    // fusion dense: it runs on the context's side stream, forked from and joined back into s, so its short,
+    // latency-bound kernels overlap the video encoder (the profiling path keeps one stream for per-stage
+    // events; AVSE_SERIAL=1 forces it).  The fork waits for everything enqueued on s before this call.
+    const bool concurrent = ev == nullptr && !serial_forward();
+    hipStream_t sa = s;
+    if (concurrent) {
+        if (!c->side) {
+            AVSE_HIP_CHECK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+            AVSE_HIP_CHECK(hipEventCreateWithFlags(&c->fork, hipEventDisableTiming));
+            AVSE_HIP_CHECK(hipEventCreateWithFlags(&c->join, hipEventDisableTiming));
+        }
+        AVSE_HIP_CHECK(hipEventRecord(c->fork, s));
+        AVSE_HIP_CHECK(hipStreamWaitEvent(c->side, c->fork, 0));
+        sa = c->side;
+    }
+    if ((rc = launch_audio_prep(audio, buf(B_AIN), N, dt, sa)) || (rc = mark())) return rc;
     // audio encoder (network.py:88-109)
     const int a_in[5] = {B_AIN, B_A1, B_A2, B_A3, B_A4};
     for (int i = 0; i < 5; ++i) {
@@ -825,8 +853,9 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
         const long long in_cs = (long long)G.def.hin * G.def.win * (i == 0 ? G.cin_pad : G.def.cin);
         ConvArgs a = (i < 4) ? conv_args(G, buf(a_in[i]), in_cs, buf(a_in[i + 1]), (long long)G.ho * G.wo * G.def.cout, G.def.cout, 0, N)
                              : conv_args(G, buf(a_in[i]), in_cs, buf(B_CAT), 5248, G.def.cout, 0, N);   // Flatten -> concat[0:3200]
-        if ((rc = run_conv(a, dt, s)) || (rc = mark())) return rc;
+        if ((rc = run_conv(a, dt, sa)) || (rc = mark())) return rc;
     }
+    if (concurrent) AVSE_HIP_CHECK(hipEventRecord(c->join, sa));
     // video encoder (network.py:138-175)
     const int v_in[6] = {B_VIN, B_V1, B_V2, B_V3, B_V4, B_V5};
     for (int i = 0; i < 6; ++i) {
@@ -844,6 +873,7 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
         if (i == 5) split(a);
         if ((rc = run_conv(a, dt, s)) || (rc = mark())) return rc;
     }
+    if (concurrent) AVSE_HIP_CHECK(hipStreamWaitEvent(s, c->join, 0));
     // fusion + decoder dense (network.py:53-58, :66-78)
     {
         ConvArgs a = conv_args(L(11), buf(B_CAT), 5248, buf(B_E1), 1312, 1312, 0, N);
