@@ -261,7 +261,10 @@ size_t split_ws_bytes(int64_t N, int dtype) {
     size_t mx = 0;
     for (const auto& x : g) {
         const int ks = choose_ksplit(x.M, x.Co, x.kpad, dtype);
-        if (ks > 1) mx = std::max(mx, (size_t)ks * (size_t)x.M * (size_t)x.Co * 4);
+        // k_conv's partials cover whole 128 x BN tiles (MFMA-native order), igemm's are [ks][M][Co]
+        const int bn = x.Co <= 64 ? 64 : 128;
+        const size_t mp = (size_t)((x.M + 127) / 128) * 128, np = (size_t)((x.Co + bn - 1) / bn) * bn;
+        if (ks > 1) mx = std::max(mx, (size_t)ks * mp * np * 4);
     }
     return mx;
 }

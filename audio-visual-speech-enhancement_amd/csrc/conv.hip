@@ -285,20 +285,17 @@ __global__ __launch_bounds__(256, (conv_occupancy<BN, FAST>())) void k_conv(Conv
 #undef AS
 #undef BS
     // ---- epilogue: scale/shift (bias + BN), [pool], LeakyReLU, strided NHWC store ----
-    if (a.ksplit > 1) {   // raw fp32 partial sums; k_splitk_reduce applies the layer tail
-        float* part = a.partial + (size_t)zsplit * M * a.Co;
+    if (a.ksplit > 1) {
+        // raw fp32 partial sums in MFMA-native order, consumed only by k_splitk_reduce_tiles: unit
+        // ((zsplit * tiles + tile) * NI*NJ + i*NJ + j) * 256 + tid is this thread's f32x4 of fragment (i, j)
+        // (4 rows of one column), so every store instruction writes 4 contiguous KB (row-major partials
+        // were 4-byte stores strided by Cout: 64 per lane, the bulk of a short-K dense layer's time)
+        const int tiles = gridDim.x * gridDim.y, tile = blockIdx.y * gridDim.x + blockIdx.x;
+        f32x4* part = reinterpret_cast<f32x4*>(a.partial) + (size_t)(zsplit * tiles + tile) * (NI * NJ) * 256 + tid;
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            const int n = n0 + wn * WN + 16 * j + fr;
-            if (n >= a.Co) continue;
+        for (int i = 0; i < NI; ++i)
 #pragma unroll
-            for (int i = 0; i < NI; ++i) {
-                const int mb = m0 + wm * 64 + 16 * i + 4 * fg;
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    if (mb + r < M) part[(size_t)(mb + r) * a.Co + n] = acc[i][j][r];
-            }
-        }
+            for (int j = 0; j < NJ; ++j) part[(i * NJ + j) * 256] = acc[i][j];
         return;
     }
     T* out = reinterpret_cast<T*>(a.out);
@@ -434,6 +431,45 @@ __global__ void k_splitk_reduce(ConvArgs a) {
             o = clip * a.out_clip_stride + (long long)(oy * a.Wo + ox) * a.out_pix_stride + a.out_c_off + n;
         }
         out[o] = from_f<T>(x);
+    }
+}
+
+// split-K tail for k_conv's MFMA-native partials: one thread per f32x4 unit (4 rows of one column of one
+// fragment), summed over the splits, then scale/shift, [2x2 max pool: the 4 rows are one window],
+// LeakyReLU, strided store.  Single phase (dense layers, v_conv6).
+template <typename T, int BN>
+__global__ void k_splitk_reduce_tiles(ConvArgs a) {
+    constexpr int WN = BN / 2, NJ = WN / 16, NIJ = 4 * NJ;
+    const int M = a.N * a.Hq * a.Wq;
+    const int mtiles = (M + BM - 1) / BM, tiles = mtiles * ((a.Co + BN - 1) / BN);
+    const long long total = (long long)tiles * NIJ * 256;
+    const f32x4* part = reinterpret_cast<const f32x4*>(a.partial);
+    T* out = reinterpret_cast<T*>(a.out);
+    for (long long u = blockIdx.x * (long long)blockDim.x + threadIdx.x; u < total; u += (long long)gridDim.x * blockDim.x) {
+        const int tid = (int)(u & 255), ij = (int)((u >> 8) % NIJ), tile = (int)((u >> 8) / NIJ);
+        const int bx = tile % mtiles, by = tile / mtiles, i = ij / NJ, j = ij % NJ;
+        const int wid = tid >> 6, lane = tid & 63;
+        const int n = by * BN + (wid & 1) * WN + 16 * j + (lane & 15);
+        const int mb = bx * BM + (wid >> 1) * 64 + 16 * i + 4 * (lane >> 4);
+        if (n >= a.Co || mb >= M) continue;
+        f32x4 acc = part[u];
+        for (int z = 1; z < a.ksplit; ++z) acc += part[(size_t)z * total + u];
+        const float sc = a.scale[n], sh = a.shift[n];
+        if (a.pool) {
+            float x = fmaxf(fmaxf(acc[0] * sc + sh, acc[1] * sc + sh), fmaxf(acc[2] * sc + sh, acc[3] * sc + sh));
+            if (a.act) x = x >= 0.f ? x : LRELU * x;
+            const int p = mb >> 2, pw = a.Wq >> 1, phh = a.Hq >> 1;
+            const int clip = p / (phh * pw), rr = p - clip * phh * pw;
+            out[clip * a.out_clip_stride + (long long)rr * a.out_pix_stride + a.out_c_off + n] = from_f<T>(x);
+        } else {
+            for (int r = 0; r < 4 && mb + r < M; ++r) {
+                float x = acc[r] * sc + sh;
+                if (a.act) x = x >= 0.f ? x : LRELU * x;
+                const int m = mb + r, clip = m / (a.Hq * a.Wq), rr = m - clip * a.Hq * a.Wq;
+                const int oy = (rr / a.Wq) * a.oys, ox = (rr % a.Wq) * a.oxs;
+                out[clip * a.out_clip_stride + (long long)(oy * a.Wo + ox) * a.out_pix_stride + a.out_c_off + n] = from_f<T>(x);
+            }
+        }
     }
 }
 
@@ -576,10 +612,22 @@ int launch_conv(const ConvArgs& a, int dtype, hipStream_t s) {
         }
     }
     AVSE_HIP_CHECK(hipGetLastError());
-    if (a.ksplit > 1) return launch_splitk_reduce(a, dtype, s);
+    if (a.ksplit > 1) {
+        const long long units = (long long)grid.x * grid.y * (BN / 2 / 16 * 4) * 256;
+        const dim3 rg(grid_for(units, 256));
+        if (dtype == 1) {
+            if (BN == 64) hipLaunchKernelGGL((k_splitk_reduce_tiles<bf16_t, 64>), rg, dim3(256), 0, s, a);
+            else hipLaunchKernelGGL((k_splitk_reduce_tiles<bf16_t, 128>), rg, dim3(256), 0, s, a);
+        } else {
+            if (BN == 64) hipLaunchKernelGGL((k_splitk_reduce_tiles<float, 64>), rg, dim3(256), 0, s, a);
+            else hipLaunchKernelGGL((k_splitk_reduce_tiles<float, 128>), rg, dim3(256), 0, s, a);
+        }
+        AVSE_HIP_CHECK(hipGetLastError());
+    }
     return 0;
 }
 
+// row-major [ksplit][M][Co] partials (igemm.hip's split-K)
 int launch_splitk_reduce(const ConvArgs& a, int dtype, hipStream_t s) {
     const int M = a.N * a.Hq * a.Wq;
     const long long total = (long long)(a.pool ? M / 4 : M) * a.Co;
