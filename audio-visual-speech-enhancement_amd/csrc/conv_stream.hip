@@ -52,8 +52,10 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 // 16-B slot swizzles of the LDS images (found by exhaustive search over the ds_read_b128 lane groups of
 // the v_mfma_f32_32x32x16_bf16 operand layout, every tap offset and all three tile geometries)
-__device__ __forceinline__ int wswz(int row) { return (row >> 2) & 3; }
-__device__ __forceinline__ int hsw(int y) { return y & 3; }
+// M16 = the v_mfma_f32_16x16x32_bf16 operand layout (lane l: row l & 15, 16-B k-group l >> 4), 4x4-pixel
+// fragment blocks: found by the same search (tools/lds_swizzle_search.py)
+template <bool M16> __device__ __forceinline__ int wswz(int row) { return M16 ? 2 * ((row >> 2) & 1) : (row >> 2) & 3; }
+template <bool M16> __device__ __forceinline__ int hsw(int y) { return M16 ? 2 * (y & 1) : y & 3; }
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, long long bytes) {
     const int nrec = bytes > kOOB ? kOOB : (bytes < 0 ? 0 : (int)bytes);
@@ -90,7 +92,7 @@ struct StreamGeom {
     // slice and land in a 2-slot LDS ring; 3 halo chunk slots
     static constexpr int LAT = LAT_, WD = LAT + 2, NHS = 3, PAIR = 2 * NTAP;
     static constexpr int LDS = NHS * CSLOT + 2 * WSLOT;
-    static_assert(LDS <= 160 * 1024, "LDS");   // one workgroup per CU: ~250 VGPRs x 8 waves fill the register file
+    static_assert(LDS + 1024 <= 160 * 1024, "LDS");   // one workgroup per CU: ~250 VGPRs x 8 waves fill the register file
     static_assert(NCLIP * TH * TW == 256, "tile = 256 conv pixels (4 waves x 4 fragments)");
     static_assert(PAIR % LAT == 0 && LAT < NTAP, "the ring set of a step is compile-time");
     // chunk g+2's pieces are loaded at taps 0..HPW-1 of chunk g and written LAT steps later, before
@@ -114,7 +116,7 @@ struct StreamGeom {
 // loop, 2 = no weight streaming in the loop, 4 = no barrier/wait, 8 = no fragment reads, 16 = no MFMAs,
 // 64 = every tile reads clip 0's window (L2-resident input), 128 = s_memtime per step: cycles working /
 // waiting (vmcnt, lgkmcnt) / in the barrier, per wave, into a.prof[(block * 8 + wave) * 4 + {0,1,2, 3=steps}]
-template <int KS, int TH, int TW, int NCLIP, int LAT_ = StreamGeom<KS, TH, TW, NCLIP>::LAT, int ABL = 0>
+template <int KS, int TH, int TW, int NCLIP, bool M16 = true, int LAT_ = StreamGeom<KS, TH, TW, NCLIP>::LAT, int ABL = 0>
 __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
     using G = StreamGeom<KS, TH, TW, NCLIP, LAT_>;
     constexpr int HH = G::HH, HW = G::HW, HPIX = G::HPIX, HPW = G::HPW, NTAP = G::NTAP;
@@ -137,14 +139,19 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
     const int tiles_x = a.Wc / TW, tiles_y = a.Hc / TH;
     const int tiles_per_clip = tiles_x * tiles_y;
     const int ntiles = ((a.N + NCLIP - 1) / NCLIP) * tiles_per_clip;
-    const int nmine = (ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+    // XCD-aware tile order: workgroups are dispatched round-robin over the 8 XCDs (XCD = linear id % 8), so
+    // slot bx % 8 * (gx / 8) + bx / 8 gives each XCD a contiguous run of tiles per round (whole clips): the
+    // halo rows neighbouring tiles share are then fetched into that XCD's L2 once
+    const int gxs = (int)gridDim.x;
+    const int slot = (gxs % 8 == 0) ? ((int)blockIdx.x % 8) * (gxs / 8) + (int)blockIdx.x / 8 : (int)blockIdx.x;
+    const int nmine = (ntiles - slot + gxs - 1) / gxs;
     if (nmine <= 0) return;
     const int nchunks = nmine * nch;
     const int co0 = blockIdx.y * 128;
     const long long clip_bytes = (long long)a.Hc * a.Wc * a.Ci * 2;
 
     auto tile_origin = [&](int k, int& clip0, int& oy0, int& ox0) {
-        const int t = (int)blockIdx.x + k * (int)gridDim.x;
+        const int t = slot + k * gxs;
         clip0 = (ABL & 64) ? 0 : (t / tiles_per_clip) * NCLIP;
         const int tt = t % tiles_per_clip;
         oy0 = (tt / tiles_x) * TH;
@@ -161,7 +168,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
             const int row = 32 * w + 16 * u + (lane >> 2), sl = lane & 3;
-            wvoff[u] = row * 64 + ((sl ^ wswz(row)) << 4);
+            wvoff[u] = row * 64 + ((sl ^ wswz<M16>(row)) << 4);
         }
         char* const wdst = wring + 2048 * w + lane * 16;   // + slot * WSLOT + 1024 u
         auto tile_rsrc = [&](int clip0) {
@@ -180,7 +187,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
                 const int cl = p / (HH * HW), rr = p - cl * (HH * HW);
                 const int y = rr / HW, x = rr - y * HW;
                 const int iy = oy0 + y - PAD, ix = ox0 + x - PAD;
-                const int off = ((cl * hc + iy) * wc + ix) * ci2 + ((sl ^ hsw(y)) << 4);
+                const int off = ((cl * hc + iy) * wc + ix) * ci2 + ((sl ^ hsw<M16>(y)) << 4);
                 const bool ok = (P < G::HPIECES) & (p < HPIX) & ((unsigned)iy < (unsigned)hc) & ((unsigned)ix < (unsigned)wc);
                 vo[pc] = ok ? off : kOOB;
             }
@@ -321,6 +328,122 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
     // =============================== compute waves ===============================
     // the MFMA stream gets issue priority over the co-resident loader wave of its SIMD (-2% time)
     __builtin_amdgcn_s_setprio(2);
+    if constexpr (M16) {
+        // v_mfma_f32_16x16x32_bf16 (lane l: row / column l & 15, channels 8 (l >> 4) .. +8 of the slice): on
+        // random data the chip holds a higher clock under this shape than under 32x32x16 at equal cycles per
+        // FLOP (MI355X_MICROARCH.md, DVFS item 7).  Wave w owns 4 fragment blocks of 4x4 conv pixels (blocks
+        // 4w .. 4w+3 of the tile, row-major per clip) x 128 output channels (8 blocks of 16): per K-slice
+        // 4 A + 8 B fragment reads (12 KB, as before) for 32 MFMAs.  Block row r = 4 q + 2 dy + dx is pixel
+        // (2 (q >> 1) + dy, 2 (q & 1) + dx): a lane's 4 accumulator rows 4 (l >> 4) .. +3 are pool window l >> 4.
+        constexpr int SBX = TW / 4, SB = (TH / 4) * SBX;   // 4x4 blocks per row / clip
+        static_assert(TH % 4 == 0 && TW % 4 == 0 && (SBX % 4 == 0 || SBX == 2) && SB % 4 == 0, "block geometry");
+        const int r16 = lane & 15, kg = lane >> 4;
+        const int q = r16 >> 2, dy = (r16 >> 1) & 1, dx = r16 & 1;
+        const int b0 = 4 * w, cl0 = b0 / SB, bb0 = b0 % SB;
+        const int by0 = bb0 / SBX, bx0 = bb0 % SBX;
+        const int ab = ((cl0 * HH + 4 * by0 + 2 * (q >> 1) + dy) * HW + 4 * bx0 + 2 * (q & 1) + dx) * 64;
+        // block i of the wave relative to block 0 (bx0 % SBX == 0 or SBX == 2 with bx0 == 0)
+        auto boff_of = [](int i) { return ((i / SBX) * 4 * HW + (i % SBX) * 4) * 64; };
+        const int bo16 = r16 * 64 + ((kg ^ wswz<true>(r16)) << 4);   // + 1024 j for column block j
+        auto frags = [&](int hs, int tap, int ws, i32x4 (&fa)[4], i32x4 (&fb)[8]) {
+            const int ky = tap / KS, kx = tap % KS;
+            const int pos = (kg ^ hsw<true>(dy + ky)) << 4;
+            const char* hp = halo + hs * CSLOT + ab + (ky * HW + kx) * 64 + pos;
+            const char* wp = wring + ws * WSLOT + bo16;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) fa[i] = *reinterpret_cast<const i32x4*>(hp + boff_of(i));
+#pragma unroll
+            for (int j = 0; j < 8; ++j) fb[j] = *reinterpret_cast<const i32x4*>(wp + 1024 * j);
+        };
+        // BN scale / shift of this column block in LDS (past the rings), read in the epilogue: 16 VGPRs held
+        // for the whole tile would spill the 256-register budget (128 accumulators + 2 x 12 fragments)
+        float* const ssh = reinterpret_cast<float*>(lds + G::LDS);
+        if (w == 0) {
+            ssh[lane] = a.scale[co0 + lane];
+            ssh[lane + 64] = a.scale[co0 + 64 + lane];
+            ssh[128 + lane] = a.shift[co0 + lane];
+            ssh[192 + lane] = a.shift[co0 + 64 + lane];
+        }
+        barrier_raw();   // the loaders' prologue (and ssh: the compute waves' LDS stores are drained by the
+                         // lgkmcnt(0) wait before the next barrier, which precedes any epilogue)
+
+        f32x4 acc[4][8];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[i][j] = (f32x4){};
+        const int Wp = a.Wc / 2;
+        auto epilogue = [&](int clip0, int oy0, int ox0) {
+            const long long cbytes = a.out_clip_stride * 2;
+            const __amdgpu_buffer_rsrc_t ors = make_rsrc(reinterpret_cast<const char*>(a.out) + (long long)clip0 * cbytes,
+                                                         (long long)(a.N - clip0) * cbytes);
+            const int cbase = cl0 * (int)a.out_clip_stride + a.out_c_off + co0 + r16;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int py = (oy0 + 4 * (by0 + i / SBX)) / 2 + (kg >> 1);
+                const int px = (ox0 + 4 * (bx0 + i % SBX)) / 2 + (kg & 1);
+                const int pbase = cbase + (py * Wp + px) * a.out_pix_stride;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float mx = fmaxf(fmaxf(acc[i][j][0], acc[i][j][1]), fmaxf(acc[i][j][2], acc[i][j][3]));
+                    float x = fmaf(mx, ssh[16 * j + r16], ssh[128 + 16 * j + r16]);
+                    x = fmaxf(x, LRELU * x);
+                    __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (bf16_t)x), ors,
+                                                          (pbase + 16 * j) * 2, 0, 0);
+                    // restart the chain in place: x * 0 (not a constant, which the register allocator would
+                    // materialise elsewhere and then shuffle — that spilled the 256-register budget)
+                    acc[i][j] *= 0.f;
+                }
+            }
+        };
+
+        int tap1 = 1, hs1 = 0;
+        i32x4 fa[4], fb[8], na[4], nb[8];
+        frags(0, 0, 0, fa, fb);
+        if constexpr ((ABL & 8) != 0) frags(0, 0, 0, na, nb);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        barrier_raw();   // slice 0 read: the loaders may now overwrite weight slot 0
+
+        auto cstep = [&](auto first, int t, i32x4 (&ca)[4], i32x4 (&cb)[8], i32x4 (&xa)[4], i32x4 (&xb)[8]) {
+            if constexpr (!(ABL & 8)) frags(hs1, tap1, (t + 1) & 1, xa, xb);
+            if constexpr (!(ABL & 16))
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 8; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                            __builtin_bit_cast(bf16x8, ca[i]), __builtin_bit_cast(bf16x8, cb[j]), acc[i][j], 0, 0, 0);
+#pragma unroll
+            for (int r = 0; r < 12; ++r) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);   // MFMA
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
+            }
+            __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (!(ABL & 4)) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                barrier_raw();
+            }
+            if (++tap1 == NTAP) {
+                tap1 = 0;
+                hs1 = hs1 == 2 ? 0 : hs1 + 1;
+            }
+        };
+        int t = 0;
+        int cur_clip0, cur_oy0, cur_ox0;
+        for (int kt = 0; kt < nmine; ++kt) {
+            cstep(std::true_type{}, t, fa, fb, na, nb);
+            cstep(std::false_type{}, t + 1, na, nb, fa, fb);
+            t += 2;
+            for (int s = 2; s < spt; s += 2, t += 2) {
+                cstep(std::false_type{}, t, fa, fb, na, nb);
+                cstep(std::false_type{}, t + 1, na, nb, fa, fb);
+            }
+            tile_origin(kt, cur_clip0, cur_oy0, cur_ox0);
+            epilogue(cur_clip0, cur_oy0, cur_ox0);
+        }
+        return;
+    }
     // fragment geometry (v_mfma_f32_32x32x16_bf16: lane l holds row/column l & 31 and k-half hi = l >> 5).
     // Wave w owns blocks 2w, 2w+1; block row r = 4 q + 2 dy + dx is pixel (2 (q >> 2) + dy, 2 (q & 3) + dx)
     // of the block: rows 4q..4q+3 are 2x2 pool window q
@@ -338,12 +461,12 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
     const int ylo = 2 * ((r32 >> 4) & 1) + ((r32 >> 1) & 1);          // this lane's pixel y mod 4
     int boffm[2];                                                      // + 2048 jb for column block jb
 #pragma unroll
-    for (int m = 0; m < 2; ++m) boffm[m] = r32 * 64 + (((2 * m + hi) ^ wswz(r32)) << 4);
+    for (int m = 0; m < 2; ++m) boffm[m] = r32 * 64 + (((2 * m + hi) ^ wswz<M16>(r32)) << 4);
     // fragments of K-slice (chunk slot hs, tap) with weights in ring slot ws: fa[2 i + m] = block i,
     // channels 16 m .. 16 m + 15 of the slice; fb[2 jb + m] = output channels 32 jb .., same channels
     auto frags = [&](int hs, int tap, int ws, i32x4 (&fa)[4], i32x4 (&fb)[8]) {
         const int ky = tap / KS, kx = tap % KS;
-        const int sw = hsw(ylo + ky);
+        const int sw = hsw<M16>(ylo + ky);
         const char* hp = halo + hs * CSLOT + ab + (ky * HW + kx) * 64;
         const char* wp = wring + ws * WSLOT;
 #pragma unroll
@@ -468,13 +591,13 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
         }
 }
 
-template <int KS, int TH, int TW, int NCLIP>
+template <int KS, int TH, int TW, int NCLIP, bool M16>
 int launch_stream(const HaloArgs& a, hipStream_t s) {
     using G = StreamGeom<KS, TH, TW, NCLIP>;
     static bool attr = false;
     if (!attr) {
-        AVSE_HIP_CHECK(hipFuncSetAttribute((const void*)k_conv_stream<KS, TH, TW, NCLIP>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
+        AVSE_HIP_CHECK(hipFuncSetAttribute((const void*)k_conv_stream<KS, TH, TW, NCLIP, M16>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS + 1024));
         attr = true;
     }
     if (a.Hc % TH || a.Wc % TW || a.Co % 128 || a.Ci % 64) {   // an even number of 32-channel chunks
@@ -490,18 +613,25 @@ int launch_stream(const HaloArgs& a, hipStream_t s) {
     int gx = ncu / cob;
     gx = gx >= 8 ? gx / 8 * 8 : (gx < 1 ? 1 : gx);
     if (gx > tiles) gx = tiles;
-    hipLaunchKernelGGL((k_conv_stream<KS, TH, TW, NCLIP>), dim3(gx, cob), dim3(512), G::LDS, s, a);
+    hipLaunchKernelGGL((k_conv_stream<KS, TH, TW, NCLIP, M16>), dim3(gx, cob), dim3(512), G::LDS + 1024, s, a);
     AVSE_HIP_CHECK(hipGetLastError());
     return 0;
 }
 
 }  // namespace
 
+// AVSE_MFMA32=1 (read per launch): the v_mfma_f32_32x32x16_bf16 compute waves (A/B switch)
+static bool use_mfma32() {
+    const char* e = std::getenv("AVSE_MFMA32");
+    return e && e[0] == '1';
+}
+
 int launch_conv_stream(const HaloArgs& a, hipStream_t s) {
+    const bool m32 = use_mfma32();
     switch (a.variant) {
-        case HALO_K5: return launch_stream<5, 16, 16, 1>(a, s);
-        case HALO_K3_16: return launch_stream<3, 16, 16, 1>(a, s);
-        case HALO_K3_8: return launch_stream<3, 8, 8, 4>(a, s);
+        case HALO_K5: return m32 ? launch_stream<5, 16, 16, 1, false>(a, s) : launch_stream<5, 16, 16, 1, true>(a, s);
+        case HALO_K3_16: return m32 ? launch_stream<3, 16, 16, 1, false>(a, s) : launch_stream<3, 16, 16, 1, true>(a, s);
+        case HALO_K3_8: return m32 ? launch_stream<3, 8, 8, 4, false>(a, s) : launch_stream<3, 8, 8, 4, true>(a, s);
     }
     set_error("stream conv: unsupported variant");
     return 3;

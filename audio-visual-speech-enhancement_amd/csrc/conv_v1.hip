@@ -66,11 +66,16 @@ __global__ __launch_bounds__(512, 1) void k_conv_v1(HaloArgs a) {
 
     const int tiles_x = a.Wc / TW, tiles_per_clip = tiles_x * (a.Hc / TH);
     const int ntiles = a.N * tiles_per_clip;
-    const int nmine = (ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+    // XCD-aware tile order: workgroups are dispatched round-robin over the 8 XCDs (XCD = linear id % 8), so
+    // slot bx % 8 * (gx / 8) + bx / 8 gives each XCD a contiguous run of tiles per round (whole clips): the
+    // halo rows neighbouring tiles share are then fetched into that XCD's L2 once
+    const int gxs = (int)gridDim.x;
+    const int slot = (gxs % 8 == 0) ? ((int)blockIdx.x % 8) * (gxs / 8) + (int)blockIdx.x / 8 : (int)blockIdx.x;
+    const int nmine = (ntiles - slot + gxs - 1) / gxs;
     if (nmine <= 0) return;
     const int total = nmine * NSL;
     auto tile_origin = [&](int k, int& clip, int& oy0, int& ox0) {
-        const int t = (int)blockIdx.x + k * (int)gridDim.x;
+        const int t = slot + k * gxs;
         clip = t / tiles_per_clip;
         const int tt = t - clip * tiles_per_clip;
         oy0 = (tt / tiles_x) * TH;

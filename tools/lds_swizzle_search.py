@@ -1,0 +1,58 @@
+"""Exhaustive bank-conflict check / search of the k_conv_stream LDS images for the v_mfma_f32_16x16x32_bf16
+operand layout (lane l reads row l & 15, 16-B k-group l >> 4 with one ds_read_b128).
+
+ds_read_b128 serves a wave in four 16-lane groups (MI355X_MICROARCH.md, LDS table); a group is conflict-free
+when its 16 lanes hit 16 distinct 16-B bank units of a 256-B line.  Checked for every tap offset and for the
+three tile geometries of conv_stream.hip (5x5 16x16, 3x3 16x16, 3x3 8x8 x 4 clips).
+    python tools/lds_swizzle_search.py
+"""
+import itertools
+
+GROUPS = [[0, 1, 2, 3, 12, 13, 14, 15] + list(range(20, 28)), list(range(4, 12)) + [16, 17, 18, 19, 28, 29, 30, 31]]
+GROUPS += [[g + 32 for g in grp] for grp in GROUPS]
+GEOMS = [dict(KS=5, TH=16, TW=16, NC=1), dict(KS=3, TH=16, TW=16, NC=1), dict(KS=3, TH=8, TW=8, NC=4)]
+
+
+def lane_pixel(lane):
+    """Row r = 4 q + 2 dy + dx of a 4x4-pixel block -> pixel (2 (q >> 1) + dy, 2 (q & 1) + dx); k-group."""
+    r, k = lane & 15, lane >> 4
+    q, dy, dx = r >> 2, (r >> 1) & 1, r & 1
+    return 2 * (q >> 1) + dy, 2 * (q & 1) + dx, k
+
+
+def halo_ok(f):
+    for g in GEOMS:
+        ks = g["KS"]
+        hh, hw = g["TH"] + ks - 1, g["TW"] + ks - 1
+        for cl in range(g["NC"]):
+            for y0 in range(0, g["TH"], 4):
+                for x0 in range(0, g["TW"], 4):
+                    for ky in range(ks):
+                        for kx in range(ks):
+                            for grp in GROUPS:
+                                units = set()
+                                for lane in grp:
+                                    py, px, k = lane_pixel(lane)
+                                    y, x = y0 + py + ky, x0 + px + kx
+                                    p = (cl * hh + y) * hw + x
+                                    units.add((4 * (p % 4) + (k ^ f(y))) % 16)
+                                if len(units) < 16:
+                                    return False
+    return True
+
+
+def weights_ok(tab):
+    for jb in range(8):
+        for grp in GROUPS:
+            units = {(4 * ((16 * jb + (l & 15)) % 4) + ((l >> 4) ^ tab[((16 * jb + (l & 15)) >> 2) & 3])) % 16 for l in grp}
+            if len(units) < 16:
+                return False
+    return True
+
+
+if __name__ == "__main__":
+    assert halo_ok(lambda y: 2 * (y & 1)), "hsw<true>"
+    assert weights_ok((0, 2, 0, 2)), "wswz<true>"
+    assert not halo_ok(lambda y: y & 3)      # the 32x32x16 swizzle conflicts under the 16x16x32 layout
+    print("halo swizzles (y mod 4 -> slot xor):", [t for t in itertools.product(range(4), repeat=4) if halo_ok(lambda y, t=t: t[y % 4])])
+    print("weight swizzles ((co >> 2) mod 4 -> slot xor):", [t for t in itertools.product(range(4), repeat=4) if weights_ok(t)])

@@ -1,4 +1,4 @@
-// Ablation timing of the persistent warp-specialised kernel (k_conv_stream<5,16,16,1,ABL>, conv_stream.hip) at
+// Ablation timing of the persistent warp-specialised kernel (k_conv_stream<5,16,16,1,M16,LAT,ABL>, conv_stream.hip) at
 // the v_conv2 bench shape (N=512, 64x64x128 -> 128, 5x5).  Timing only: outputs are meaningless for
 // ABL != 0.   hipcc --offload-arch=gfx950 -O3 -std=c++20 -o _stream_ablate stream_ablate.hip
 #include <cstdint>
@@ -15,19 +15,19 @@ void set_error(const std::string& msg) { std::fprintf(stderr, "error: %s\n", msg
 
 using namespace avse;
 
-template <int ABL, int LAT = 10>
+template <int ABL, int LAT = 10, bool M16 = true>
 float run(const HaloArgs& a, int reps) {
     using G = StreamGeom<5, 16, 16, 1, LAT>;
-    (void)hipFuncSetAttribute((const void*)k_conv_stream<5, 16, 16, 1, LAT, ABL>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)k_conv_stream<5, 16, 16, 1, M16, LAT, ABL>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               G::LDS);
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
     for (int r = 0; r < 10; ++r)   // warm-up long enough for the clock to settle under MFMA load
-        hipLaunchKernelGGL((k_conv_stream<5, 16, 16, 1, LAT, ABL>), dim3(256, 1), dim3(512), G::LDS, 0, a);
+        hipLaunchKernelGGL((k_conv_stream<5, 16, 16, 1, M16, LAT, ABL>), dim3(256, 1), dim3(512), G::LDS, 0, a);
     (void)hipEventRecord(e0, 0);
     for (int r = 0; r < reps; ++r)
-        hipLaunchKernelGGL((k_conv_stream<5, 16, 16, 1, LAT, ABL>), dim3(256, 1), dim3(512), G::LDS, 0, a);
+        hipLaunchKernelGGL((k_conv_stream<5, 16, 16, 1, M16, LAT, ABL>), dim3(256, 1), dim3(512), G::LDS, 0, a);
     (void)hipEventRecord(e1, 0);
     (void)hipEventSynchronize(e1);
     float ms = 0.f;
@@ -70,6 +70,8 @@ int main() {
     auto rep = [&](const char* name, float ms) {
         std::printf("%-34s %8.4f ms  %7.1f TF/s\n", name, ms, flop / (ms * 1e-3) / 1e12);
     };
+    rep("full, 32x32x16 compute waves", run<0, 10, false>(a, reps));
+    rep("MFMA only, 32x32x16 (15)", run<15, 10, false>(a, reps));
     rep("full", run<0, 10>(a, reps));
     rep("no halo pieces (1)", run<1, 10>(a, reps));
     rep("no weight streaming (2)", run<2, 10>(a, reps));
@@ -85,7 +87,7 @@ int main() {
     (void)hipMalloc(&prof, 256 * 8 * 4 * 8);
     (void)hipMemset(prof, 0, 256 * 8 * 4 * 8);
     a.prof = prof;
-    rep("instrumented (128)", run<128, 10>(a, reps));
+    rep("instrumented (128, 32x32x16)", run<128, 10, false>(a, reps));
     auto split = [&](const char* title) {
     std::vector<unsigned long long> hp(256 * 8 * 4);
     (void)hipMemcpy(hp.data(), prof, hp.size() * 8, hipMemcpyDeviceToHost);
