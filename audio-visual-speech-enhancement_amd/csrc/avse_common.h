@@ -141,6 +141,7 @@ struct HaloArgs {
     const float* vstd;
     void* out;               // bf16, pooled [N][Hc/2][Wc/2][Co] at (clip stride, pixel stride, channel offset)
     const void* w;           // bf16 [step][Co][32]
+    const void* w2;          // V1 only: [5][Co][32] kernel-row packing (conv_v1r.hip)
     const float* scale;
     const float* shift;
     int N, Hc, Wc, Ci, Co;
@@ -152,7 +153,8 @@ struct HaloArgs {
 
 int launch_conv_halo(const HaloArgs& a, hipStream_t s);
 int launch_conv_stream(const HaloArgs& a, hipStream_t s);   // conv_stream.hip (non-V1 variants)
-int launch_conv_v1(const HaloArgs& a, hipStream_t s);       // conv_v1.hip (v_conv1)
+int launch_conv_v1(const HaloArgs& a, hipStream_t s);       // conv_v1.hip (v_conv1, dense im2col)
+int launch_conv_v1r(const HaloArgs& a, hipStream_t s);      // conv_v1r.hip (v_conv1, kernel-row runs)
 int launch_video_prep(const float* video, const float* mean, const float* stdv, void* out, int64_t N,
                       int dtype, hipStream_t s);
 int launch_audio_prep(const float* audio, void* out, int64_t N, int dtype, hipStream_t s);

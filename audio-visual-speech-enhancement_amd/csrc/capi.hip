@@ -176,6 +176,7 @@ struct GpuLayer {
     int2* taps = nullptr;
     int halo = HALO_NONE;     // halo-tiled kernel variant (bf16 video convs)
     void* w_halo = nullptr;   // bf16 packing for conv_stream.hip / conv_v1.hip (see build_layer)
+    void* w_halo2 = nullptr;  // v_conv1 only: [5 kernel rows][Cout][32] packing for conv_v1r.hip
     float* scale_h = nullptr; // |scale| for w_halo: channels with a negative BN scale have negated weights
 };
 
@@ -551,6 +552,19 @@ int build_layer(avse_weights* W, const LayerDef& L, const float* kernel, const f
         uint16_t* d;
         if ((rc = upload(W, hp, &d))) return rc;
         G.w_halo = d;
+        if (G.halo == HALO_V1) {
+            // conv_v1r.hip: slice ky, k = kx * 6 + frame (frame 5 and k = 30, 31 zero)
+            std::vector<uint16_t> hr((size_t)L.kh * L.cout * 32, 0);
+            for (int ky = 0; ky < L.kh; ++ky)
+                for (int n = 0; n < L.cout; ++n)
+                    for (int kx = 0; kx < L.kw; ++kx)
+                        for (int f = 0; f < L.cin; ++f)
+                            hr[((size_t)ky * L.cout + n) * 32 + kx * 6 + f] =
+                                f2bf(sgn[n] * kernel[((size_t)(ky * L.kw + kx) * L.cin + f) * L.cout + n]);
+            uint16_t* d2;
+            if ((rc = upload(W, hr, &d2))) return rc;
+            G.w_halo2 = d2;
+        }
     }
     return 0;
 }
@@ -566,6 +580,7 @@ HaloArgs halo_args(const GpuLayer& G, const void* in, const float* video, const 
     a.vstd = vstd;
     a.out = out;
     a.w = G.w_halo;
+    a.w2 = G.w_halo2;
     a.scale = G.scale_h;
     a.shift = G.shift;
     a.N = (int)N;

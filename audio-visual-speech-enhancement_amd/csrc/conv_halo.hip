@@ -344,7 +344,14 @@ int launch_conv_halo(const HaloArgs& a, hipStream_t s) {
     const bool pipe = mode == 1;
     if (mode == 2 && a.variant != HALO_V1) return launch_conv_stream(a, s);
     switch (a.variant) {
-        case HALO_V1: return launch_conv_v1(a, s);
+        case HALO_V1: {
+            // AVSE_V1_IM2COL=1 (read per launch): the dense-im2col kernel (A/B switch)
+            const char* e = std::getenv("AVSE_V1_IM2COL");
+            if ((e && e[0] == '1') || !a.w2) return launch_conv_v1(a, s);
+            HaloArgs r = a;
+            r.w = a.w2;
+            return launch_conv_v1r(r, s);
+        }
         case HALO_K5:
             return pipe ? launch_halo_t<5, 16, 16, 1, false, true>(a, s) : launch_halo_t<5, 16, 16, 1, false, false>(a, s);
         case HALO_K3_16:

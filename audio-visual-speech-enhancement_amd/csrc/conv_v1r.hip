@@ -1,0 +1,349 @@
+// v_conv1 (network.py:139-143: Conv2D(128, 5x5, 'same') on the normalised 5-frame mouth crops ->
+// BatchNorm -> LeakyReLU(0.3) -> MaxPooling2D(2x2)) fused with VideoNormalizer.normalize
+// (data_processor.py:208-212) and the f32 -> bf16 cast, gfx950 — row-run formulation.
+//
+// The K axis is split by kernel row: K-slice ky holds k = kx * 6 + frame (kx < 5, frame < 6; frame 5 and
+// k = 30, 31 carry zero weights).  The normalised window is stored in LDS as 12-byte pixels (frames 0..4
+// as bf16 and a zero), so the 32 k of slice ky for output pixel (y, x) are the 64 contiguous bytes that
+// start at window pixel (y + ky, x): the MFMA A fragments are read straight from the window (two
+// ds_read2_b32 per fragment: the rows are only 4-byte aligned) and nothing is rearranged.  Against the
+// dense im2col kernel (conv_v1.hip: K = 128 in 4 slices, loader waves rebuilding a 64-byte im2col row per
+// lane per slice, one barrier per slice) this costs 5 slices of MFMAs instead of 4, but the loader work
+// drops to one window per tile and the compute waves meet the loaders at one barrier per tile.
+//   * 512 threads: 4 compute waves (v_mfma_f32_16x16x32_bf16, issue priority) + 4 loader waves;
+//   * weights: 5 slices x 128 co x 32 k bf16 (40 KB) resident in LDS for the whole launch;
+//   * window: 20 x 20 pixels x 12 B, two LDS slots; tile k+2's f32 window is in flight in the loader
+//     registers while tile k computes, tile k+1's is normalised and stored;
+//   * compute wave w owns conv-pixel rows 4w .. 4w+3 of the 16 x 16 tile as 4 blocks of 4x4 pixels x 128
+//     output channels; block row r = 4 q + 2 dy + dx is pixel (2 (q >> 1) + dy, 2 (q & 1) + dx), so a lane's
+//     4 accumulator rows are one 2x2 pool window and BN / pool / LeakyReLU happen in registers.
+// Persistent over tiles in XCD-aware order (as conv_stream.hip).
+#include "avse_common.h"
+
+namespace avse {
+namespace {
+
+constexpr float LRELU = 0.3f;
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef int i32x2 __attribute__((ext_vector_type(2)));
+constexpr int kOOB = 0x7fffff00;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, long long bytes) {
+    const int nrec = bytes > kOOB ? kOOB : (bytes < 0 ? 0 : (int)bytes);
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, nrec, 0x00020000);
+}
+__device__ __forceinline__ void barrier_raw() { asm volatile("s_barrier" ::: "memory"); }
+// weights image: row (slice, co) 64 B, 16-B k-group s at s ^ wsw(co) (conflict-free for the 16x16x32
+// B-operand lane groups, tools/lds_swizzle_search.py)
+__device__ __forceinline__ int wsw(int co) { return 2 * ((co >> 2) & 1); }
+
+constexpr int TH = 16, TW = 16, KS = 5, PAD = 2, NF = 5;
+constexpr int HH = TH + KS - 1, HW = TW + KS - 1, HPIX = HH * HW;   // 20 x 20 window
+constexpr int PB = 12;                                              // bytes per window pixel
+// LDS row pitch 24 pixels (20 used): 20 gave 2-way bank conflicts on the A-fragment ds_read2_b32, 24 none
+// (tools/lds_swizzle_search.py --v1r); columns 20..23 stay zero (the row run of x = 15 reads 4 B of x = 20)
+constexpr int HWP = 24;
+constexpr int HSLOT = HH * HWP * PB + 64;                           // + zero tail read by the last row runs
+constexpr int NSL = KS;                                             // K-slices per tile (one per kernel row)
+constexpr int WIMG = NSL * 128 * 64;                                // 40 KB resident weights
+constexpr int SSH = 2 * 128 * 4;                                    // BN scale / shift
+constexpr int NWS = 3;                                              // window slots
+// pooled f32 tile (8 x 8 px x 128 co), row pitch 576 B: the compute waves' ds_write_b32 (pixels P, P+1 in
+// one 32-lane group) land 16 banks apart, the loaders' lane-linear ds_read_b128 are conflict-free
+constexpr int SPITCH = 576;
+constexpr int STG = 64 * SPITCH;
+constexpr int LDS_BYTES = WIMG + NWS * HSLOT + SSH + 2 * STG;
+constexpr int PPL = (HPIX + 255) / 256;                             // window pixels per loader lane (2)
+static_assert(HSLOT % 16 == 0 && LDS_BYTES <= 160 * 1024, "LDS");
+
+// ABL: ablation mask for tools/v1r_ablate.hip only (0 in the library): 1 = loaders skip the output pass,
+// 2 = loaders skip the per-tile window work, 4 = no MFMAs, 8 = no barrier in the tile loop
+template <int ABL = 0>
+__global__ __launch_bounds__(512, 1) void k_conv_v1r(HaloArgs a) {
+    extern __shared__ __attribute__((aligned(1024))) char lds[];
+    char* const wimg = lds;
+    char* const halo = lds + WIMG;                  // [NWS][HSLOT]
+    float* const ssh = reinterpret_cast<float*>(halo + NWS * HSLOT);
+    char* const stg = halo + NWS * HSLOT + SSH;     // [2][STG] pooled raw maxima, compute -> loader
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int w = wave & 3;
+
+    const int tiles_x = a.Wc / TW, tiles_per_clip = tiles_x * (a.Hc / TH);
+    const int ntiles = a.N * tiles_per_clip;
+    const int gxs = (int)gridDim.x;
+    const int slot = (gxs % 8 == 0) ? ((int)blockIdx.x % 8) * (gxs / 8) + (int)blockIdx.x / 8 : (int)blockIdx.x;
+    const int nmine = (ntiles - slot + gxs - 1) / gxs;
+    if (nmine <= 0) return;
+    auto tile_origin = [&](int k, int& clip, int& oy0, int& ox0) {
+        const int t = slot + k * gxs;
+        clip = t / tiles_per_clip;
+        const int tt = t - clip * tiles_per_clip;
+        oy0 = (tt / tiles_x) * TH;
+        ox0 = (tt % tiles_x) * TW;
+    };
+
+    if (wave >= 4) {
+        // =============================== loader waves ===============================
+        const int L = w * 64 + lane;
+        {   // resident weights [slice][co][32] (host packing) and the BN tail
+            const __amdgpu_buffer_rsrc_t wrs = make_rsrc(a.w, (long long)WIMG);
+#pragma unroll
+            for (int i = 0; i < WIMG / 16 / 256; ++i) {
+                const int C = L + 256 * i, row = C >> 2, sl = C & 3;
+                const i32x4 v = __builtin_amdgcn_raw_buffer_load_b128(wrs, C * 16, 0, 0);
+                *reinterpret_cast<i32x4*>(wimg + row * 64 + ((sl ^ wsw(row & 127)) << 4)) = v;
+            }
+            if (L < 128) {
+                ssh[L] = a.scale[L];
+                ssh[128 + L] = a.shift[L];
+            }
+            // zero the pitch padding (columns 20..23) and the tails of both slots: never written afterwards
+            for (int i = L; i < NWS * HSLOT / 4; i += 256) {
+                const int off = (i * 4) % HSLOT;
+                if (off >= HH * HWP * PB || (off / PB) % HWP >= HW) reinterpret_cast<int*>(halo)[i] = 0;
+            }
+        }
+        const long long clip_bytes = (long long)a.Hc * a.Wc * NF * 4;
+        const bool norm = a.vmean != nullptr;
+        const __amdgpu_buffer_rsrc_t mrs = make_rsrc(norm ? a.vmean : a.video, (long long)a.Hc * a.Wc * 4);
+        const __amdgpu_buffer_rsrc_t srs = make_rsrc(norm ? a.vstd : a.video, (long long)a.Hc * a.Wc * 4);
+        // two register sets: window k+2 is loaded two tiles ahead, so the vmcnt wait for it never waits on
+        // output stores younger than two tiles (vmcnt retires in issue order, stores included)
+        f32x4 v4[2][PPL];
+        float v1[2][PPL], pm[2][PPL], ps[2][PPL];
+        int pok[2][PPL];
+        auto win_load = [&](auto set, int k) {
+            constexpr int Q = decltype(set)::value;
+            int clip, oy0, ox0;
+            tile_origin(k, clip, oy0, ox0);
+            const __amdgpu_buffer_rsrc_t vrs =
+                make_rsrc(reinterpret_cast<const char*>(a.video) + (long long)clip * clip_bytes, clip_bytes);
+#pragma unroll
+            for (int e = 0; e < PPL; ++e) {
+                const int P = L + 256 * e;
+                const int wy = P / HW, wx = P - wy * HW;
+                const int iy = oy0 + wy - PAD, ix = ox0 + wx - PAD;
+                const int ok = (int)(P < HPIX) & (int)((unsigned)iy < (unsigned)a.Hc) & (int)((unsigned)ix < (unsigned)a.Wc);
+                const int pix = iy * a.Wc + ix;
+                const int voff = ok ? pix * NF * 4 : kOOB, moff = ok ? pix * 4 : kOOB;
+                v4[Q][e] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(vrs, voff, 0, 0));
+                v1[Q][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(vrs, voff, 16, 0));
+                pm[Q][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(mrs, moff, 0, 0));
+                ps[Q][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(srs, moff, 0, 0));
+                pok[Q][e] = ok;
+            }
+        };
+        // VideoNormalizer ((v - mean) / std, one reciprocal per pixel), then 'same' zero padding, bf16
+        auto win_store = [&](auto set, int hs) {
+            constexpr int Q = decltype(set)::value;
+#pragma unroll
+            for (int e = 0; e < PPL; ++e) {
+                const int P = L + 256 * e;
+                if (P >= HPIX) continue;
+                const float rs = 1.f / ps[Q][e];
+                float f[NF] = {v4[Q][e][0], v4[Q][e][1], v4[Q][e][2], v4[Q][e][3], v1[Q][e]};
+                unsigned short h[6];
+#pragma unroll
+                for (int i = 0; i < NF; ++i) {
+                    const float n = norm ? (f[i] - pm[Q][e]) * rs : f[i];
+                    h[i] = __builtin_bit_cast(unsigned short, (bf16_t)(pok[Q][e] ? n : 0.f));
+                }
+                h[5] = 0;
+                const int wy = P / HW, wx = P - wy * HW;
+                unsigned* d = reinterpret_cast<unsigned*>(halo + hs * HSLOT + (wy * HWP + wx) * PB);
+                d[0] = h[0] | ((unsigned)h[1] << 16);
+                d[1] = h[2] | ((unsigned)h[3] << 16);
+                d[2] = h[4];
+            }
+        };
+        // output pass of tile k: BN (|scale|, shift) + LeakyReLU(0.3) on the pooled raw maxima the compute
+        // waves left in staging slot k & 1, bf16, 8-B stores.  Float4 F = L + 256 r: pooled pixel F / 32,
+        // channels 4 (F % 32) .. +3 (lane-constant), so a 32-lane half stores one pixel's 256 contiguous bytes
+        const int c4 = (L & 31) * 4;
+        float osc[4], osh[4];
+        const int Wp = a.Wc / 2;
+        auto out_pass = [&](int k) {
+            int clip, oy0, ox0;
+            tile_origin(k, clip, oy0, ox0);
+            const long long cb = a.out_clip_stride * 2;
+            const __amdgpu_buffer_rsrc_t ors = make_rsrc(reinterpret_cast<const char*>(a.out) + (long long)clip * cb, cb);
+            const char* sbase = stg + (k & 1) * STG + (L >> 5) * SPITCH + c4 * 4;
+            const int obase = ((oy0 >> 1) * Wp + (ox0 >> 1) + (L >> 5)) * a.out_pix_stride + a.out_c_off + c4;
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {   // pooled pixel (r, L >> 5) of the 8 x 8 tile
+                const f32x4 m = *reinterpret_cast<const f32x4*>(sbase + 8 * r * SPITCH);
+                float v[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float x = fmaf(m[e], osc[e], osh[e]);
+                    asm("v_max_f32 %0, %1, %2" : "=v"(v[e]) : "v"(x), "v"(LRELU * x));   // LeakyReLU, no canonicalise
+                }
+                const bf16x2 lo = __builtin_convertvector((f32x2){v[0], v[1]}, bf16x2);
+                const bf16x2 hi = __builtin_convertvector((f32x2){v[2], v[3]}, bf16x2);
+                const i32x2 o = {__builtin_bit_cast(int, lo), __builtin_bit_cast(int, hi)};
+                __builtin_amdgcn_raw_buffer_store_b64(o, ors, (obase + r * Wp * a.out_pix_stride) * 2, 0, 0);
+            }
+        };
+        using Q0 = std::integral_constant<int, 0>;
+        using Q1 = std::integral_constant<int, 1>;
+        win_load(Q0{}, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        win_store(Q0{}, 0);
+        if (nmine > 1) {
+            win_load(Q1{}, 1);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            win_store(Q1{}, 1);
+        }
+        if (nmine > 2) win_load(Q0{}, 2);
+        if (nmine > 3) win_load(Q1{}, 3);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        barrier_raw();   // B_-1: weights, BN tail, windows 0 and 1
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            osc[e] = ssh[c4 + e];
+            osh[e] = ssh[128 + c4 + e];
+        }
+        // iteration k (set k & 1 holds window k+2): output pass of tile k-1, window k+2 -> LDS slot (k+2) % 3,
+        // window k+4's loads into the freed set, barrier B_k
+        auto iter = [&](auto set, int k) {
+            const bool out = k >= 1 && !(ABL & 1);
+            if (out) out_pass(k - 1);
+            if (k + 2 < nmine && !(ABL & 2)) {
+                // younger than window k+2's loads: tile k-1's stores (k >= 2), window k+3's loads (issued
+                // one iteration later, k+3 < nmine) and this iteration's stores
+                const int n = ((k >= 2 && !(ABL & 1)) ? 8 : 0) + (k + 3 < nmine ? 8 : 0) + (out ? 8 : 0);
+                if (n >= 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+                else if (n >= 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+                else if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                win_store(set, (k + 2) % NWS);     // slot of window k-1, last read during tile k-1
+                if (k + 4 < nmine) win_load(set, k + 4);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if constexpr (!(ABL & 8)) barrier_raw();   // B_k: staging k written, window k+2 stored
+        };
+        for (int k = 0; k < nmine; k += 2) {
+            iter(Q0{}, k);
+            if (k + 1 < nmine) iter(Q1{}, k + 1);
+        }
+        if (!(ABL & 1)) out_pass(nmine - 1);
+        return;
+    }
+
+    // =============================== compute waves ===============================
+    __builtin_amdgcn_s_setprio(2);
+    const int r16 = lane & 15, kg = lane >> 4;
+    const int q = r16 >> 2, dy = (r16 >> 1) & 1, dx = r16 & 1;
+    // window byte offset of this lane's 16 bytes of slice 0 in block 0: pixel (4w + 2(q>>1) + dy, 2(q&1) + dx)
+    const int abase = ((4 * w + 2 * (q >> 1) + dy) * HWP + 2 * (q & 1) + dx) * PB + 16 * kg;
+    const int bbase = r16 * 64 + ((kg ^ wsw(r16)) << 4);   // + slice * 8192 + 1024 j
+    auto frags = [&](int hs, int ky, i32x4 (&fa)[4], i32x4 (&fb)[8]) {
+        const char* hp = halo + hs * HSLOT + abase + ky * HWP * PB;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const unsigned* p = reinterpret_cast<const unsigned*>(hp + 4 * i * PB);   // block i: 4 pixels right
+            fa[i] = (i32x4){(int)p[0], (int)p[1], (int)p[2], (int)p[3]};
+        }
+        const char* wp = wimg + ky * 8192 + bbase;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) fb[j] = *reinterpret_cast<const i32x4*>(wp + 1024 * j);
+    };
+    barrier_raw();   // B_-1
+
+    f32x4 acc[4][8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = (f32x4){};
+    // pool: the 4 accumulator rows of a lane are one 2x2 window (raw maxima: scale >= 0 after the host sign
+    // fold, so BN commutes); inline asm keeps the compiler from canonicalising the operands (2 instead of 4
+    // instructions per window).  The loader waves apply BN / LeakyReLU and store (out_pass).
+    auto max4 = [](f32x4 v) {
+        float r;
+        asm volatile("v_max3_f32 %0, %1, %2, %3\n\tv_max_f32 %0, %0, %4" : "=&v"(r) : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]));
+        return r;
+    };
+    // staging: pooled pixel P = (2w + (kg >> 1)) * 8 + 2i + (kg & 1), channel 16 j + r16 at P * SPITCH + 4 co
+    char* const sl0 = stg + ((2 * w + (kg >> 1)) * 8 + (kg & 1)) * SPITCH + r16 * 4;
+    auto epilogue = [&](int k) {
+        char* const sb = sl0 + (k & 1) * STG;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) *reinterpret_cast<float*>(sb + 2 * i * SPITCH + 64 * j) = max4(acc[i][j]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[i][j] *= 0.f;   // restart the chains in place (see conv_stream.hip)
+    };
+    auto mfmas = [&](const i32x4 (&ca)[4], const i32x4 (&cb)[8]) {
+        if constexpr ((ABL & 4) != 0) return;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ca[i]),
+                                                                     __builtin_bit_cast(bf16x8, cb[j]), acc[i][j], 0, 0, 0);
+    };
+    // slice s: MFMAs on (ca, cb) interleaved with the fragment reads of slice s+1 into (xa, xb)
+    auto slice = [&](int hs, int ky_next, i32x4 (&ca)[4], i32x4 (&cb)[8], i32x4 (&xa)[4], i32x4 (&xb)[8]) {
+        frags(hs, ky_next, xa, xb);
+        mfmas(ca, cb);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    i32x4 fa[4], fb[8], na[4], nb[8];
+    // one tile: slice 0 in (xa, xb); tile k+1's slice 0 lands in (ya, yb) (parity flips per tile)
+    auto tile = [&](int k, i32x4 (&xa)[4], i32x4 (&xb)[8], i32x4 (&ya)[4], i32x4 (&yb)[8]) {
+        const int hs = k % NWS, hn = (k + 1) % NWS;
+        slice(hs, 1, xa, xb, ya, yb);
+        slice(hs, 2, ya, yb, xa, xb);
+        slice(hs, 3, xa, xb, ya, yb);
+        slice(hs, 4, ya, yb, xa, xb);
+        // slice 4, with tile k+1's first fragments (window k+1 was stored before B_{k-1}; past the last tile
+        // the read hits a stale slot and is never used)
+        slice(hn, 0, xa, xb, ya, yb);
+        epilogue(k);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if constexpr (!(ABL & 8)) barrier_raw();   // B_k: staging k is written; window k is no longer read
+    };
+    frags(0, 0, fa, fb);
+    for (int k = 0; k < nmine; k += 2) {
+        tile(k, fa, fb, na, nb);
+        if (k + 1 < nmine) tile(k + 1, na, nb, fa, fb);
+    }
+}
+
+}  // namespace
+
+int launch_conv_v1r(const HaloArgs& a, hipStream_t s) {
+    static bool attr = false;
+    if (!attr) {
+        AVSE_HIP_CHECK(hipFuncSetAttribute((const void*)k_conv_v1r<0>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
+        attr = true;
+    }
+    if (a.Hc % TH || a.Wc % TW || a.Co != 128 || a.Ci != NF || !a.w) {
+        set_error("v_conv1 row-run kernel: unexpected layer shape or missing packing");
+        return 3;
+    }
+    int dev = 0, ncu = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    const int tiles = a.N * (a.Hc / TH) * (a.Wc / TW);
+    int gx = ncu >= 8 ? ncu / 8 * 8 : ncu;
+    if (gx > tiles) gx = tiles;
+    hipLaunchKernelGGL(k_conv_v1r<0>, dim3(gx), dim3(512), LDS_BYTES, s, a);
+    AVSE_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+}  // namespace avse

@@ -195,3 +195,28 @@ def test_network_api_shapes(gpu):
     assert net.predict(mel[:1], video[:1]).shape == (80, 20)      # np.squeeze quirk (network.py:212)
     loss = net.evaluate(mel, video, mel)
     assert isinstance(loss, float) and np.isfinite(loss)
+
+
+@pytest.mark.parametrize("env", ["AVSE_V1_IM2COL", "AVSE_MFMA32"])
+def test_bf16_video_kernel_variants_agree(gpu, env, monkeypatch):
+    """A/B kernel variants of the bf16 video encoder (conv_v1r.hip kernel-row runs vs conv_v1.hip dense
+    im2col; 16x16x32 vs 32x32x16 stream-conv compute waves) give the same layer outputs and match the oracle."""
+    from avse_amd import ops
+    from avse_amd.model import KerasModel
+    N = 3
+    model = KerasModel.init(seed=5, randomize=True)
+    mel, video = make_inputs(N, 21)
+    mean, std = R.video_normalizer_fit(video)
+    args = [ops.to_device(mel), ops.to_device(video), ops.to_device(mean), ops.to_device(std)]
+    inter = {}
+    K.forward(model.layer_dict(), mel, R.video_normalize(video, mean, std).astype(np.float32), intermediates=inter)
+    dw = ops.DeviceWeights(model, "bfloat16")
+    out_a = ops.forward(dw, *args).cpu().numpy()
+    sc_a = scratch(dw, N)
+    monkeypatch.setenv(env, "1")
+    out_b = ops.forward(dw, *args).cpu().numpy()
+    sc_b = scratch(dw, N)
+    for k in ["v_conv1", "v_conv2", "v_conv3", "v_conv4", "v_conv5"]:
+        assert rel_rms(sc_a[k], inter[k]) <= 1.5e-2, (k, rel_rms(sc_a[k], inter[k]))
+        assert rel_rms(sc_a[k], sc_b[k]) <= 1e-2, (k, rel_rms(sc_a[k], sc_b[k]))
+    assert rel_rms(out_a, out_b) <= 1e-2

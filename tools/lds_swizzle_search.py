@@ -50,7 +50,33 @@ def weights_ok(tab):
     return True
 
 
+def v1r_read2_cycles(pitch, pb=12):
+    """conv_v1r.hip A fragments: lane (r16, kg) reads 16 B at window pixel (y, x) of its 4x4 block, byte
+    16 kg, as 4 dwords (two ds_read2_b32); ds_read_b32 banks are (a / 4) mod 32 over 2 groups of 32 lanes.
+    Returns LDS cycles per fragment (8 = conflict-free) over all rows of the tile and kernel rows."""
+    worst = 0
+    for w in range(4):
+        for ky in range(5):
+            for i in range(4):
+                tot = 0
+                for half in range(2):
+                    for d in range(4):
+                        banks = {}
+                        for lane in range(32 * half, 32 * half + 32):
+                            py, px, k = lane_pixel(lane)
+                            a = ((4 * w + py + ky) * pitch + 4 * i + px) * pb + 16 * k + 4 * d
+                            banks.setdefault((a // 4) % 32, set()).add(a)
+                        tot += max(len(v) for v in banks.values())
+                worst = max(worst, tot)
+    return worst
+
+
 if __name__ == "__main__":
+    import sys
+    if "--v1r" in sys.argv:
+        for pitch in range(20, 29):
+            print(f"conv_v1r window pitch {pitch}: {v1r_read2_cycles(pitch)} LDS cycles per A fragment (8 = conflict-free)")
+        sys.exit(0)
     assert halo_ok(lambda y: 2 * (y & 1)), "hsw<true>"
     assert weights_ok((0, 2, 0, 2)), "wswz<true>"
     assert not halo_ok(lambda y: y & 3)      # the 32x32x16 swizzle conflicts under the 16x16x32 layout
