@@ -242,7 +242,7 @@ bool unfused_tail() {
 }
 
 int run_conv(const ConvArgs& a, int dtype, hipStream_t s) {
-    if (dtype == AVSE_BF16 && !no_igemm() && a.Ci % 32 == 0) return launch_igemm(a, s);
+    if (dtype == AVSE_BF16 && !no_igemm() && a.Ci % 32 == 0 && !a.fuse_w) return launch_igemm(a, s);
     return launch_conv(a, dtype, s);
 }
 
@@ -916,7 +916,7 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
             a.fuse_w = W->d6_w;
             a.fuse_bias = W->d6_bias;
             a.fuse_out = out;
-            if ((rc = launch_conv(a, dt, s)) || (rc = mark())) return rc;
+            if ((rc = run_conv(a, dt, s)) || (rc = mark())) return rc;
             continue;
         }
         ConvArgs a = conv_args(G, buf(d_in[i]), in_cs, buf(d_in[i + 1]), (long long)G.ho * G.wo * G.def.cout, G.def.cout, 0, N);

@@ -162,6 +162,18 @@ __global__ __launch_bounds__(256, (conv_occupancy<BN, FAST>())) void k_conv(Conv
         }
     }
 
+    // epilogue parameters of this lane's columns, loaded before the K loop so that their latency is hidden
+    // (loaded at the end they exposed one global-load latency per tile: ~20 us on d_deconv5's 3200 tiles)
+    float esc[NJ], esh[NJ], ewf[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        const int n = n0 + wn * WN + 16 * j + (lane & 15);
+        const bool ok = n < a.Co && a.ksplit == 1;
+        esc[j] = ok ? a.scale[n] : 0.f;
+        esh[j] = ok ? a.shift[n] : 0.f;
+        ewf[j] = (ok && a.fuse_w) ? a.fuse_w[n] : 0.f;
+    }
+
     // P register stages: slabs s+1 .. s+P-1 are in flight while slab s computes (a layer with a short K loop
     // was a serial chain of one global-load latency per slab: ~0.7-1.2 us each, measured at batch 8)
     constexpr int P = 3;
@@ -333,24 +345,28 @@ __global__ __launch_bounds__(256, (conv_occupancy<BN, FAST>())) void k_conv(Conv
                 for (int r = 0; r < 4; ++r) part[i][r] = 0.f;
 #pragma unroll
             for (int j = 0; j < NJ; ++j) {
-                const int n = wn * WN + 16 * j + fr;
-                const float sc = a.scale[n], sh = a.shift[n], wf = a.fuse_w[n];
 #pragma unroll
                 for (int i = 0; i < NI; ++i)
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        float x = acc[i][j][r] * sc + sh;
+                        float x = acc[i][j][r] * esc[j] + esh[j];
                         if (a.act) x = x >= 0.f ? x : LRELU * x;
-                        part[i][r] = fmaf(to_f(from_f<T>(x)), wf, part[i][r]);
+                        part[i][r] = fmaf(to_f(from_f<T>(x)), ewf[j], part[i][r]);
                     }
             }
-            // sum over the 16 lanes holding the same rows (lane bits 0..3 = column within a fragment)
+            // sum over the 16 lanes holding the same rows (lane bits 0..3 = column within a fragment): DPP
+            // row_ror 8, 4, 2, 1 inside the 16-lane row (each add one VALU op; __shfl_xor went through LDS)
 #pragma unroll
             for (int i = 0; i < NI; ++i)
 #pragma unroll
-                for (int r = 0; r < 4; ++r)
-#pragma unroll
-                    for (int o = 1; o < 16; o <<= 1) part[i][r] += __shfl_xor(part[i][r], o);
+                for (int r = 0; r < 4; ++r) {
+                    float v = part[i][r];
+                    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x128, 0xf, 0xf, false));
+                    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x124, 0xf, 0xf, false));
+                    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x122, 0xf, 0xf, false));
+                    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x121, 0xf, 0xf, false));
+                    part[i][r] = v;
+                }
             // then over the two column halves (wn = 0, 1) through LDS (the K loop ended on a barrier)
             float* red = reinterpret_cast<float*>(lds);
             if (wn == 1 && fr == 0)
@@ -373,7 +389,7 @@ __global__ __launch_bounds__(256, (conv_occupancy<BN, FAST>())) void k_conv(Conv
     for (int j = 0; j < NJ; ++j) {
         const int n = n0 + wn * WN + 16 * j + fr;
         if (n >= a.Co) continue;
-        const float sc = a.scale[n], sh = a.shift[n];
+        const float sc = esc[j], sh = esh[j];
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
             float v[4];
