@@ -119,6 +119,30 @@ struct ConvArgs {
 
 int launch_conv(const ConvArgs& a, int dtype, hipStream_t s);
 int launch_splitk_reduce(const ConvArgs& a, int dtype, hipStream_t s);   // conv.hip: split-K tail
+
+// fused decoder tail d_deconv4 -> d_deconv5 -> d_deconv6, one workgroup per clip (conv_dec.hip, bf16)
+struct DecTailArgs {
+    const bf16_t* in;        // d_deconv3 output [N][40][10][128]
+    float* out;              // [N][80][20]
+    int N;
+    const bf16_t* w4;        // d_deconv4 packed [64][kpad4], k = tap * 128 + c
+    const float* sc4;        // folded bias + BN
+    const float* sh4;
+    int nt4, kpad4;
+    int pt4, pl4, rows4, pitch4;   // zero-padded input window: top / left pad, rows, pitch (pixels)
+    int dy4, dx4, nx4;       // taps: t -> (dy4 - t / nx4, dx4 - t % nx4) (checked on the host)
+    const bf16_t* w5;        // d_deconv5 packed, phase p at element w5 + woff5[p]: [64][kpad5[p]], k = tap * 64 + c
+    const float* sc5;
+    const float* sh5;
+    int nt5[4], kpad5[4];
+    int dy5[4], dx5[4], nx5[4];    // phase p's taps: t -> (dy5 - t / nx5, dx5 - t % nx5)
+    long long woff5[4];
+    int pt5, pl5, rows5, pitch5;   // zero-padded d_deconv4 output image
+    const float* w6;         // d_deconv6 1x1 weights [64] + bias
+    float b6;
+};
+bool dec_tail_supported(const DecTailArgs& a);
+int launch_dec_tail(const DecTailArgs& a, hipStream_t s);
 int launch_igemm(const ConvArgs& a, hipStream_t s);                      // igemm.hip (bf16)
 int choose_ksplit_ws(long long M, int Co, int kpad);                     // igemm.hip split-K choice
 

@@ -178,6 +178,7 @@ struct GpuLayer {
     void* w_halo = nullptr;   // bf16 packing for conv_stream.hip / conv_v1.hip (see build_layer)
     void* w_halo2 = nullptr;  // v_conv1 only: [5 kernel rows][Cout][32] packing for conv_v1r.hip
     float* scale_h = nullptr; // |scale| for w_halo: channels with a negative BN scale have negated weights
+    int2 htaps[MAX_TAPS * MAX_PHASES] = {};   // host copy of taps (conv_dec.hip's kernel arguments)
 };
 
 struct avse_weights {
@@ -511,6 +512,7 @@ int build_layer(avse_weights* W, const LayerDef& L, const float* kernel, const f
     if ((rc = upload(W, scale, &G.scale))) return rc;
     if ((rc = upload(W, shift, &G.shift))) return rc;
     if ((rc = upload(W, taps, &G.taps))) return rc;
+    for (size_t t = 0; t < taps.size() && t < (size_t)(MAX_TAPS * MAX_PHASES); ++t) G.htaps[t] = taps[t];
 
     // packing for the bf16 video conv kernels: conv_stream.hip [slice][Cout][32], slice = (cg*4 + cc)*KS^2
     // + tap; conv_v1.hip (v_conv1) [Cout][128] in im2col order
@@ -591,6 +593,69 @@ HaloArgs halo_args(const GpuLayer& G, const void* in, const float* video, const 
     a.out_clip_stride = out_clip_stride;
     a.out_pix_stride = out_pix_stride;
     a.out_c_off = out_c_off;
+    return a;
+}
+
+// fused d_deconv4 -> d_deconv5 -> d_deconv6 (conv_dec.hip): window geometry from the layers' tap extents
+DecTailArgs dec_tail_args(const GpuLayer& G4, const GpuLayer& G5, const avse_weights* W, const void* in, float* out,
+                          int64_t N) {
+    DecTailArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.in = reinterpret_cast<const bf16_t*>(in);
+    a.out = out;
+    a.N = (int)N;
+    auto extents = [](const GpuLayer& G, int p, int& dy0, int& dy1, int& dx0, int& dx1) {
+        dy0 = dx0 = 1 << 20;
+        dy1 = dx1 = -(1 << 20);
+        for (int t = 0; t < G.ph[p].ntaps; ++t) {
+            const int2 d = G.htaps[G.ph[p].tap_off + t];
+            dy0 = std::min(dy0, d.x); dy1 = std::max(dy1, d.x);
+            dx0 = std::min(dx0, d.y); dx1 = std::max(dx1, d.y);
+        }
+    };
+    a.w4 = reinterpret_cast<const bf16_t*>(G4.w);
+    a.sc4 = G4.scale;
+    a.sh4 = G4.shift;
+    a.nt4 = G4.ph[0].ntaps;
+    a.kpad4 = G4.ph[0].kpad;
+    int dy0, dy1, dx0, dx1;
+    extents(G4, 0, dy0, dy1, dx0, dx1);
+    a.pt4 = -dy0; a.pl4 = -dx0; a.rows4 = G4.hq + dy1 - dy0; a.pitch4 = G4.wq + dx1 - dx0;
+    // the kernel walks a phase's taps as a (dy0 - a, dx0 - b) grid with nx columns: check that layout
+    bool grid_ok = true;
+    auto tap_grid = [&](const GpuLayer& G, int p, int& dy, int& dx, int& nx) {
+        const int2* t = G.htaps + G.ph[p].tap_off;
+        const int nt = G.ph[p].ntaps;
+        dy = t[0].x;
+        dx = t[0].y;
+        nx = 1;
+        while (nx < nt && t[nx].x == dy) ++nx;
+        for (int k = 0; k < nt; ++k)
+            if (t[k].x != dy - k / nx || t[k].y != dx - k % nx) grid_ok = false;
+    };
+    tap_grid(G4, 0, a.dy4, a.dx4, a.nx4);
+    a.w5 = reinterpret_cast<const bf16_t*>(G5.w);
+    a.sc5 = G5.scale;
+    a.sh5 = G5.shift;
+    int ey0 = 1 << 20, ey1 = -(1 << 20), ex0 = 1 << 20, ex1 = -(1 << 20);
+    for (int p = 0; p < 4 && p < G5.nphase; ++p) {
+        a.nt5[p] = G5.ph[p].ntaps;
+        a.kpad5[p] = G5.ph[p].kpad;
+        a.woff5[p] = G5.ph[p].w_off;
+        tap_grid(G5, p, a.dy5[p], a.dx5[p], a.nx5[p]);
+        extents(G5, p, dy0, dy1, dx0, dx1);
+        ey0 = std::min(ey0, dy0); ey1 = std::max(ey1, dy1);
+        ex0 = std::min(ex0, dx0); ex1 = std::max(ex1, dx1);
+    }
+    a.pt5 = -ey0; a.pl5 = -ex0; a.rows5 = G5.hq + ey1 - ey0; a.pitch5 = G5.wq + ex1 - ex0;
+    a.w6 = W->d6_w;
+    a.b6 = W->d6_bias;
+    // shapes the kernel is written for (network.py:125-133 at the 200-ms segment); anything else: k_conv
+    const bool shape_ok = G4.def.kind == DECONV && G5.def.kind == DECONV && G4.hq == 40 && G4.wq == 10 &&
+                          G4.def.cin == 128 && G4.def.cout == 64 && G4.nphase == 1 && G5.hq == 40 && G5.wq == 10 &&
+                          G5.def.cin == 64 && G5.def.cout == 64 && G5.nphase == 4 && G5.def.sh == 2 && G5.def.sw == 2 &&
+                          grid_ok;
+    if (!shape_ok) a.N = 0;   // dec_tail_supported() refuses
     return a;
 }
 
@@ -909,6 +974,14 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
     for (int i = 0; i < 5; ++i) {
         const GpuLayer& G = L(14 + i);
         const long long in_cs = (long long)G.def.hin * G.def.win * G.def.cin;
+        if (i == 3 && dt == AVSE_BF16 && !unfused_tail()) {
+            // d_deconv4 + d_deconv5 + d_deconv6 in one kernel, one workgroup per clip (conv_dec.hip)
+            const DecTailArgs da = dec_tail_args(L(17), L(18), W, buf(d_in[3]), out, N);
+            if (dec_tail_supported(da)) {
+                if ((rc = launch_dec_tail(da, s)) || (rc = mark()) || (rc = mark())) return rc;   // d4, d5 stages
+                break;
+            }
+        }
         if (i == 4 && !unfused_tail()) {
             // d_deconv5 with d_deconv6 (1x1, 64 -> 1, network.py:133) fused into its epilogue: the 64-channel
             // [N, 80, 20] activation is never written; orow addresses the float output pixel directly
