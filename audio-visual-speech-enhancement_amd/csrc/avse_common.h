@@ -142,6 +142,23 @@ struct DecTailArgs {
     float b6;
 };
 bool dec_tail_supported(const DecTailArgs& a);
+
+// fused audio encoder a_conv1 -> a_conv5, one workgroup per clip (conv_aud.hip, bf16)
+struct AudEncArgs {
+    const float* mel;        // [N][80][20] network input
+    bf16_t* out;             // concat buffer: a_conv5's HWC flatten at [clip * out_clip_stride, + 3200)
+    long long out_clip_stride;
+    int N;
+    const bf16_t* w1;        // a_conv1 dense [64][32], k = ky * 5 + kx (25 real)
+    const bf16_t* w2;        // a_conv2 packed [64][1024], k = tap * 64 + c
+    const bf16_t* w3;        // a_conv3 packed [128][1024]
+    const bf16_t* w4;        // a_conv4 packed [128][512], k = tap * 128 + c
+    const bf16_t* w5;        // a_conv5 packed [128][512]
+    const float* sc[5];      // folded bias + BN per layer
+    const float* sh[5];
+};
+bool aud_enc_supported(const AudEncArgs& a);
+int launch_aud_enc(const AudEncArgs& a, hipStream_t s);
 int launch_dec_tail(const DecTailArgs& a, hipStream_t s);
 int launch_igemm(const ConvArgs& a, hipStream_t s);                      // igemm.hip (bf16)
 int choose_ksplit_ws(long long M, int Co, int kpad);                     // igemm.hip split-K choice

@@ -177,6 +177,7 @@ struct GpuLayer {
     int halo = HALO_NONE;     // halo-tiled kernel variant (bf16 video convs)
     void* w_halo = nullptr;   // bf16 packing for conv_stream.hip / conv_v1.hip (see build_layer)
     void* w_halo2 = nullptr;  // v_conv1 only: [5 kernel rows][Cout][32] packing for conv_v1r.hip
+    void* w_dense = nullptr;  // a_conv1 only (bf16): [Cout][32], k = ky * kw + kx, for conv_aud.hip
     float* scale_h = nullptr; // |scale| for w_halo: channels with a negative BN scale have negated weights
     int2 htaps[MAX_TAPS * MAX_PHASES] = {};   // host copy of taps (conv_dec.hip's kernel arguments)
 };
@@ -508,6 +509,15 @@ int build_layer(avse_weights* W, const LayerDef& L, const float* kernel, const f
         float* d;
         if ((rc = upload(W, packed, &d))) return rc;
         G.w = d;
+    }
+    if (W->dtype == AVSE_BF16 && L.kind == CONV && L.cin == 1 && L.kh * L.kw <= 32) {
+        // conv_aud.hip's a_conv1: the single input channel's taps as a dense 32-deep K (25 real)
+        std::vector<uint16_t> dw((size_t)L.cout * 32, 0);
+        for (int n = 0; n < L.cout; ++n)
+            for (int t = 0; t < L.kh * L.kw; ++t) dw[(size_t)n * 32 + t] = f2bf(kernel[(size_t)t * L.cout + n]);
+        uint16_t* d;
+        if ((rc = upload(W, dw, &d))) return rc;
+        G.w_dense = d;
     }
     if ((rc = upload(W, scale, &G.scale))) return rc;
     if ((rc = upload(W, shift, &G.shift))) return rc;
@@ -928,10 +938,39 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
         AVSE_HIP_CHECK(hipStreamWaitEvent(c->side, c->fork, 0));
         sa = c->side;
     }
-    if ((rc = launch_audio_prep(audio, buf(B_AIN), N, dt, sa)) || (rc = mark())) return rc;
-    // audio encoder (network.py:88-109)
+    // audio encoder (network.py:88-109): one fused kernel per clip (conv_aud.hip) when the layers have the network's
+    // shapes (AVSE_NO_AUDENC=1: per-layer launches); profiled, its time shows as the audio_prep stage
+    bool aud_fused = false;
+    if (dt == AVSE_BF16) {
+        AudEncArgs aa;
+        std::memset(&aa, 0, sizeof(aa));
+        aa.mel = audio;
+        aa.out = reinterpret_cast<bf16_t*>(buf(B_CAT));
+        aa.out_clip_stride = 5248;
+        aa.N = (int)N;
+        const void* ws[5] = {L(0).w_dense, L(1).w, L(2).w, L(3).w, L(4).w};
+        const LayerDef* d = &L(0).def;
+        const bool shapes = d[0].cin == 1 && L(0).hq == 40 && L(0).wq == 10 && L(1).def.cin == 64 && L(1).def.cout == 64 &&
+                            L(1).def.kh == 4 && L(2).def.cout == 128 && L(2).hq == 20 && L(2).wq == 5 && L(3).hq == 10 &&
+                            L(3).wq == 5 && L(4).hq == 5 && L(4).wq == 5 && L(3).ph[0].kpad == 512 && L(4).ph[0].kpad == 512 &&
+                            L(1).ph[0].kpad == 1024 && L(2).ph[0].kpad == 1024;
+        aa.w1 = (const bf16_t*)ws[0]; aa.w2 = (const bf16_t*)ws[1]; aa.w3 = (const bf16_t*)ws[2];
+        aa.w4 = (const bf16_t*)ws[3]; aa.w5 = (const bf16_t*)ws[4];
+        for (int i = 0; i < 5; ++i) { aa.sc[i] = L(i).scale; aa.sh[i] = L(i).shift; }
+        if (shapes && aud_enc_supported(aa)) {
+            // on the caller's stream: beside the persistent video convolutions its 148-KB workgroups hold whole CUs
+            // they wait for (measured: concurrent 2.377 ms vs serial 2.304 ms per step); AVSE_AUD_SIDE=1 keeps the
+            // side stream
+            const char* e = std::getenv("AVSE_AUD_SIDE");
+            if ((rc = launch_aud_enc(aa, (e && e[0] == '1') ? sa : s))) return rc;
+            for (int k = 0; k < 6; ++k)
+                if ((rc = mark())) return rc;   // audio_prep (= the fused kernel), a_conv1..a_conv5
+            aud_fused = true;
+        }
+    }
+    if (!aud_fused && ((rc = launch_audio_prep(audio, buf(B_AIN), N, dt, sa)) || (rc = mark()))) return rc;
     const int a_in[5] = {B_AIN, B_A1, B_A2, B_A3, B_A4};
-    for (int i = 0; i < 5; ++i) {
+    for (int i = 0; i < 5 && !aud_fused; ++i) {
         const GpuLayer& G = L(i);
         const long long in_cs = (long long)G.def.hin * G.def.win * (i == 0 ? G.cin_pad : G.def.cin);
         ConvArgs a = (i < 4) ? conv_args(G, buf(a_in[i]), in_cs, buf(a_in[i + 1]), (long long)G.ho * G.wo * G.def.cout, G.def.cout, 0, N)
