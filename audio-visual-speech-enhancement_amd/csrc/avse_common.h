@@ -158,6 +158,26 @@ struct AudEncArgs {
     const float* sh[5];
 };
 bool aud_enc_supported(const AudEncArgs& a);
+
+// batched-clip GEMM (gemm.hip, bf16): mode 0 dense rows, mode 1 v_conv6 (3x3 'same' on 4 x 4 x 512 + 2x2 pool)
+struct GemmArgs {
+    const bf16_t* a;         // mode 0: [M][lda]; mode 1: input [M / 16][4][4][512], clip stride lda
+    long long lda;
+    const bf16_t* w;         // [N][kpad] (k = tap * 512 + c in mode 1)
+    int M, N, kpad;
+    const float* scale;      // folded bias + BN
+    const float* shift;
+    int act;
+    bf16_t* out;             // mode 0: out[m * ldo + out_off + n]; mode 1: out[clip * ldo + out_off + q * N + n]
+    long long ldo;
+    int out_off;
+    int ksplit;              // split-K over blockIdx.z, reduced by the last workgroup of each tile
+    float* partial;          // [tiles][ksplit][128 x 128] fp32
+    int* counters;           // [tiles], zero between launches
+};
+int gemm_ksplit(int M, int N, int kpad);
+size_t gemm_ws_bytes(int M, int N, int kpad);
+int launch_gemm(const GemmArgs& g, int mode, hipStream_t s);
 int launch_aud_enc(const AudEncArgs& a, hipStream_t s);
 int launch_dec_tail(const DecTailArgs& a, hipStream_t s);
 int launch_igemm(const ConvArgs& a, hipStream_t s);                      // igemm.hip (bf16)

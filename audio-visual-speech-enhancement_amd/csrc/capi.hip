@@ -157,6 +157,7 @@ struct avse_ctx {
     unsigned* umax = nullptr;
     int64_t umax_cap = 0;
     float* mse_partial = nullptr;
+    int* gemm_counters = nullptr;   // gemm.hip split-K tickets (zero between launches)
     char* arena = nullptr;
     size_t arena_bytes = 0;
     // side stream for the audio branch of the forward (runs concurrently with the video encoder)
@@ -268,6 +269,7 @@ size_t split_ws_bytes(int64_t N, int dtype) {
         const int bn = x.Co <= 64 ? 64 : 128;
         const size_t mp = (size_t)((x.M + 127) / 128) * 128, np = (size_t)((x.Co + bn - 1) / bn) * bn;
         if (ks > 1) mx = std::max(mx, (size_t)ks * mp * np * 4);
+        if (dtype == AVSE_BF16) mx = std::max(mx, gemm_ws_bytes((int)x.M, x.Co, x.kpad));   // gemm.hip's split-K
     }
     return mx;
 }
@@ -723,7 +725,11 @@ int avse_ctx_create(int device, avse_ctx** out) {
     AVSE_HIP_CHECK(hipSetDevice(device));
     avse_ctx* c = new avse_ctx();
     c->device = device;
-    if (hipMalloc((void**)&c->mse_partial, sizeof(float) * 256) != hipSuccess) {
+    if (hipMalloc((void**)&c->mse_partial, sizeof(float) * 256) != hipSuccess ||
+        hipMalloc((void**)&c->gemm_counters, sizeof(int) * 8192) != hipSuccess ||
+        hipMemset(c->gemm_counters, 0, sizeof(int) * 8192) != hipSuccess) {
+        (void)hipFree(c->mse_partial);
+    (void)hipFree(c->gemm_counters);
         delete c;
         return fail(AVSE_ERR_OOM, "hipMalloc failed (ctx)");
     }
@@ -905,6 +911,28 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
     size_t off[B_COUNT + 1];
     arena_bytes(N, dt, off);
     auto buf = [&](int b) { return (void*)(c->arena + off[b]); };
+    // dense layers and v_conv6 on gemm.hip (bf16; AVSE_NO_GEMM=1 keeps k_conv + split-K reduce)
+    const bool use_gemm = dt == AVSE_BF16 && !(std::getenv("AVSE_NO_GEMM") && std::getenv("AVSE_NO_GEMM")[0] == '1');
+    auto gemm = [&](const GpuLayer& G, const void* in, long long lda, void* outp, long long ldo, int out_off, int mode) {
+        GemmArgs g;
+        std::memset(&g, 0, sizeof(g));
+        g.a = reinterpret_cast<const bf16_t*>(in);
+        g.lda = lda;
+        g.w = reinterpret_cast<const bf16_t*>(G.w);
+        g.M = (int)(mode == 1 ? N * 16 : N);
+        g.N = G.def.cout;
+        g.kpad = G.ph[0].kpad;
+        g.scale = G.scale;
+        g.shift = G.shift;
+        g.act = 1;
+        g.out = reinterpret_cast<bf16_t*>(outp);
+        g.ldo = ldo;
+        g.out_off = out_off;
+        g.ksplit = gemm_ksplit(g.M, g.N, g.kpad);
+        g.partial = reinterpret_cast<float*>(c->arena + off[B_COUNT]);
+        g.counters = c->gemm_counters;
+        return launch_gemm(g, mode, s);
+    };
     auto split = [&](ConvArgs& a) {   // dense layers / v_conv6: split-K when the grid is small
         if (a.nphase != 1) return;
         const int64_t M = (int64_t)a.N * a.Hq * a.Wq;
@@ -990,6 +1018,11 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
             continue;
         }
         const long long in_cs = (long long)G.def.hin * G.def.win * (i == 0 ? G.cin_pad : G.def.cin);
+        if (i == 5 && use_gemm && G.def.hin == 4 && G.def.win == 4 && G.def.cin == 512 && G.def.kh == 3 && G.def.pool &&
+            G.ph[0].kpad == 9 * 512) {
+            if ((rc = gemm(G, buf(v_in[i]), in_cs, buf(B_CAT), 5248, 3200, 1)) || (rc = mark())) return rc;   // concat[3200:5248]
+            continue;
+        }
         ConvArgs a = (i < 5) ? conv_args(G, buf(v_in[i]), in_cs, buf(v_in[i + 1]), (long long)G.ho * G.wo * G.def.cout, G.def.cout, 0, N)
                              : conv_args(G, buf(v_in[i]), in_cs, buf(B_CAT), 5248, G.def.cout, 3200, N);  // concat[3200:5248]
         if (i == 5) split(a);
@@ -997,7 +1030,11 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
     }
     if (concurrent) AVSE_HIP_CHECK(hipStreamWaitEvent(s, c->join, 0));
     // fusion + decoder dense (network.py:53-58, :66-78)
-    {
+    if (use_gemm) {
+        if ((rc = gemm(L(11), buf(B_CAT), 5248, buf(B_E1), 1312, 0, 0)) || (rc = mark())) return rc;
+        if ((rc = gemm(L(12), buf(B_E1), 1312, buf(B_E2), 1312, 0, 0)) || (rc = mark())) return rc;
+        if ((rc = gemm(L(13), buf(B_E2), 1312, buf(B_E3), 3200, 0, 0)) || (rc = mark())) return rc;
+    } else {
         ConvArgs a = conv_args(L(11), buf(B_CAT), 5248, buf(B_E1), 1312, 1312, 0, N);
         split(a);
         if ((rc = run_conv(a, dt, s)) || (rc = mark())) return rc;

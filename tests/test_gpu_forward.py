@@ -220,3 +220,30 @@ def test_bf16_video_kernel_variants_agree(gpu, env, monkeypatch):
         assert rel_rms(sc_a[k], inter[k]) <= 1.5e-2, (k, rel_rms(sc_a[k], inter[k]))
         assert rel_rms(sc_a[k], sc_b[k]) <= 1e-2, (k, rel_rms(sc_a[k], sc_b[k]))
     assert rel_rms(out_a, out_b) <= 1e-2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N", [1, 5, 37])
+def test_bf16_fused_per_clip_kernels_match_layer_path(gpu, N, monkeypatch):
+    """The per-clip fused kernels (conv_aud.hip: a_conv1..a_conv5; conv_dec.hip: d_deconv4..d_deconv6) against the
+    layer-by-layer k_conv launches (AVSE_NO_AUDENC=1, AVSE_NO_DECTAIL=1) and the float64 oracle: the audio
+    embedding (concat[0:3200]) and the network output.  Both paths round every activation to bf16, so they differ
+    only in fp32 summation order."""
+    from avse_amd import ops
+    from avse_amd.model import KerasModel
+    model = KerasModel.init(seed=11, randomize=True)
+    mel, video = make_inputs(N, 31)
+    mean, std = R.video_normalizer_fit(video)
+    args = [ops.to_device(mel), ops.to_device(video), ops.to_device(mean), ops.to_device(std)]
+    inter = {}
+    ref = K.forward(model.layer_dict(), mel, R.video_normalize(video, mean, std).astype(np.float32), intermediates=inter)
+    dw = ops.DeviceWeights(model, "bfloat16")
+    out_f = ops.forward(dw, *args).cpu().numpy()
+    cat_f = scratch(dw, N)["concat"][:, :3200].copy()
+    monkeypatch.setenv("AVSE_NO_AUDENC", "1")
+    monkeypatch.setenv("AVSE_NO_DECTAIL", "1")
+    out_l = ops.forward(dw, *args).cpu().numpy()
+    cat_l = scratch(dw, N)["concat"][:, :3200].copy()
+    assert rel_rms(cat_f, cat_l) <= 1e-2, rel_rms(cat_f, cat_l)
+    assert rel_rms(out_f, out_l) <= 1e-2, rel_rms(out_f, out_l)
+    assert rel_rms(out_f.reshape(ref.shape), ref) <= 3e-2, rel_rms(out_f.reshape(ref.shape), ref)
