@@ -60,7 +60,8 @@ constexpr int ph_ny(int p) { return 2 + (p >> 1); }
 constexpr int ph_nx(int p) { return 2 + (p & 1); }
 constexpr int ph_nt(int p) { return ph_ny(p) * ph_nx(p); }
 constexpr int ph_woff(int p) { int s = 0; for (int q = 0; q < p; ++q) s += CO * ph_nt(q) * CO; return s; }  // elements
-__device__ __forceinline__ int ph_nt_rt(int p) { return p == 0 ? 4 : p == 3 ? 9 : 6; }
+constexpr int ph_pstart(int p) { int s = 0; for (int q = 0; q < p; ++q) s += (2 * ph_nt(q) + 3) / 4 * 4; return s; }  // padded
+constexpr int ph_ofp(int g) { int p = 0; while (p < 3 && g >= ph_pstart(p + 1)) ++p; return p; }
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, long long bytes) {
     const int nrec = bytes > kOOB ? kOOB : (bytes < 0 ? 0 : (int)bytes);
@@ -261,28 +262,28 @@ __global__ __launch_bounds__(NT, 1) void k_dec_tail(DecTailArgs a) {
     }
     float* const outc = a.out + (long long)clip * (4 * HW);
     const __amdgpu_buffer_rsrc_t rsW5 = make_rsrc(a.w5, (long long)ph_woff(4) * 2);
-    // weight cursor (slab S + 8 of the padded sequence): phase lp, slab ls of its 2 nt (padded to a multiple of 4)
-    int lp = 0, ls = 0;
-    auto bpiece5 = [&]() {
-        const int nt = lp == 0 ? 4 : lp == 3 ? 9 : lp > 3 ? 9 : 6;
-        const int base = (lp == 0 ? 0 : lp == 1 ? ph_woff(1) : lp == 2 ? ph_woff(2) : ph_woff(3)) * 2;
-        const i32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rsW5, brow * (nt * CO * 2) + kq * 16 + kh * 8, base + (ls < 2 * nt ? ls : 0) * 64, 0);
-        if (++ls == ((2 * nt + 3) / 4) * 4) { ls = 0; ++lp; }
-        return v;
+    // the padded slab sequence over the four phases (phase p: 2 nt slabs, slab = 2 tap + chunk, padded to a multiple
+    // of 4) is compile-time: tap offsets, ring slots and weight offsets are immediates / scalar constants
+    int vrow5[3];   // weight row byte offset of this lane's ring piece for kpad 256, 384, 576
+    vrow5[0] = brow * (4 * CO * 2) + kq * 16 + kh * 8;
+    vrow5[1] = brow * (6 * CO * 2) + kq * 16 + kh * 8;
+    vrow5[2] = brow * (9 * CO * 2) + kq * 16 + kh * 8;
+    auto bpiece5 = [&](auto gg) {   // ring piece of global padded slab g (past the end: phase 3's slab 0, unused)
+        constexpr int g = decltype(gg)::value < ph_pstart(4) ? decltype(gg)::value : ph_pstart(3);
+        constexpr int p = ph_ofp(g), sl = g - ph_pstart(p), sv = sl < 2 * ph_nt(p) ? sl : 0;
+        constexpr int kk = p == 0 ? 0 : p == 3 ? 2 : 1;
+        return __builtin_amdgcn_raw_buffer_load_b64(rsW5, vrow5[kk], ph_woff(p) * 2 + sv * 64, 0);
     };
-    // fragment cursor (the slab read next): tap (ta, tb) of the phase, chunk tc; offset of tap (dy, dx) from (-1, -1)
-    int rp = 0, ta = 0, tb = 0, tc = 0;
-    auto read_a5 = [&](i32x4 (&f)[NF]) {
-        const int imm = (((rp >> 1) - ta + 1) * P5 + ((rp & 1) - tb + 1)) * S5 + tc * 64;
+    auto read_a5 = [&](auto gg, i32x4 (&f)[NF]) {
+        constexpr int g = decltype(gg)::value;
+        constexpr int p = ph_ofp(g), sl = g - ph_pstart(p), tap = sl / 2, c = sl % 2;
+        constexpr int dy = (p >> 1) - tap / ph_nx(p), dx = (p & 1) - tap % ph_nx(p);
+        constexpr int imm = ((dy + 1) * P5 + (dx + 1)) * S5 + c * 64;
 #pragma unroll
-        for (int i = 0; i < NF; ++i) f[i] = lds16(lds, vb5[i] + imm);
-        if (++tc == 2) {
-            tc = 0;
-            if (++tb == 2 + (rp & 1)) { tb = 0; ++ta; }
-        }
+        for (int i = 0; i < NF; ++i) f[i] = lds16(lds + imm, vb5[i]);
     };
-    auto epilogue5 = [&](int p) {
-        const int py = p >> 1, px = p & 1;
+    auto epilogue5 = [&](auto pp) {
+        constexpr int p = decltype(pp)::value, py = p >> 1, px = p & 1;
         float part[NF][4];
 #pragma unroll
         for (int i = 0; i < NF; ++i)
@@ -318,43 +319,43 @@ __global__ __launch_bounds__(NT, 1) void k_dec_tail(DecTailArgs a) {
     i32x2 pb[4];
     {
         i32x2 w0[4];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) w0[t] = bpiece5();
-#pragma unroll
-        for (int t = 0; t < 4; ++t) pb[t] = bpiece5();
+        unroll(std::make_integer_sequence<int, 4>{}, [&](auto tt) {
+            constexpr int t = decltype(tt)::value;
+            w0[t] = bpiece5(tt);
+            pb[t] = bpiece5(std::integral_constant<int, t + 4>{});
+        });
 #pragma unroll
         for (int t = 0; t < 4; ++t) st8(bst + t * 4096, w0[t]);
     }
+    zero_acc();
     __syncthreads();
     i32x4 fa[2][NF], fb[2][4];
-    int G = 0;   // group of the slab being computed (padded sequence over the four phases)
-    for (int p = 0; p < 4; ++p) {
-        const int nsl = 2 * ph_nt_rt(p), npad = ((nsl + 3) / 4) * 4;
-        rp = p; ta = tb = tc = 0;
-        zero_acc();
-        read_a5(fa[0]);
-        read_b(bfr + (G & 1) * 16384, fb[0]);
-        // 4 slabs per iteration = one group: the padding slabs of phase 3 only move weights
-        for (int s0 = 0; s0 < npad; s0 += 4, ++G) {
-            const int bcur = bfr + (G & 1) * 16384, bnxt = bfr + ((G + 1) & 1) * 16384;
-            const int snxt = bst + ((G + 1) & 1) * 16384;
-            unroll(std::make_integer_sequence<int, 4>{}, [&](auto qq) {
-                constexpr int q = decltype(qq)::value;
-                const int s = s0 + q;
-                __builtin_amdgcn_sched_barrier(0);
-                st8(snxt + q * 4096, pb[q]);    // slab S + 4 -> the next group's slot
-                pb[q] = bpiece5();               // slab S + 8
-                if constexpr (q == 3) __syncthreads();
-                if (s + 1 < nsl) {
-                    read_a5(fa[(q + 1) & 1]);
-                    read_b(q == 3 ? bnxt : bcur + (q + 1) * 4096, fb[(q + 1) & 1]);
-                }
-                __builtin_amdgcn_sched_barrier(0);
-                if (s < nsl) mfma_all(fa[q & 1], fb[q & 1]);
-            });
+    read_a5(std::integral_constant<int, 0>{}, fa[0]);
+    read_b(bfr, fb[0]);
+    // global padded slab g: store g + 4 -> slot ((g / 4) + 1) & 1, load g + 8, barrier every 4 slabs; the fragments of
+    // g + 1 (the next phase's first slab at a phase end, read after its epilogue) go out before g's MFMAs
+    unroll(std::make_integer_sequence<int, ph_pstart(4)>{}, [&](auto gg) {
+        constexpr int g = decltype(gg)::value, p = ph_ofp(g);
+        constexpr bool real = g - ph_pstart(p) < 2 * ph_nt(p), last = g + 1 == ph_pstart(p + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        st8(bst + (((g / 4) + 1) & 1) * 16384 + (g % 4) * 4096, pb[g & 3]);
+        pb[g & 3] = bpiece5(std::integral_constant<int, g + 8>{});
+        if constexpr (g % 4 == 3) __syncthreads();
+        if constexpr (!last && g + 1 - ph_pstart(p) < 2 * ph_nt(p)) {
+            read_a5(std::integral_constant<int, g + 1>{}, fa[(g + 1) & 1]);
+            read_b(bfr + (((g + 1) / 4) & 1) * 16384 + ((g + 1) % 4) * 4096, fb[(g + 1) & 1]);
         }
-        epilogue5(p);
-    }
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (real) mfma_all(fa[g & 1], fb[g & 1]);
+        if constexpr (last) {
+            epilogue5(std::integral_constant<int, p>{});
+            if constexpr (p < 3) {
+                zero_acc();
+                read_a5(std::integral_constant<int, g + 1>{}, fa[(g + 1) & 1]);
+                read_b(bfr + (((g + 1) / 4) & 1) * 16384 + ((g + 1) % 4) * 4096, fb[(g + 1) & 1]);
+            }
+        }
+    });
 }
 
 }  // namespace
