@@ -159,6 +159,22 @@ struct AudEncArgs {
 };
 bool aud_enc_supported(const AudEncArgs& a);
 
+// fused decoder head d_deconv1 -> d_deconv3, one workgroup per clip (conv_dech.hip, bf16)
+struct DecHeadArgs {
+    const bf16_t* in;        // dec_dense2 output [N][3200] (= [5][5][128])
+    long long in_clip_stride;
+    bf16_t* out;             // d_deconv3 output [N][40][10][128]
+    long long out_clip_stride;
+    int N;
+    const bf16_t* w1;        // packed per phase [phase][128][kpad], k = tap * 128 + c (kpad 256, 256, 512)
+    const bf16_t* w2;
+    const bf16_t* w3;
+    const float* sc[3];
+    const float* sh[3];
+};
+bool dec_head_supported(const DecHeadArgs& a);
+int launch_dec_head(const DecHeadArgs& a, hipStream_t s);
+
 // batched-clip GEMM (gemm.hip, bf16): mode 0 dense rows, mode 1 v_conv6 (3x3 'same' on 4 x 4 x 512 + 2x2 pool)
 struct GemmArgs {
     const bf16_t* a;         // mode 0: [M][lda]; mode 1: input [M / 16][4][4][512], clip stride lda

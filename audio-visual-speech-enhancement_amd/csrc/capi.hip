@@ -1050,6 +1050,39 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
     for (int i = 0; i < 5; ++i) {
         const GpuLayer& G = L(14 + i);
         const long long in_cs = (long long)G.def.hin * G.def.win * G.def.cin;
+        if (i == 0 && dt == AVSE_BF16) {
+            // d_deconv1 + d_deconv2 + d_deconv3 in one kernel, one workgroup per clip (conv_dech.hip): the layers
+            // must have the network's shapes and sub-pixel tap grids (checked here)
+            auto taps_ok = [&](const GpuLayer& D, int np, int nt, bool wide) {
+                if (D.nphase != np || D.def.cin != 128 || D.def.cout != 128) return false;
+                for (int p = 0; p < np; ++p) {
+                    if (D.ph[p].ntaps != nt || D.ph[p].kpad != nt * 128 || D.ph[p].w_off != (long long)p * 128 * nt * 128) return false;
+                    for (int t = 0; t < nt; ++t) {
+                        const int2 d = D.htaps[D.ph[p].tap_off + t];
+                        const int dy = wide ? (p >> 1) - (t >> 1) : 0, dx = wide ? (p & 1) - (t & 1) : -t;
+                        if (d.x != dy || d.y != dx) return false;
+                    }
+                }
+                return true;
+            };
+            const bool shapes = L(14).hq == 5 && L(14).wq == 5 && L(15).hq == 10 && L(15).wq == 5 && L(16).hq == 20 &&
+                                L(16).wq == 5 && taps_ok(L(14), 2, 2, false) && taps_ok(L(15), 2, 2, false) &&
+                                taps_ok(L(16), 4, 4, true);
+            DecHeadArgs ha;
+            std::memset(&ha, 0, sizeof(ha));
+            ha.in = reinterpret_cast<const bf16_t*>(buf(B_E3));
+            ha.in_clip_stride = 3200;
+            ha.out = reinterpret_cast<bf16_t*>(buf(B_D3));
+            ha.out_clip_stride = 40 * 10 * 128;
+            ha.N = (int)N;
+            ha.w1 = (const bf16_t*)L(14).w; ha.w2 = (const bf16_t*)L(15).w; ha.w3 = (const bf16_t*)L(16).w;
+            for (int k = 0; k < 3; ++k) { ha.sc[k] = L(14 + k).scale; ha.sh[k] = L(14 + k).shift; }
+            if (shapes && dec_head_supported(ha)) {
+                if ((rc = launch_dec_head(ha, s)) || (rc = mark()) || (rc = mark()) || (rc = mark())) return rc;
+                i = 2;   // continue with d_deconv4
+                continue;
+            }
+        }
         if (i == 3 && dt == AVSE_BF16 && !unfused_tail()) {
             // d_deconv4 + d_deconv5 + d_deconv6 in one kernel, one workgroup per clip (conv_dec.hip)
             const DecTailArgs da = dec_tail_args(L(17), L(18), W, buf(d_in[3]), out, N);

@@ -1,0 +1,220 @@
+// Fused decoder head, one workgroup per clip (bf16, gfx950): network.py:112-123
+//   d_deconv1  Conv2DTranspose(128, 2x2, strides (2, 1), 'same')   5 x 5 x 128 -> 10 x 5 x 128
+//   d_deconv2  Conv2DTranspose(128, 2x2, strides (2, 1), 'same')  10 x 5 x 128 -> 20 x 5 x 128
+//   d_deconv3  Conv2DTranspose(128, 4x4, strides (2, 2), 'same')  20 x 5 x 128 -> 40 x 10 x 128 (-> HBM, k_dec_tail)
+// each + BatchNormalization + LeakyReLU(0.3); input = dec_dense2's [5, 5, 128] reshape.
+//
+// Why: three k_conv launches (~0.105 ms per 512 clips; d_deconv1 / d_deconv2 ~17-20 us each for 1-2 GFLOP,
+// d_deconv3 26.8 GFLOP at ~400 TFLOP/s).  The recipe of conv_aud.hip / conv_dec.hip: activations in zero-padded LDS
+// images (288-B rows: 128 channels + pad), weights through the LDS slab ring (8 KB slabs, groups of 2, the next
+// layer's first slabs prefetched under each epilogue), the sub-pixel phases of each transposed conv as in k_conv
+// (only the taps that hit a phase: phase (py, px) tap (a, b) = input offset (py - a, px - b)), the whole slab
+// schedule compile-time.
+//   * d_deconv1 / d_deconv2: wave w owns output channels 16 w .. 16 w + 15 and all M fragments of a phase;
+//   * d_deconv3 (7 M fragments per phase): wave (mh, nq) owns fragments 4 mh .. 4 mh + 3 x channels 32 nq .. + 31.
+#include <cstdlib>
+#include <utility>
+
+#include "avse_common.h"
+
+namespace avse {
+namespace {
+
+constexpr float LRELU = 0.3f;
+constexpr int NW = 8, NT = 64 * NW;
+constexpr int S = 288;                                       // image pixel stride (128 bf16 channels + 32 B)
+constexpr int IMG3 = 0, P3 = 7, IMG3B = 22 * P3 * S;         // d_deconv3 input: 20 x 5 padded by 1 -> 22 x 7
+constexpr int IMG1 = 44544, P1 = 6, IMG1B = 5 * P1 * S;      // d_deconv1 input: 5 x 5, left pad 1 -> 5 x 6
+constexpr int IMG2 = 53248, P2 = 6, IMG2B = 10 * P2 * S;     // d_deconv2 input: 10 x 5, left pad 1 -> 10 x 6
+constexpr int BOFF = 71680;                                  // weight ring: 2 slots x 2 slabs x 8 KB
+constexpr int LDS_BYTES = BOFF + 32768;                      // 104,448
+static_assert(IMG3B <= IMG1 && IMG1 + IMG1B <= IMG2 && IMG2 + IMG2B <= BOFF, "LDS map");
+
+struct Pre { i32x4 w0, w1, p0, p1; };
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, long long bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ int wsw(int row) { return 2 * ((row >> 2) & 1); }
+__device__ __forceinline__ i32x4 lds16(const char* base, int off) { return *reinterpret_cast<const i32x4*>(base + off); }
+template <int... I, typename F>
+__device__ __forceinline__ void unroll(std::integer_sequence<int, I...>, F&& f) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+__device__ __forceinline__ f32x4 mfma(i32x4 a, i32x4 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+__device__ __forceinline__ float bn_lrelu(float acc, float sc, float sh) {
+    const float v = acc * sc + sh;
+    return v >= 0.f ? v : LRELU * v;
+}
+
+// Layer geometry.  L = 1, 2: phases py in {0, 1} (px = 0), taps b in {0, 1}: input (yq, xq - b); grid HQ x 5.
+// L = 3: phases (py, px), taps (a, b) in {0, 1}^2: input (yq + py - a, xq + px - b); grid 20 x 5.
+template <int L> struct Geo {
+    static constexpr int NP = L == 3 ? 4 : 2, NTAP = L == 3 ? 4 : 2, HQ = L == 1 ? 5 : L == 2 ? 10 : 20, WQ = 5;
+    static constexpr int M = HQ * WQ, NFR = (M + 15) / 16;            // M fragments per phase
+    static constexpr int NSL = NTAP * 4;                               // slabs per phase: tap * 4 + chunk
+    static constexpr int KPAD = NTAP * 128;
+    static constexpr int IMG = L == 1 ? IMG1 : L == 2 ? IMG2 : IMG3, P = L == 3 ? P3 : P1, PT = L == 3 ? 1 : 0, PL = 1;
+    // smallest tap offset: (dy, dx) = (-1, -1) for L = 3, (0, -1) otherwise
+    static constexpr int DY0 = L == 3 ? -1 : 0, DX0 = -1;
+    static constexpr int tap_dy(int p, int t) { return L == 3 ? (p >> 1) - (t >> 1) : 0; }
+    static constexpr int tap_dx(int p, int t) { return L == 3 ? (p & 1) - (t & 1) : -t; }
+};
+
+__global__ __launch_bounds__(NT, 1) void k_dec_head(DecHeadArgs a) {
+    extern __shared__ __attribute__((aligned(1024))) char lds[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r16 = lane & 15, kg = lane >> 4;
+    const int clip = blockIdx.x;
+    const int mh = w >> 2, nq = w & 3;   // d_deconv3's wave split
+    auto st16 = [&](int addr, i32x4 v) { *reinterpret_cast<i32x4*>(lds + addr) = v; };
+
+    // ---- weight ring: lane tid moves 16 B (kq = tid & 3) of row tid >> 2 of an 8-KB slab ----
+    const int brow = tid >> 2, kq = tid & 3;
+    const int bst = BOFF + brow * 64 + ((kq ^ wsw(brow)) << 4);   // + slot 16384 + pos 8192
+    const __amdgpu_buffer_rsrc_t rsW1 = make_rsrc(a.w1, 2 * 128 * 256 * 2), rsW2 = make_rsrc(a.w2, 2 * 128 * 256 * 2),
+                                 rsW3 = make_rsrc(a.w3, 4 * 128 * 512 * 2);
+    // ring piece of slab s of layer L (phase s / NSL, slab within phase s % NSL): k = tap * 128 + chunk * 32
+    auto piece = [&](auto ll, auto ss) -> i32x4 {
+        constexpr int LL = decltype(ll)::value, s = decltype(ss)::value;
+        using G = Geo<LL>;
+        constexpr int sv = s < G::NP * G::NSL ? s : 0, p = sv / G::NSL, sl = sv % G::NSL;
+        const __amdgpu_buffer_rsrc_t& rs = LL == 1 ? rsW1 : LL == 2 ? rsW2 : rsW3;
+        return __builtin_amdgcn_raw_buffer_load_b128(rs, brow * (G::KPAD * 2) + kq * 16, (p * 128 * G::KPAD + sl * 32) * 2, 0);
+    };
+    auto prefetch = [&](auto ll) {
+        Pre pr;
+        pr.w0 = piece(ll, std::integral_constant<int, 0>{});
+        pr.w1 = piece(ll, std::integral_constant<int, 1>{});
+        pr.p0 = piece(ll, std::integral_constant<int, 2>{});
+        pr.p1 = piece(ll, std::integral_constant<int, 3>{});
+        return pr;
+    };
+
+    // ---- d_deconv1 input: dec_dense2's 5 x 5 x 128 (HWC) -> image pixel (y, x + 1) ----
+    for (int o = tid * 16; o < BOFF; o += NT * 16) st16(o, (i32x4){0, 0, 0, 0});   // zero padding rings
+    Pre pre = prefetch(std::integral_constant<int, 1>{});
+    __syncthreads();
+    if (tid < 400) {
+        const int px = tid >> 4, part = tid & 15, y = px / 5, x = px - y * 5;
+        const i32x4 v = *reinterpret_cast<const i32x4*>(reinterpret_cast<const char*>(a.in) + (long long)clip * a.in_clip_stride * 2 + px * 256 + part * 16);
+        st16(IMG1 + (y * P1 + x + 1) * S + part * 16, v);
+    }
+
+    auto layer = [&](auto ll, const float* scp, const float* shp, auto store, auto next) {
+        constexpr int LL = decltype(ll)::value;
+        using G = Geo<LL>;
+        constexpr bool WIDE = LL == 3;                 // waves split M and N (d_deconv3) or N only
+        constexpr int NI = WIDE ? 4 : G::NFR, NJ = WIDE ? 2 : 1;
+        const int row0 = WIDE ? 32 * nq : 16 * w;      // this wave's first output channel
+        // fragment slot i: M fragment (WIDE ? 4 mh + i : i), lane row r16 -> grid (yq, xq) -> image base at tap (DY0, DX0)
+        int vb[NI];
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int f = WIDE ? 4 * mh + i : i, m = (16 * f + r16 < G::M) ? 16 * f + r16 : 0;
+            const int yq = m / 5, xq = m - yq * 5;
+            vb[i] = G::IMG + ((yq + G::PT + G::DY0) * G::P + (xq + G::PL + G::DX0)) * S + kg * 16;
+        }
+        float sc[NJ], sh[NJ];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) { sc[j] = scp[row0 + 16 * j + r16]; sh[j] = shp[row0 + 16 * j + r16]; }
+        f32x4 acc[NI][NJ];
+        auto zero_acc = [&] {
+#pragma unroll
+            for (int i = 0; i < NI; ++i)
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        };
+        i32x4 fa[2][NI], fb[2][NJ];
+        auto read = [&](auto ss, int buf) {
+            constexpr int s = decltype(ss)::value, p = s / G::NSL, sl = s % G::NSL, t = sl / 4, c = sl % 4;
+            constexpr int imm = ((G::tap_dy(p, t) - G::DY0) * G::P + (G::tap_dx(p, t) - G::DX0)) * S + c * 64;
+#pragma unroll
+            for (int i = 0; i < NI; ++i) fa[buf][i] = lds16(lds + imm, vb[i]);
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+                fb[buf][j] = lds16(lds, BOFF + (((s / 2) & 1) * 16384 + (s % 2) * 8192) + (row0 + 16 * j + r16) * 64 +
+                                            ((kg ^ wsw(r16)) << 4));
+        };
+        i32x4 pb[2] = {pre.p0, pre.p1};
+        st16(bst, pre.w0);
+        st16(bst + 8192, pre.w1);
+        zero_acc();
+        __syncthreads();
+        read(std::integral_constant<int, 0>{}, 0);
+        constexpr int NS = G::NP * G::NSL;
+        unroll(std::make_integer_sequence<int, NS>{}, [&](auto ss) {
+            constexpr int s = decltype(ss)::value, p = s / G::NSL;
+            constexpr bool last = (s + 1) % G::NSL == 0;
+            __builtin_amdgcn_sched_barrier(0);
+            st16(bst + (((s / 2) + 1) & 1) * 16384 + (s % 2) * 8192, pb[s & 1]);   // slab s + 2
+            pb[s & 1] = piece(ll, std::integral_constant<int, s + 4>{});          // slab s + 4
+            if constexpr (s % 2 == 1) __syncthreads();
+            if constexpr (s + 1 < NS && !last) read(std::integral_constant<int, s + 1>{}, (s + 1) & 1);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 0; i < NI; ++i)
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) acc[i][j] = mfma(fa[s & 1][i], fb[s & 1][j], acc[i][j]);
+            if constexpr (last) {
+                if constexpr (p + 1 == G::NP) {   // layer done: the next layer's first slabs load under this epilogue
+                    __syncthreads();
+                    next();
+                }
+                // epilogue of phase p: grid (yq, xq) -> output (2 yq + py, OXS xq + px)
+                constexpr int py = LL == 3 ? p >> 1 : p, px = LL == 3 ? p & 1 : 0;
+#pragma unroll
+                for (int i = 0; i < NI; ++i)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int m = 16 * (WIDE ? 4 * mh + i : i) + 4 * kg + e;
+                        if (m >= G::M) continue;
+                        const int yq = m / 5, xq = m - yq * 5;
+#pragma unroll
+                        for (int j = 0; j < NJ; ++j)
+                            store(2 * yq + py, (LL == 3 ? 2 : 1) * xq + px, row0 + 16 * j + r16, bn_lrelu(acc[i][j][e], sc[j], sh[j]));
+                    }
+                if constexpr (p + 1 < G::NP) {
+                    zero_acc();
+                    read(std::integral_constant<int, s + 1>{}, (s + 1) & 1);
+                }
+            }
+        });
+        __syncthreads();
+    };
+
+    layer(std::integral_constant<int, 1>{}, a.sc[0], a.sh[0], [&](int y, int x, int n, float v) {
+        *reinterpret_cast<bf16_t*>(lds + IMG2 + (y * P2 + x + 1) * S + n * 2) = (bf16_t)v;
+    }, [&] { pre = prefetch(std::integral_constant<int, 2>{}); });
+    layer(std::integral_constant<int, 2>{}, a.sc[1], a.sh[1], [&](int y, int x, int n, float v) {
+        *reinterpret_cast<bf16_t*>(lds + IMG3 + ((y + 1) * P3 + x + 1) * S + n * 2) = (bf16_t)v;
+    }, [&] { pre = prefetch(std::integral_constant<int, 3>{}); });
+    bf16_t* const outc = a.out + (long long)clip * a.out_clip_stride;
+    layer(std::integral_constant<int, 3>{}, a.sc[2], a.sh[2], [&](int y, int x, int n, float v) {
+        outc[(y * 10 + x) * 128 + n] = (bf16_t)v;
+    }, [] {});
+}
+
+}  // namespace
+
+bool dec_head_supported(const DecHeadArgs& a) {
+    const char* e = std::getenv("AVSE_NO_DECHEAD");
+    if (e && e[0] == '1') return false;
+    return a.N > 0 && a.w1 && a.w2 && a.w3;
+}
+
+int launch_dec_head(const DecHeadArgs& a, hipStream_t s) {
+    static bool attr = false;
+    if (!attr) {
+        AVSE_HIP_CHECK(hipFuncSetAttribute((const void*)k_dec_head, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
+        attr = true;
+    }
+    hipLaunchKernelGGL(k_dec_head, dim3(a.N), dim3(NT), LDS_BYTES, s, a);
+    AVSE_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+}  // namespace avse

@@ -225,8 +225,9 @@ def test_bf16_video_kernel_variants_agree(gpu, env, monkeypatch):
 @pytest.mark.gpu
 @pytest.mark.parametrize("N", [1, 5, 37])
 def test_bf16_fused_per_clip_kernels_match_layer_path(gpu, N, monkeypatch):
-    """The per-clip fused kernels (conv_aud.hip: a_conv1..a_conv5; conv_dec.hip: d_deconv4..d_deconv6) against the
-    layer-by-layer k_conv launches (AVSE_NO_AUDENC=1, AVSE_NO_DECTAIL=1) and the float64 oracle: the audio
+    """The per-clip fused kernels (conv_aud.hip: a_conv1..a_conv5; conv_dech.hip: d_deconv1..d_deconv3; conv_dec.hip:
+    d_deconv4..d_deconv6) and gemm.hip (v_conv6, dense) against the layer-by-layer k_conv launches
+    (AVSE_NO_AUDENC / AVSE_NO_DECHEAD / AVSE_NO_DECTAIL / AVSE_NO_GEMM = 1) and the float64 oracle: the audio
     embedding (concat[0:3200]) and the network output.  Both paths round every activation to bf16, so they differ
     only in fp32 summation order."""
     from avse_amd import ops
@@ -240,8 +241,8 @@ def test_bf16_fused_per_clip_kernels_match_layer_path(gpu, N, monkeypatch):
     dw = ops.DeviceWeights(model, "bfloat16")
     out_f = ops.forward(dw, *args).cpu().numpy()
     cat_f = scratch(dw, N)["concat"][:, :3200].copy()
-    monkeypatch.setenv("AVSE_NO_AUDENC", "1")
-    monkeypatch.setenv("AVSE_NO_DECTAIL", "1")
+    for env in ("AVSE_NO_AUDENC", "AVSE_NO_DECHEAD", "AVSE_NO_DECTAIL", "AVSE_NO_GEMM"):
+        monkeypatch.setenv(env, "1")
     out_l = ops.forward(dw, *args).cpu().numpy()
     cat_l = scratch(dw, N)["concat"][:, :3200].copy()
     assert rel_rms(cat_f, cat_l) <= 1e-2, rel_rms(cat_f, cat_l)
