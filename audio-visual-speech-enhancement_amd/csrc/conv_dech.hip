@@ -1,4 +1,4 @@
-// Fused decoder head, one workgroup per clip (bf16, gfx950): network.py:112-123
+// Fused decoder head, two clips per workgroup (bf16, gfx950): network.py:112-123
 //   d_deconv1  Conv2DTranspose(128, 2x2, strides (2, 1), 'same')   5 x 5 x 128 -> 10 x 5 x 128
 //   d_deconv2  Conv2DTranspose(128, 2x2, strides (2, 1), 'same')  10 x 5 x 128 -> 20 x 5 x 128
 //   d_deconv3  Conv2DTranspose(128, 4x4, strides (2, 2), 'same')  20 x 5 x 128 -> 40 x 10 x 128 (-> HBM, k_dec_tail)
@@ -10,8 +10,16 @@
 // layer's first slabs prefetched under each epilogue), the sub-pixel phases of each transposed conv as in k_conv
 // (only the taps that hit a phase: phase (py, px) tap (a, b) = input offset (py - a, px - b)), the whole slab
 // schedule compile-time.
-//   * d_deconv1 / d_deconv2: wave w owns output channels 16 w .. 16 w + 15 and all M fragments of a phase;
-//   * d_deconv3 (7 M fragments per phase): wave (mh, nq) owns fragments 4 mh .. 4 mh + 3 x channels 32 nq .. + 31.
+// The head's layers are small (M = 25 / 50 / 100 pixels per phase and clip) against 768 KB of weights per clip: with
+// one clip per workgroup a slab carried 2-8 MFMAs per wave and the weight stream (L2 latency, 8 KB per slab, two
+// slabs of look-ahead) bounded the kernel.  Here:
+//   * two clips share every weight slab (twice the MFMAs per slab, half the weight traffic per clip);
+//   * the weight pieces run DA slabs ahead in registers;
+//   * the MFMA computes D = W x A (channels x pixels): a lane's 4 accumulator rows are 4 consecutive channels of one
+//     pixel, so the epilogue stores 8 B per lane and fragment (ds_write_b64 / buffer 8-B stores) instead of four
+//     2-byte stores;
+//   * d_deconv1 / d_deconv2: wave w owns output channels 16 w .. 16 w + 15 and all M fragments of both clips;
+//     d_deconv3 (7 M fragments per phase and clip): wave (c, nq) owns clip c's fragments x channels 32 nq .. + 31.
 #include <cstdlib>
 #include <utility>
 
@@ -22,15 +30,28 @@ namespace {
 
 constexpr float LRELU = 0.3f;
 constexpr int NW = 8, NT = 64 * NW;
+constexpr int NC = 2;                                        // clips per workgroup
 constexpr int S = 288;                                       // image pixel stride (128 bf16 channels + 32 B)
+// per-clip LDS region: d_deconv3's input image, d_deconv1's input aliased into its first 30 pixels (dead once
+// d_deconv1 is done; the border pixels it covered are re-zeroed before d_deconv3 reads them), d_deconv2's input
 constexpr int IMG3 = 0, P3 = 7, IMG3B = 22 * P3 * S;         // d_deconv3 input: 20 x 5 padded by 1 -> 22 x 7
-constexpr int IMG1 = 44544, P1 = 6, IMG1B = 5 * P1 * S;      // d_deconv1 input: 5 x 5, left pad 1 -> 5 x 6
-constexpr int IMG2 = 53248, P2 = 6, IMG2B = 10 * P2 * S;     // d_deconv2 input: 10 x 5, left pad 1 -> 10 x 6
-constexpr int BOFF = 71680;                                  // weight ring: 2 slots x 2 slabs x 8 KB
-constexpr int LDS_BYTES = BOFF + 32768;                      // 104,448
-static_assert(IMG3B <= IMG1 && IMG1 + IMG1B <= IMG2 && IMG2 + IMG2B <= BOFF, "LDS map");
+constexpr int IMG1 = 0, P1 = 6, IMG1B = 5 * P1 * S;          // d_deconv1 input: 5 x 5, left pad 1 -> 5 x 6
+constexpr int IMG2 = IMG3B, P2 = 6, IMG2B = 10 * P2 * S;     // d_deconv2 input: 10 x 5, left pad 1 -> 10 x 6
+constexpr int CLB = IMG2 + IMG2B;                            // 61,632 B per clip
+constexpr int BOFF = NC * CLB;                               // weight ring: 2 slots x 2 slabs x 8 KB
+constexpr int LDS_BYTES = BOFF + 32768;                      // 156,032
+constexpr int DA = 6;                                        // weight pieces in flight in registers
+static_assert(NC == 2 && IMG1B <= IMG3B && CLB % 64 == 0 && LDS_BYTES <= 160 * 1024, "LDS map");
+// IMG3 border pixels among IMG1's 30: row 0, columns 0 / 6 of rows 1..3, (4, 0)
+constexpr int NBZ = 14;
+__device__ __forceinline__ int border_px(int i) {
+    return i < 7 ? i : i < 13 ? ((i - 7) / 2 + 1) * P3 + ((i - 7) & 1) * 6 : 4 * P3;
+}
 
-struct Pre { i32x4 w0, w1, p0, p1; };
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef int i32x2 __attribute__((ext_vector_type(2)));
+struct Pre { i32x4 w[DA + 2]; };   // a layer's first DA + 2 weight pieces
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, long long bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
@@ -45,15 +66,21 @@ __device__ __forceinline__ f32x4 mfma(i32x4 a, i32x4 b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
 }
 __device__ __forceinline__ float bn_lrelu(float acc, float sc, float sh) {
-    const float v = acc * sc + sh;
-    return v >= 0.f ? v : LRELU * v;
+    const float v = fmaf(acc, sc, sh);
+    float r;
+    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(v), "v"(LRELU * v));   // LeakyReLU, no canonicalise
+    return r;
+}
+__device__ __forceinline__ i32x2 pack4(float a, float b, float c, float d) {   // 4 bf16 (RNE, as (bf16_t) casts)
+    const bf16x2 lo = __builtin_convertvector((f32x2){a, b}, bf16x2), hi = __builtin_convertvector((f32x2){c, d}, bf16x2);
+    return (i32x2){__builtin_bit_cast(int, lo), __builtin_bit_cast(int, hi)};
 }
 
 // Layer geometry.  L = 1, 2: phases py in {0, 1} (px = 0), taps b in {0, 1}: input (yq, xq - b); grid HQ x 5.
 // L = 3: phases (py, px), taps (a, b) in {0, 1}^2: input (yq + py - a, xq + px - b); grid 20 x 5.
 template <int L> struct Geo {
     static constexpr int NP = L == 3 ? 4 : 2, NTAP = L == 3 ? 4 : 2, HQ = L == 1 ? 5 : L == 2 ? 10 : 20, WQ = 5;
-    static constexpr int M = HQ * WQ, NFR = (M + 15) / 16;            // M fragments per phase
+    static constexpr int M = HQ * WQ, NFR = (M + 15) / 16;            // M fragments per phase and clip
     static constexpr int NSL = NTAP * 4;                               // slabs per phase: tap * 4 + chunk
     static constexpr int KPAD = NTAP * 128;
     static constexpr int IMG = L == 1 ? IMG1 : L == 2 ? IMG2 : IMG3, P = L == 3 ? P3 : P1, PT = L == 3 ? 1 : 0, PL = 1;
@@ -63,13 +90,16 @@ template <int L> struct Geo {
     static constexpr int tap_dx(int p, int t) { return L == 3 ? (p & 1) - (t & 1) : -t; }
 };
 
+// ABL: ablation mask for tools/dech_ablate.hip only (0 in the library): 1 = no MFMAs, 2 = no epilogue stores,
+// 4 = no barriers in the slab loop (2: the stores are skipped by a runtime test, so the MFMAs stay live), 8 = no weight-piece loads (timing only: results are meaningless)
+template <int ABL = 0>
 __global__ __launch_bounds__(NT, 1) void k_dec_head(DecHeadArgs a) {
     extern __shared__ __attribute__((aligned(1024))) char lds[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int r16 = lane & 15, kg = lane >> 4;
-    const int clip = blockIdx.x;
-    const int mh = w >> 2, nq = w & 3;   // d_deconv3's wave split
+    const int clip0 = NC * blockIdx.x;
+    const int mh = w >> 2, nq = w & 3;   // d_deconv3's wave split: clip mh, channels 32 nq .. + 31
     auto st16 = [&](int addr, i32x4 v) { *reinterpret_cast<i32x4*>(lds + addr) = v; };
 
     // ---- weight ring: lane tid moves 16 B (kq = tid & 3) of row tid >> 2 of an 8-KB slab ----
@@ -83,14 +113,12 @@ __global__ __launch_bounds__(NT, 1) void k_dec_head(DecHeadArgs a) {
         using G = Geo<LL>;
         constexpr int sv = s < G::NP * G::NSL ? s : 0, p = sv / G::NSL, sl = sv % G::NSL;
         const __amdgpu_buffer_rsrc_t& rs = LL == 1 ? rsW1 : LL == 2 ? rsW2 : rsW3;
+        if constexpr ((ABL & 8) != 0) return (i32x4){s, 0, 0, 0};
         return __builtin_amdgcn_raw_buffer_load_b128(rs, brow * (G::KPAD * 2) + kq * 16, (p * 128 * G::KPAD + sl * 32) * 2, 0);
     };
     auto prefetch = [&](auto ll) {
         Pre pr;
-        pr.w0 = piece(ll, std::integral_constant<int, 0>{});
-        pr.w1 = piece(ll, std::integral_constant<int, 1>{});
-        pr.p0 = piece(ll, std::integral_constant<int, 2>{});
-        pr.p1 = piece(ll, std::integral_constant<int, 3>{});
+        unroll(std::make_integer_sequence<int, DA + 2>{}, [&](auto k) { pr.w[decltype(k)::value] = piece(ll, k); });
         return pr;
     };
 
@@ -98,29 +126,39 @@ __global__ __launch_bounds__(NT, 1) void k_dec_head(DecHeadArgs a) {
     for (int o = tid * 16; o < BOFF; o += NT * 16) st16(o, (i32x4){0, 0, 0, 0});   // zero padding rings
     Pre pre = prefetch(std::integral_constant<int, 1>{});
     __syncthreads();
-    if (tid < 400) {
-        const int px = tid >> 4, part = tid & 15, y = px / 5, x = px - y * 5;
+    for (int q = tid; q < NC * 400; q += NT) {
+        const int c = q >= 400, r = q - 400 * c;
+        const int px = r >> 4, part = r & 15, y = px / 5, x = px - y * 5;
+        const int clip = clip0 + c < a.N ? clip0 + c : a.N - 1;   // a missing second clip computes on a copy
         const i32x4 v = *reinterpret_cast<const i32x4*>(reinterpret_cast<const char*>(a.in) + (long long)clip * a.in_clip_stride * 2 + px * 256 + part * 16);
-        st16(IMG1 + (y * P1 + x + 1) * S + part * 16, v);
+        st16(c * CLB + IMG1 + (y * P1 + x + 1) * S + part * 16, v);
     }
 
     auto layer = [&](auto ll, const float* scp, const float* shp, auto store, auto next) {
         constexpr int LL = decltype(ll)::value;
         using G = Geo<LL>;
-        constexpr bool WIDE = LL == 3;                 // waves split M and N (d_deconv3) or N only
-        constexpr int NI = WIDE ? 4 : G::NFR, NJ = WIDE ? 2 : 1;
+        constexpr bool WIDE = LL == 3;                 // waves split clips and N (d_deconv3) or N only
+        constexpr int NI = WIDE ? G::NFR : NC * G::NFR, NJ = WIDE ? 2 : 1;
         const int row0 = WIDE ? 32 * nq : 16 * w;      // this wave's first output channel
-        // fragment slot i: M fragment (WIDE ? 4 mh + i : i), lane row r16 -> grid (yq, xq) -> image base at tap (DY0, DX0)
+        // fragment slot i: clip (WIDE ? mh : i / NFR), M fragment (WIDE ? i : i % NFR); lane row r16 -> grid
+        // (yq, xq) -> image base at tap (DY0, DX0)
         int vb[NI];
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
-            const int f = WIDE ? 4 * mh + i : i, m = (16 * f + r16 < G::M) ? 16 * f + r16 : 0;
+            const int c = WIDE ? mh : i / G::NFR, f = WIDE ? i : i % G::NFR;
+            const int m = (16 * f + r16 < G::M) ? 16 * f + r16 : 0;
             const int yq = m / 5, xq = m - yq * 5;
-            vb[i] = G::IMG + ((yq + G::PT + G::DY0) * G::P + (xq + G::PL + G::DX0)) * S + kg * 16;
+            vb[i] = c * CLB + G::IMG + ((yq + G::PT + G::DY0) * G::P + (xq + G::PL + G::DX0)) * S + kg * 16;
         }
-        float sc[NJ], sh[NJ];
+        // accumulator row e of channel fragment j = channel row0 + 16 j + 4 kg + e
+        float sc[NJ][4], sh[NJ][4];
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) { sc[j] = scp[row0 + 16 * j + r16]; sh[j] = shp[row0 + 16 * j + r16]; }
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                sc[j][e] = scp[row0 + 16 * j + 4 * kg + e];
+                sh[j][e] = shp[row0 + 16 * j + 4 * kg + e];
+            }
         f32x4 acc[NI][NJ];
         auto zero_acc = [&] {
 #pragma unroll
@@ -139,44 +177,54 @@ __global__ __launch_bounds__(NT, 1) void k_dec_head(DecHeadArgs a) {
                 fb[buf][j] = lds16(lds, BOFF + (((s / 2) & 1) * 16384 + (s % 2) * 8192) + (row0 + 16 * j + r16) * 64 +
                                             ((kg ^ wsw(r16)) << 4));
         };
-        i32x4 pb[2] = {pre.p0, pre.p1};
-        st16(bst, pre.w0);
-        st16(bst + 8192, pre.w1);
+        constexpr int NS = G::NP * G::NSL;
+        // register ring: pb[s % DA] holds slab s + 2 at step s
+        i32x4 pb[DA];
+#pragma unroll
+        for (int k = 0; k < DA; ++k) pb[k] = pre.w[k + 2];
+        st16(bst, pre.w[0]);
+        st16(bst + 8192, pre.w[1]);
         zero_acc();
         __syncthreads();
         read(std::integral_constant<int, 0>{}, 0);
-        constexpr int NS = G::NP * G::NSL;
         unroll(std::make_integer_sequence<int, NS>{}, [&](auto ss) {
             constexpr int s = decltype(ss)::value, p = s / G::NSL;
             constexpr bool last = (s + 1) % G::NSL == 0;
             __builtin_amdgcn_sched_barrier(0);
-            st16(bst + (((s / 2) + 1) & 1) * 16384 + (s % 2) * 8192, pb[s & 1]);   // slab s + 2
-            pb[s & 1] = piece(ll, std::integral_constant<int, s + 4>{});          // slab s + 4
-            if constexpr (s % 2 == 1) __syncthreads();
+            if constexpr (s + 2 < NS) {
+                st16(bst + (((s / 2) + 1) & 1) * 16384 + (s % 2) * 8192, pb[s % DA]);    // slab s + 2
+                if constexpr (s + 2 + DA < NS) pb[s % DA] = piece(ll, std::integral_constant<int, s + 2 + DA>{});
+            }
+            if constexpr (s % 2 == 1 && !(ABL & 4)) __syncthreads();
             if constexpr (s + 1 < NS && !last) read(std::integral_constant<int, s + 1>{}, (s + 1) & 1);
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int i = 0; i < NI; ++i)
 #pragma unroll
-                for (int j = 0; j < NJ; ++j) acc[i][j] = mfma(fa[s & 1][i], fb[s & 1][j], acc[i][j]);
+                for (int j = 0; j < NJ; ++j)
+                    if constexpr (!(ABL & 1)) acc[i][j] = mfma(fb[s & 1][j], fa[s & 1][i], acc[i][j]);   // W x A
+                    else acc[i][j][0] += __builtin_bit_cast(float, fa[s & 1][i][0] ^ fb[s & 1][j][0]);
             if constexpr (last) {
                 if constexpr (p + 1 == G::NP) {   // layer done: the next layer's first slabs load under this epilogue
                     __syncthreads();
                     next();
                 }
-                // epilogue of phase p: grid (yq, xq) -> output (2 yq + py, OXS xq + px)
+                // epilogue of phase p: lane pixel m = 16 f + r16 of the grid (yq, xq) -> output (2 yq + py, OXS xq + px)
                 constexpr int py = LL == 3 ? p >> 1 : p, px = LL == 3 ? p & 1 : 0;
 #pragma unroll
-                for (int i = 0; i < NI; ++i)
+                for (int i = 0; i < NI; ++i) {
+                    const int c = WIDE ? mh : i / G::NFR, f = WIDE ? i : i % G::NFR;
+                    const int m = 16 * f + r16;
+                    if (((ABL & 2) != 0 && a.N != -1) || (16 * f + 15 >= G::M && m >= G::M)) continue;
+                    const int yq = m / 5, xq = m - yq * 5;
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        const int m = 16 * (WIDE ? 4 * mh + i : i) + 4 * kg + e;
-                        if (m >= G::M) continue;
-                        const int yq = m / 5, xq = m - yq * 5;
-#pragma unroll
-                        for (int j = 0; j < NJ; ++j)
-                            store(2 * yq + py, (LL == 3 ? 2 : 1) * xq + px, row0 + 16 * j + r16, bn_lrelu(acc[i][j][e], sc[j], sh[j]));
+                    for (int j = 0; j < NJ; ++j) {
+                        const f32x4 v = acc[i][j];
+                        store(c, 2 * yq + py, (LL == 3 ? 2 : 1) * xq + px, row0 + 16 * j + 4 * kg,
+                              pack4(bn_lrelu(v[0], sc[j][0], sh[j][0]), bn_lrelu(v[1], sc[j][1], sh[j][1]),
+                                    bn_lrelu(v[2], sc[j][2], sh[j][2]), bn_lrelu(v[3], sc[j][3], sh[j][3])));
                     }
+                }
                 if constexpr (p + 1 < G::NP) {
                     zero_acc();
                     read(std::integral_constant<int, s + 1>{}, (s + 1) & 1);
@@ -186,15 +234,22 @@ __global__ __launch_bounds__(NT, 1) void k_dec_head(DecHeadArgs a) {
         __syncthreads();
     };
 
-    layer(std::integral_constant<int, 1>{}, a.sc[0], a.sh[0], [&](int y, int x, int n, float v) {
-        *reinterpret_cast<bf16_t*>(lds + IMG2 + (y * P2 + x + 1) * S + n * 2) = (bf16_t)v;
+    layer(std::integral_constant<int, 1>{}, a.sc[0], a.sh[0], [&](int c, int y, int x, int n, i32x2 v) {
+        *reinterpret_cast<i32x2*>(lds + c * CLB + IMG2 + (y * P2 + x + 1) * S + n * 2) = v;
     }, [&] { pre = prefetch(std::integral_constant<int, 2>{}); });
-    layer(std::integral_constant<int, 2>{}, a.sc[1], a.sh[1], [&](int y, int x, int n, float v) {
-        *reinterpret_cast<bf16_t*>(lds + IMG3 + ((y + 1) * P3 + x + 1) * S + n * 2) = (bf16_t)v;
+    // d_deconv1's input is dead: restore the zero border of d_deconv3's image it overlapped
+    if (tid < NC * NBZ * 16) {
+        const int c = tid >= NBZ * 16, r = tid - NBZ * 16 * c;
+        st16(c * CLB + IMG3 + border_px(r >> 4) * S + (r & 15) * 16, (i32x4){0, 0, 0, 0});
+    }
+    layer(std::integral_constant<int, 2>{}, a.sc[1], a.sh[1], [&](int c, int y, int x, int n, i32x2 v) {
+        *reinterpret_cast<i32x2*>(lds + c * CLB + IMG3 + ((y + 1) * P3 + x + 1) * S + n * 2) = v;
     }, [&] { pre = prefetch(std::integral_constant<int, 3>{}); });
-    bf16_t* const outc = a.out + (long long)clip * a.out_clip_stride;
-    layer(std::integral_constant<int, 3>{}, a.sc[2], a.sh[2], [&](int y, int x, int n, float v) {
-        outc[(y * 10 + x) * 128 + n] = (bf16_t)v;
+    // d_deconv3: wave clip mh -> HBM [clip][40][10][128]; a missing last clip of the grid stores nothing
+    const __amdgpu_buffer_rsrc_t ors =
+        make_rsrc(a.out + (long long)(clip0 + mh) * a.out_clip_stride, clip0 + mh < a.N ? 400 * 128 * 2 : 0);
+    layer(std::integral_constant<int, 3>{}, a.sc[2], a.sh[2], [&](int, int y, int x, int n, i32x2 v) {
+        __builtin_amdgcn_raw_buffer_store_b64(v, ors, ((y * 10 + x) * 128 + n) * 2, 0, 0);
     }, [] {});
 }
 
@@ -209,10 +264,10 @@ bool dec_head_supported(const DecHeadArgs& a) {
 int launch_dec_head(const DecHeadArgs& a, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
-        AVSE_HIP_CHECK(hipFuncSetAttribute((const void*)k_dec_head, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
+        AVSE_HIP_CHECK(hipFuncSetAttribute((const void*)k_dec_head<0>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
         attr = true;
     }
-    hipLaunchKernelGGL(k_dec_head, dim3(a.N), dim3(NT), LDS_BYTES, s, a);
+    hipLaunchKernelGGL(k_dec_head<0>, dim3((a.N + NC - 1) / NC), dim3(NT), LDS_BYTES, s, a);
     AVSE_HIP_CHECK(hipGetLastError());
     return 0;
 }
