@@ -30,8 +30,11 @@
 //   * the d_deconv4 result (BN, LeakyReLU, rounded to bf16 exactly like the layer-by-layer path) is written
 //     into a zero-padded 42 x 14 image over the dead windows, which d_deconv5 reads for its four stride
 //     phases (sub-pixel decomposition as in k_conv: only the taps that hit a phase);
+//   * the MFMAs compute D = W x A (channels x pixels), so a lane's 4 accumulator rows are 4 consecutive channels of
+//     one pixel: d_deconv4's epilogue stores 8 B per lane and fragment (it was 4 x 4 two-byte LDS stores);
 //   * d_deconv5's epilogue folds BN, LeakyReLU, the bf16 rounding of its output and d_deconv6's 64 -> 1
-//     dot + bias, reduced over the 16 lanes of a DPP row; one float per output pixel is stored.
+//     dot + bias: 16 channels in-lane, then the four lane rows by three permlane swaps for four fragment slots;
+//     one float per output pixel is stored.
 #include <cstdlib>
 #include <utility>
 
@@ -53,7 +56,9 @@ constexpr int WBUF = NPIX4 * S4;                                  // 57,792
 // d_deconv5 phase p = 2 py + px: taps (py - a, px - b), a < 2 + py, b < 2 + px; image pixel (y + dy + 1, x + dx + 1)
 constexpr int P5 = 14, ROWS5 = 42, S5 = 160, OIMG = ROWS5 * P5 * S5;   // 94,080 B over the windows
 constexpr int BOFF = 2 * WBUF;                                        // weight slab ring: 2 groups x 4 slabs x 4 KB
-constexpr int LDS_BYTES = BOFF + 2 * 4 * 4096;                        // 148,352
+constexpr int PAR = BOFF + 2 * 4 * 4096;                              // folded BN / d_deconv6 parameters (f32):
+constexpr int PSC4 = PAR, PSH4 = PAR + 256, PSC5 = PAR + 512, PSH5 = PAR + 768, PW6 = PAR + 1024;   // 64 each
+constexpr int LDS_BYTES = PAR + 1280;                                 // 149,632
 static_assert(OIMG <= BOFF, "d_deconv5 image must fit over the d_deconv4 windows");
 
 constexpr int ph_ny(int p) { return 2 + (p >> 1); }
@@ -69,12 +74,18 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, lo
 }
 __device__ __forceinline__ int wsw(int row) { return 2 * ((row >> 2) & 1); }   // weight-slab slot swizzle
 __device__ __forceinline__ i32x4 lds16(const char* base, int off) { return *reinterpret_cast<const i32x4*>(base + off); }
-__device__ __forceinline__ float dpp_row_sum(float v) {   // sum over the 16 lanes of a DPP row (row_ror 8, 4, 2, 1)
-    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x128, 0xf, 0xf, false));
-    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x124, 0xf, 0xf, false));
-    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x122, 0xf, 0xf, false));
-    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x121, 0xf, 0xf, false));
-    return v;
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float bn_lrelu(float acc, float sc, float sh) {
+    const float v = fmaf(acc, sc, sh);
+    float r;
+    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(v), "v"(LRELU * v));   // LeakyReLU, no canonicalise
+    return r;
+}
+__device__ __forceinline__ auto pack4(float a, float b, float c, float d) {   // 4 bf16 (RNE, as (bf16_t) casts)
+    typedef int i32x2 __attribute__((ext_vector_type(2)));
+    const bf16x2 lo = __builtin_convertvector((f32x2){a, b}, bf16x2), hi = __builtin_convertvector((f32x2){c, d}, bf16x2);
+    return (i32x2){__builtin_bit_cast(int, lo), __builtin_bit_cast(int, hi)};
 }
 template <int... I, typename F>
 __device__ __forceinline__ void unroll(std::integer_sequence<int, I...>, F&& f) {
@@ -125,8 +136,8 @@ __global__ __launch_bounds__(NT, 1) void k_dec_tail(DecTailArgs a) {
         for (int i = 0; i < NF; ++i)
 #pragma unroll
             for (int j = 0; j < 4; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fa[i]),
-                                                                     __builtin_bit_cast(bf16x8, fb[j]), acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fb[j]),   // W x A
+                                                                     __builtin_bit_cast(bf16x8, fa[i]), acc[i][j], 0, 0, 0);
     };
 
     // =============================== d_deconv4 ===============================
@@ -153,12 +164,15 @@ __global__ __launch_bounds__(NT, 1) void k_dec_tail(DecTailArgs a) {
             constexpr int t = decltype(tt)::value;
             return __builtin_amdgcn_raw_buffer_load_b64(rsW, vbl + t * 256, csoff, 0);
         };
-        float sc[4], sh[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            sc[j] = a.sc4[16 * j + r16];
-            sh[j] = a.sh4[16 * j + r16];
+        // epilogue parameters -> LDS (read per fragment in the epilogues: no registers held across the loops)
+        if (tid < 64) {
+            reinterpret_cast<float*>(lds + PSC4)[tid] = a.sc4[tid];
+            reinterpret_cast<float*>(lds + PSH4)[tid] = a.sh4[tid];
+            reinterpret_cast<float*>(lds + PSC5)[tid] = a.sc5[tid];
+            reinterpret_cast<float*>(lds + PSH5)[tid] = a.sh5[tid];
+            reinterpret_cast<float*>(lds + PW6)[tid] = a.w6[tid];
         }
+        auto par4 = [&](int base, int j) { return *reinterpret_cast<const f32x4*>(lds + base + (16 * j + 4 * kg) * 4); };
 
         // prologue: window chunk 0 -> buffer 0; weight slabs 0, 1, 2 in flight
         {
@@ -231,35 +245,26 @@ __global__ __launch_bounds__(NT, 1) void k_dec_tail(DecTailArgs a) {
         // zero the d_deconv5 image (its padding ring reads as zero)
         for (int o = tid * 16; o < OIMG; o += NT * 16) *reinterpret_cast<i32x4*>(lds + o) = (i32x4){0, 0, 0, 0};
         __syncthreads();
-        // epilogue: BN + LeakyReLU -> bf16 at image pixel (y + 1, x + 1); lane holds block rows 4 kg + e
+        // epilogue: BN + LeakyReLU -> bf16 at image pixel (y + 1, x + 1); lane = block row r16, channels
+        // 16 j + 4 kg .. + 3: one 8-B store per fragment pair (i, j)
 #pragma unroll
         for (int i = 0; i < NF; ++i) {
             const int f = w + NW * i;
             if (f >= NFRAG) continue;
+            const int y = 8 * (f / 5) + (r16 >> 1), x = 2 * (f % 5) + (r16 & 1);
+            const int px = ((y + 1) * P5 + x + 1) * S5 + 8 * kg;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int r = 4 * kg + e;
-                const int y = 8 * (f / 5) + (r >> 1), x = 2 * (f % 5) + (r & 1);
-                char* const px = lds + ((y + 1) * P5 + x + 1) * S5 + r16 * 2;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    float v = acc[i][j][e] * sc[j] + sh[j];
-                    v = v >= 0.f ? v : LRELU * v;
-                    *reinterpret_cast<bf16_t*>(px + 32 * j) = (bf16_t)v;
-                }
+            for (int j = 0; j < 4; ++j) {   // channels 16 j + 4 kg + e
+                const f32x4 v = acc[i][j], sc = par4(PSC4, j), sh = par4(PSH4, j);
+                st8(px + 32 * j, pack4(bn_lrelu(v[0], sc[0], sh[0]), bn_lrelu(v[1], sc[1], sh[1]),
+                                       bn_lrelu(v[2], sc[2], sh[2]), bn_lrelu(v[3], sc[3], sh[3])));
             }
         }
         __syncthreads();
     }
 
     // =============================== d_deconv5 + d_deconv6 ===============================
-    float sc5[4], sh5[4], w6[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        sc5[j] = a.sc5[16 * j + r16];
-        sh5[j] = a.sh5[16 * j + r16];
-        w6[j] = a.w6[16 * j + r16];
-    }
+    auto par5 = [&](int base, int j) { return *reinterpret_cast<const f32x4*>(lds + base + (16 * j + 4 * kg) * 4); };
     float* const outc = a.out + (long long)clip * (4 * HW);
     const __amdgpu_buffer_rsrc_t rsW5 = make_rsrc(a.w5, (long long)ph_woff(4) * 2);
     // the padded slab sequence over the four phases (phase p: 2 nt slabs, slab = 2 tap + chunk, padded to a multiple
@@ -284,34 +289,30 @@ __global__ __launch_bounds__(NT, 1) void k_dec_tail(DecTailArgs a) {
     };
     auto epilogue5 = [&](auto pp) {
         constexpr int p = decltype(pp)::value, py = p >> 1, px = p & 1;
-        float part[NF][4];
+        // d_deconv6 partial dot of this lane's 16 channels (16 j + 4 kg + e) for block row r16 of each slot
+        float part[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int i = 0; i < NF; ++i)
+        for (int j = 0; j < 4; ++j) {   // channels 16 j + 4 kg + e
+            const f32x4 sc = par5(PSC5, j), sh = par5(PSH5, j), w6 = par5(PW6, j);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                float sum = 0.f;
+            for (int i = 0; i < 4; ++i)
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    float v = acc[i][j][e] * sc5[j] + sh5[j];
-                    v = v >= 0.f ? v : LRELU * v;
-                    sum = fmaf((float)(bf16_t)v, w6[j], sum);   // y rounded to bf16 as the unfused path stores it
-                }
-                part[i][e] = dpp_row_sum(sum);
-            }
-        // lane r16 stores the sum of (slot 4 h + r16 / 4, block row 4 kg + r16 % 4)
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            float mine = 0.f;
-#pragma unroll
-            for (int i = 4 * h; i < 4 * h + 4 && i < NF; ++i)
-#pragma unroll
-                for (int e = 0; e < 4; ++e) mine = (r16 == 4 * (i - 4 * h) + e) ? part[i][e] : mine;
-            const int i = 4 * h + (r16 >> 2), f = w + NW * i;
-            if (i < NF && f < NFRAG) {
-                const int r = 4 * kg + (r16 & 3);
-                const int y = 8 * (f / 5) + (r >> 1), x = 2 * (f % 5) + (r & 1);
-                outc[(2 * y + py) * (2 * W) + 2 * x + px] = mine + a.b6;
-            }
+                for (int e = 0; e < 4; ++e)   // y rounded to bf16 as the unfused path stores it
+                    part[i] = fmaf((float)(bf16_t)bn_lrelu(acc[i < NF ? i : 0][j][e], sc[e], sh[e]), w6[e], part[i]);
+        }
+        // sum over the four lane rows (kg) of a slot, three swaps for four slots: lanes 0-31 <-> 32-63 pairs slots
+        // (0, 1) and (2, 3), then rows 0 / 2 <-> 1 / 3: lane row kg ends with the total of slot {0, 2, 1, 3}[kg]
+        auto swap_add = [](float x, float y, auto sw) {
+            const auto r = sw(__builtin_bit_cast(unsigned, x), __builtin_bit_cast(unsigned, y));
+            return __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
+        };
+        auto sw32 = [](unsigned x, unsigned y) { return __builtin_amdgcn_permlane32_swap(x, y, false, false); };
+        auto sw16 = [](unsigned x, unsigned y) { return __builtin_amdgcn_permlane16_swap(x, y, false, false); };
+        const float tot = swap_add(swap_add(part[0], part[1], sw32), swap_add(part[2], part[3], sw32), sw16);
+        const int i = ((kg & 1) << 1) | (kg >> 1), f = w + NW * i;
+        if (i < NF && f < NFRAG) {
+            const int y = 8 * (f / 5) + (r16 >> 1), x = 2 * (f % 5) + (r16 & 1);
+            outc[(2 * y + py) * (2 * W) + 2 * x + px] = tot + a.b6;
         }
     };
 

@@ -255,10 +255,6 @@ __global__ __launch_bounds__(512, 1) void k_conv_v1r(HaloArgs a) {
     barrier_raw();   // B_-1
 
     f32x4 acc[4][8];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[i][j] = (f32x4){};
     // pool: the 4 accumulator rows of a lane are one 2x2 window (raw maxima: scale >= 0 after the host sign
     // fold, so BN commutes); inline asm keeps the compiler from canonicalising the operands (2 instead of 4
     // instructions per window).  The loader waves apply BN / LeakyReLU and store (out_pass).
@@ -275,24 +271,22 @@ __global__ __launch_bounds__(512, 1) void k_conv_v1r(HaloArgs a) {
         for (int i = 0; i < 4; ++i)
 #pragma unroll
             for (int j = 0; j < 8; ++j) *reinterpret_cast<float*>(sb + 2 * i * SPITCH + 64 * j) = max4(acc[i][j]);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) acc[i][j] *= 0.f;   // restart the chains in place (see conv_stream.hip)
     };
-    auto mfmas = [&](const i32x4 (&ca)[4], const i32x4 (&cb)[8]) {
+    // the first K-slice of a tile starts its chains from a zero C operand (no restart instructions in the epilogue)
+    auto mfmas = [&](const i32x4 (&ca)[4], const i32x4 (&cb)[8], bool first) {
         if constexpr ((ABL & 4) != 0) return;
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
             for (int j = 0; j < 8; ++j)
                 acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ca[i]),
-                                                                     __builtin_bit_cast(bf16x8, cb[j]), acc[i][j], 0, 0, 0);
+                                                                     __builtin_bit_cast(bf16x8, cb[j]),
+                                                                     first ? (f32x4){0.f, 0.f, 0.f, 0.f} : acc[i][j], 0, 0, 0);
     };
     // slice s: MFMAs on (ca, cb) interleaved with the fragment reads of slice s+1 into (xa, xb)
-    auto slice = [&](int hs, int ky_next, i32x4 (&ca)[4], i32x4 (&cb)[8], i32x4 (&xa)[4], i32x4 (&xb)[8]) {
+    auto slice = [&](int hs, int ky_next, i32x4 (&ca)[4], i32x4 (&cb)[8], i32x4 (&xa)[4], i32x4 (&xb)[8], bool first) {
         frags(hs, ky_next, xa, xb);
-        mfmas(ca, cb);
+        mfmas(ca, cb, first);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
@@ -305,13 +299,13 @@ __global__ __launch_bounds__(512, 1) void k_conv_v1r(HaloArgs a) {
     // one tile: slice 0 in (xa, xb); tile k+1's slice 0 lands in (ya, yb) (parity flips per tile)
     auto tile = [&](int k, i32x4 (&xa)[4], i32x4 (&xb)[8], i32x4 (&ya)[4], i32x4 (&yb)[8]) {
         const int hs = k % NWS, hn = (k + 1) % NWS;
-        slice(hs, 1, xa, xb, ya, yb);
-        slice(hs, 2, ya, yb, xa, xb);
-        slice(hs, 3, xa, xb, ya, yb);
-        slice(hs, 4, ya, yb, xa, xb);
+        slice(hs, 1, xa, xb, ya, yb, true);
+        slice(hs, 2, ya, yb, xa, xb, false);
+        slice(hs, 3, xa, xb, ya, yb, false);
+        slice(hs, 4, ya, yb, xa, xb, false);
         // slice 4, with tile k+1's first fragments (window k+1 was stored before B_{k-1}; past the last tile
         // the read hits a stale slot and is never used)
-        slice(hn, 0, xa, xb, ya, yb);
+        slice(hn, 0, xa, xb, ya, yb, false);
         epilogue(k);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if constexpr (!(ABL & 8)) barrier_raw();   // B_k: staging k is written; window k is no longer read
