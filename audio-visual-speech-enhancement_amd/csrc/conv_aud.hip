@@ -37,11 +37,14 @@ constexpr int P3 = 14, S3 = 160, IMG3B = 42 * P3 * S3;                // 94,080
 constexpr int P4 = 6, S4 = 288, IMG4B = 20 * P4 * S4;                 // 34,560
 constexpr int IMG5 = 40960, IMG5B = 10 * P4 * S4;                     // 17,280
 constexpr int BOFF = 2 * W2BUF;                                       // weight ring (2 x 16 KB); a_conv1's im2col
-constexpr int LDS_BYTES = BOFF + 2 * 16384;                           // 148,352
+constexpr int PAR = BOFF + 2 * 16384;                                 // folded bias / BN of the five layers (f32)
+constexpr int PSC[5] = {PAR, PAR + 512, PAR + 1024, PAR + 2048, PAR + 3072};   // scale of layer l; shift at + 4 * Cout
+constexpr int LDS_BYTES = PAR + 4096;                                 // 152,448
+constexpr int DA = 6;                                                 // a_conv3..5 weight pieces in flight (registers)
 static_assert(IMG3B <= BOFF && IMG4B <= IMG5 && IMG5 + IMG5B <= BOFF && 400 * 64 <= 32768, "LDS map");
 
 typedef int i32x2 __attribute__((ext_vector_type(2)));
-struct Pre { i32x4 w0, w1, p0, p1; };   // a layer's first four weight slabs (see prefetch)
+struct Pre { i32x4 w[DA + 2]; };   // a layer's first DA + 2 weight pieces (see prefetch)
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, long long bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
@@ -53,8 +56,19 @@ __device__ __forceinline__ void unroll(std::integer_sequence<int, I...>, F&& f) 
     (f(std::integral_constant<int, I>{}), ...);
 }
 __device__ __forceinline__ float bn_lrelu(float acc, float sc, float sh) {
-    const float v = acc * sc + sh;
-    return v >= 0.f ? v : LRELU * v;
+    const float v = fmaf(acc, sc, sh);
+    float r;
+    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(v), "v"(LRELU * v));   // LeakyReLU, no canonicalise
+    return r;
+}
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+// BN + LeakyReLU of an accumulator quad (4 consecutive channels) -> 4 bf16 (RNE, as (bf16_t) casts)
+__device__ __forceinline__ i32x2 bn_pack4(f32x4 v, f32x4 sc, f32x4 sh) {
+    const float a = bn_lrelu(v[0], sc[0], sh[0]), b = bn_lrelu(v[1], sc[1], sh[1]);
+    const float c = bn_lrelu(v[2], sc[2], sh[2]), d = bn_lrelu(v[3], sc[3], sh[3]);
+    const bf16x2 lo = __builtin_convertvector((f32x2){a, b}, bf16x2), hi = __builtin_convertvector((f32x2){c, d}, bf16x2);
+    return (i32x2){__builtin_bit_cast(int, lo), __builtin_bit_cast(int, hi)};
 }
 __device__ __forceinline__ f32x4 mfma(i32x4 a, i32x4 b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
@@ -71,19 +85,23 @@ __global__ __launch_bounds__(NT, 1) void k_aud_enc(AudEncArgs a) {
         for (int o = from + tid * 16; o < to; o += NT * 16) st16(o, (i32x4){0, 0, 0, 0});
     };
 
-    // every layer's folded bias / BN for this lane's output channels, loaded up front (in the epilogues each load
-    // exposed a global-load latency per layer)
+    // every layer's folded bias / BN -> LDS (read as f32x4 quads in the epilogues: lanes of a row group kg share
+    // an address, so the reads broadcast)
     const int mh = w >> 2, nq = w & 3;   // a_conv3: fragments 4 mh .. 4 mh + 3, channels 32 nq .. 32 nq + 31
-    float sc1[4], sh1[4], sc2[4], sh2[4], sc3[2], sh3[2];
+    {
+        constexpr int co[5] = {64, 64, 128, 128, 128};
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        sc1[j] = a.sc[0][16 * j + r16]; sh1[j] = a.sh[0][16 * j + r16];
-        sc2[j] = a.sc[1][16 * j + r16]; sh2[j] = a.sh[1][16 * j + r16];
+        for (int l = 0; l < 5; ++l)
+            if (tid < 2 * co[l])
+                reinterpret_cast<float*>(lds + PSC[l])[tid] = tid < co[l] ? a.sc[l][tid] : a.sh[l][tid - co[l]];
     }
-#pragma unroll
-    for (int j = 0; j < 2; ++j) { sc3[j] = a.sc[2][32 * nq + 16 * j + r16]; sh3[j] = a.sh[2][32 * nq + 16 * j + r16]; }
-    const float sc4 = a.sc[3][16 * w + r16], sh4 = a.sh[3][16 * w + r16];
-    const float sc5 = a.sc[4][16 * w + r16], sh5 = a.sh[4][16 * w + r16];
+    // scale / shift quad of layer l for channels n .. n + 3
+    auto bnq = [&](int l, int n, f32x4& sc, f32x4& sh) {
+        constexpr int co[5] = {64, 64, 128, 128, 128};
+        sc = *reinterpret_cast<const f32x4*>(lds + PSC[l] + n * 4);
+        sh = *reinterpret_cast<const f32x4*>(lds + PSC[l] + (co[l] + n) * 4);
+    };
+    auto st8l = [&](int addr, i32x2 v) { *reinterpret_cast<i32x2*>(lds + addr) = v; };
 
     // ================= a_conv1: im2col of the mel input (k = ky * 5 + kx, 25 of 32) =================
     zero(0, BOFF);   // a_conv2's input image: its padding ring reads as zero
@@ -121,21 +139,21 @@ __global__ __launch_bounds__(NT, 1) void k_aud_enc(AudEncArgs a) {
             const int f = (w + 8 * i < 25) ? w + 8 * i : 0;
             const i32x4 fa = lds16(lds, BOFF + (16 * f + r16) * 64 + kg * 16);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) acc[i][j] = mfma(fa, fb[j], (f32x4){0.f, 0.f, 0.f, 0.f});
+            for (int j = 0; j < 4; ++j) acc[i][j] = mfma(fb[j], fa, (f32x4){0.f, 0.f, 0.f, 0.f});   // W x A
         }
-        const float (&sc)[4] = sc1, (&sh)[4] = sh1;
-        // -> a_conv2's input: chunk (n / 32) buffer, padded pixel (oy + 1, ox + 1)
+        // -> a_conv2's input: chunk (n / 32) buffer, padded pixel (oy + 1, ox + 1); lane = pixel row r16,
+        // channels 16 j + 4 kg .. + 3
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int f = w + 8 * i;
             if (f >= 25) continue;
+            const int m = 16 * f + r16, oy = m / 10, ox = m - oy * 10;
+            const int px = ((oy + 1) * P2 + ox + 1) * S2 + kg * 8;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int m = 16 * f + 4 * kg + e, oy = m / 10, ox = m - oy * 10;
-                char* const px = lds + ((oy + 1) * P2 + ox + 1) * S2 + r16 * 2;
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    *reinterpret_cast<bf16_t*>(px + (j >> 1) * W2BUF + (j & 1) * 32) = (bf16_t)bn_lrelu(acc[i][j][e], sc[j], sh[j]);
+            for (int j = 0; j < 4; ++j) {
+                f32x4 sc, sh;
+                bnq(0, 16 * j + 4 * kg, sc, sh);
+                st8l(px + (j >> 1) * W2BUF + (j & 1) * 32, bn_pack4(acc[i][j], sc, sh));
             }
         }
     }
@@ -150,18 +168,22 @@ __global__ __launch_bounds__(NT, 1) void k_aud_enc(AudEncArgs a) {
     auto run = [&](auto nss, const __amdgpu_buffer_rsrc_t& rsW, int vbl, auto bsoff, const Pre& pre, auto read_a,
                    auto read_b, auto mm) {
         constexpr int NS = decltype(nss)::value;
-        i32x4 pb[2] = {pre.p0, pre.p1};
-        st16b(bst3, pre.w0);
-        st16b(bst3 + 8192, pre.w1);
+        i32x4 pb[DA];   // pb[S % DA] holds slab S + 2 at step S
+#pragma unroll
+        for (int k = 0; k < DA; ++k) pb[k] = pre.w[k + 2];
+        st16b(bst3, pre.w[0]);
+        st16b(bst3 + 8192, pre.w[1]);
         __syncthreads();
         read_a(std::integral_constant<int, 0>{}, 0);
         read_b(std::integral_constant<int, 0>{}, 0);
         unroll(std::make_integer_sequence<int, NS>{}, [&](auto ss) {
             constexpr int S = decltype(ss)::value;
             __builtin_amdgcn_sched_barrier(0);
-            st16b(bst3 + (((S / 2) + 1) & 1) * 16384 + (S % 2) * 8192, pb[S & 1]);   // slab S + 2
-            constexpr int SL = S + 4 < NS ? S + 4 : 0;                               // slab S + 4 (past the end: unused)
-            pb[S & 1] = __builtin_amdgcn_raw_buffer_load_b128(rsW, vbl + bsoff(std::integral_constant<int, SL>{}), 0, 0);
+            if constexpr (S + 2 < NS) {
+                st16b(bst3 + (((S / 2) + 1) & 1) * 16384 + (S % 2) * 8192, pb[S % DA]);   // slab S + 2
+                if constexpr (S + 2 + DA < NS)
+                    pb[S % DA] = __builtin_amdgcn_raw_buffer_load_b128(rsW, vbl + bsoff(std::integral_constant<int, S + 2 + DA>{}), 0, 0);
+            }
             if constexpr (S % 2 == 1) __syncthreads();
             if constexpr (S + 1 < NS) {
                 read_a(std::integral_constant<int, S + 1>{}, (S + 1) & 1);
@@ -171,13 +193,12 @@ __global__ __launch_bounds__(NT, 1) void k_aud_enc(AudEncArgs a) {
             mm(S & 1);
         });
     };
-    // a layer's first four weight slabs (two to the ring, two in flight), issued before the previous layer's epilogue
+    // a layer's first DA + 2 weight slabs (two to the ring, DA in flight), issued before the previous layer's epilogue
     auto prefetch = [&](const __amdgpu_buffer_rsrc_t& rsW, int vbl, auto bsoff) {
         Pre p;
-        p.w0 = __builtin_amdgcn_raw_buffer_load_b128(rsW, vbl + bsoff(std::integral_constant<int, 0>{}), 0, 0);
-        p.w1 = __builtin_amdgcn_raw_buffer_load_b128(rsW, vbl + bsoff(std::integral_constant<int, 1>{}), 0, 0);
-        p.p0 = __builtin_amdgcn_raw_buffer_load_b128(rsW, vbl + bsoff(std::integral_constant<int, 2>{}), 0, 0);
-        p.p1 = __builtin_amdgcn_raw_buffer_load_b128(rsW, vbl + bsoff(std::integral_constant<int, 3>{}), 0, 0);
+        unroll(std::make_integer_sequence<int, DA + 2>{}, [&](auto k) {
+            p.w[decltype(k)::value] = __builtin_amdgcn_raw_buffer_load_b128(rsW, vbl + bsoff(k), 0, 0);
+        });
         return p;
     };
     const __amdgpu_buffer_rsrc_t rsW3 = make_rsrc(a.w3, 128 * 1024 * 2), rsW4 = make_rsrc(a.w4, 128 * 512 * 2),
@@ -265,26 +286,25 @@ __global__ __launch_bounds__(NT, 1) void k_aud_enc(AudEncArgs a) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) acc[i][j] = mfma(fa[t & 1][i], fb[t & 1][j], acc[i][j]);
+                    for (int j = 0; j < 4; ++j) acc[i][j] = mfma(fb[t & 1][j], fa[t & 1][i], acc[i][j]);   // W x A
             });
         }
-        const float (&sc)[4] = sc2, (&sh)[4] = sh2;
         __syncthreads();   // every read of a_conv2's input done: a_conv3's image goes over it
         pre3 = prefetch(rsW3, vbl3, bsoff3);   // a_conv3's first slabs load under this epilogue
         zero(0, IMG3B);
         __syncthreads();
-        // -> a_conv3's input, padded pixel (oy + 1, ox + 1), 8 x 2 fragment rows
+        // -> a_conv3's input, padded pixel (oy + 1, ox + 1), 8 x 2 fragment rows; lane = fragment row r16
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int f = w + 8 * i;
             if (f >= 25) continue;
+            const int y = 8 * (f / 5) + (r16 >> 1), x = 2 * (f % 5) + (r16 & 1);
+            const int px = ((y + 1) * P3 + x + 1) * S3 + kg * 8;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int r = 4 * kg + e;
-                const int y = 8 * (f / 5) + (r >> 1), x = 2 * (f % 5) + (r & 1);
-                char* const px = lds + ((y + 1) * P3 + x + 1) * S3 + r16 * 2;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) *reinterpret_cast<bf16_t*>(px + 32 * j) = (bf16_t)bn_lrelu(acc[i][j][e], sc[j], sh[j]);
+            for (int j = 0; j < 4; ++j) {
+                f32x4 sc, sh;
+                bnq(1, 16 * j + 4 * kg, sc, sh);
+                st8l(px + 32 * j, bn_pack4(acc[i][j], sc, sh));
             }
         }
         __syncthreads();
@@ -315,29 +335,30 @@ __global__ __launch_bounds__(NT, 1) void k_aud_enc(AudEncArgs a) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
 #pragma unroll
-                    for (int j = 0; j < 2; ++j) acc[i][j] = mfma(fa[buf][i], fb[buf][j], acc[i][j]);
+                    for (int j = 0; j < 2; ++j) acc[i][j] = mfma(fb[buf][j], fa[buf][i], acc[i][j]);   // W x A
             });
-        const float (&sc)[2] = sc3, (&sh)[2] = sh3;
         __syncthreads();
         pre4 = prefetch(rsW4, vbl34 / 2, bsoff45);   // a_conv4's first slabs load under this epilogue
         zero(0, IMG4B);   // a_conv4's input: column 5 reads as zero
         __syncthreads();
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 4; ++i) {
+            const int m = 16 * (4 * mh + i) + r16;
+            if (m >= 100) continue;
+            const int oy = m / 5, ox = m - oy * 5;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int m = 16 * (4 * mh + i) + 4 * kg + e;
-                if (m >= 100) continue;
-                const int oy = m / 5, ox = m - oy * 5;
-#pragma unroll
-                for (int j = 0; j < 2; ++j)
-                    *reinterpret_cast<bf16_t*>(lds + (oy * P4 + ox) * S4 + (32 * nq + 16 * j + r16) * 2) = (bf16_t)bn_lrelu(acc[i][j][e], sc[j], sh[j]);
+            for (int j = 0; j < 2; ++j) {
+                const int n = 32 * nq + 16 * j + 4 * kg;
+                f32x4 sc, sh;
+                bnq(2, n, sc, sh);
+                st8l((oy * P4 + ox) * S4 + n * 2, bn_pack4(acc[i][j], sc, sh));
             }
+        }
         __syncthreads();
     }
 
     // ---- a_conv4 / a_conv5: 2x2 stride (2, 1), 128 -> 128; slab = chunk * 4 + tap; wave w: channels 16 w .. 16 w + 15 ----
-    auto small = [&](auto nff, int img, const __amdgpu_buffer_rsrc_t& rsW, const Pre& pre, float sc, float sh, auto store,
+    auto small = [&](auto nff, int img, const __amdgpu_buffer_rsrc_t& rsW, const Pre& pre, int layer, auto store,
                      auto next) {
         constexpr int NFR = decltype(nff)::value;   // M fragments (4: 50 rows, 2: 25 rows)
         constexpr int MR = NFR == 4 ? 50 : 25;
@@ -362,27 +383,27 @@ __global__ __launch_bounds__(NT, 1) void k_aud_enc(AudEncArgs a) {
             [&](auto ss, int buf) { b_read(16 * w, ss, 1, fb[buf]); },
             [&](int buf) {
 #pragma unroll
-                for (int i = 0; i < NFR; ++i) acc[i] = mfma(fa[buf][i], fb[buf][0], acc[i]);
+                for (int i = 0; i < NFR; ++i) acc[i] = mfma(fb[buf][0], fa[buf][i], acc[i]);   // W x A
             });
-        const int n = 16 * w + r16;
+        const int n = 16 * w + 4 * kg;   // lane channels n .. n + 3
         __syncthreads();
         next();   // the next layer's first weight slabs load under this epilogue
+        f32x4 sc, sh;
+        bnq(layer, n, sc, sh);
 #pragma unroll
-        for (int i = 0; i < NFR; ++i)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int m = 16 * i + 4 * kg + e;
-                if (m < MR) store(m / 5, m % 5, n, bn_lrelu(acc[i][e], sc, sh));
-            }
+        for (int i = 0; i < NFR; ++i) {
+            const int m = 16 * i + r16;
+            if (m < MR) store(m / 5, m % 5, n, bn_pack4(acc[i], sc, sh));
+        }
         __syncthreads();
     };
     zero(IMG5, IMG5 + IMG5B);   // a_conv5's input: column 5 reads as zero (ordered by the barriers in `small`)
-    small(std::integral_constant<int, 4>{}, 0, rsW4, pre4, sc4, sh4, [&](int oy, int ox, int n, float v) {
-        *reinterpret_cast<bf16_t*>(lds + IMG5 + (oy * P4 + ox) * S4 + n * 2) = (bf16_t)v;
+    small(std::integral_constant<int, 4>{}, 0, rsW4, pre4, 3, [&](int oy, int ox, int n, i32x2 v) {
+        st8l(IMG5 + (oy * P4 + ox) * S4 + n * 2, v);
     }, [&] { pre5 = prefetch(rsW5, vbl34 / 2, bsoff45); });
     bf16_t* const outc = a.out + (long long)clip * a.out_clip_stride;
-    small(std::integral_constant<int, 2>{}, IMG5, rsW5, pre5, sc5, sh5, [&](int oy, int ox, int n, float v) {
-        outc[(oy * 5 + ox) * 128 + n] = (bf16_t)v;   // Flatten (HWC) -> concat[0:3200]
+    small(std::integral_constant<int, 2>{}, IMG5, rsW5, pre5, 4, [&](int oy, int ox, int n, i32x2 v) {
+        *reinterpret_cast<i32x2*>(outc + (oy * 5 + ox) * 128 + n) = v;   // Flatten (HWC) -> concat[0:3200]
     }, [] {});
 }
 
