@@ -31,15 +31,19 @@ constexpr float LRELU = 0.3f;
 constexpr int NW = 8, NT = 64 * NW;
 // a_conv2 input: 2 chunk buffers, 43 rows x 14 pixels x 96 B; pixel (y + ky, x + kx) for output (y, x), tap (ky, kx)
 constexpr int P2 = 14, S2 = 96, W2BUF = 43 * P2 * S2;                 // 57,792
-// a_conv3 input: 42 x 14 x 160 B (64 channels + pad); pixel (2 y + ky, 2 x + kx)
-constexpr int P3 = 14, S3 = 160, IMG3B = 42 * P3 * S3;                // 94,080
-// a_conv4 / a_conv5 inputs: 20 (10) rows x 6 pixels x 288 B (128 channels + pad); pixel (2 y + ky, x + kx)
-constexpr int P4 = 6, S4 = 288, IMG4B = 20 * P4 * S4;                 // 34,560
-constexpr int IMG5 = 40960, IMG5B = 10 * P4 * S4;                     // 17,280
+// a_conv3 input: 42 x 13 x 144 B (64 channels + pad); pixel (2 y + ky, 2 x + kx).  a_conv3..a_conv5 gather their
+// 16-pixel M fragments from a 5-wide grid (stride 2 rows / columns): the pixel and row pitches are the ones with the
+// fewest ds_read_b128 bank conflicts over every tap (searched exhaustively, 16-lane groups of 16-B units; a_conv3
+// 2.9-way at 160 B x 14 -> 1.1-way at 144 B x 13, a_conv4 2.8 -> 1.8-way at 7 pixels per row)
+constexpr int P3 = 13, S3 = 144, IMG3B = 42 * P3 * S3;                // 78,624
+// a_conv4 / a_conv5 inputs: 20 (10) rows x 7 pixels x 288 B (128 channels + pad); pixel (2 y + ky, x + kx)
+constexpr int P4 = 7, S4 = 288, IMG4B = 20 * P4 * S4;                 // 40,320
+constexpr int IMG5 = 40960, IMG5B = 10 * P4 * S4;                     // 20,160
 constexpr int BOFF = 2 * W2BUF;                                       // weight ring (2 x 16 KB); a_conv1's im2col
 constexpr int PAR = BOFF + 2 * 16384;                                 // folded bias / BN of the five layers (f32)
 constexpr int PSC[5] = {PAR, PAR + 512, PAR + 1024, PAR + 2048, PAR + 3072};   // scale of layer l; shift at + 4 * Cout
-constexpr int LDS_BYTES = PAR + 4096;                                 // 152,448
+constexpr int MEL = PAR + 4096, MP = 24;                              // a_conv1 input: zero-padded 83 x 24 bf16
+constexpr int LDS_BYTES = MEL + 83 * MP * 2;                          // 156,432
 constexpr int DA = 6;                                                 // a_conv3..5 weight pieces in flight (registers)
 static_assert(IMG3B <= BOFF && IMG4B <= IMG5 && IMG5 + IMG5B <= BOFF && 400 * 64 <= 32768, "LDS map");
 
@@ -74,7 +78,15 @@ __device__ __forceinline__ f32x4 mfma(i32x4 a, i32x4 b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
 }
 
+// STAMP (tools/aud_stamp.hip only; 0 in the library): thread 0 records s_memtime at the phase boundaries into
+// g_stamps[block][k] (k = 0 start, 1 im2col, 2 a_conv1, 3 a_conv2 prologue, 4 a_conv2 loop, 5 its epilogue, 6 a_conv3
+// loop, 7 its epilogue, 8 a_conv4, 9 a_conv5; 10 / 11 the end of the a_conv4 / a_conv5 slab loops)
+__device__ unsigned long long* g_stamps;
+template <int STAMP = 0>
 __global__ __launch_bounds__(NT, 1) void k_aud_enc(AudEncArgs a) {
+#define STAMP_AT(k) \
+    do { if constexpr (STAMP != 0) { if (threadIdx.x == 0) g_stamps[blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memtime(); } } while (0)
+    STAMP_AT(0);
     extern __shared__ __attribute__((aligned(1024))) char lds[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -103,43 +115,45 @@ __global__ __launch_bounds__(NT, 1) void k_aud_enc(AudEncArgs a) {
     };
     auto st8l = [&](int addr, i32x2 v) { *reinterpret_cast<i32x2*>(lds + addr) = v; };
 
-    // ================= a_conv1: im2col of the mel input (k = ky * 5 + kx, 25 of 32) =================
+    // ================= a_conv1: 5x5 stride 2 on the single mel channel =================
+    // weights (global) first; the mel clip -> a zero-padded 83 x 24 bf16 image in LDS (TF 'SAME': 1 row / column
+    // before, 2 after); each lane gathers its A fragment rows (k = ky * 5 + kx, 25 of 32) straight from the image
+    // (the first version built a 400 x 32 im2col tile with 32 scalar global loads per lane: 11K cycles)
+    i32x4 fb1[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) fb1[j] = *reinterpret_cast<const i32x4*>(reinterpret_cast<const char*>(a.w1) + ((16 * j + r16) * 32 + kg * 8) * 2);
+    const f32x4 mv = tid < 400 ? *reinterpret_cast<const f32x4*>(a.mel + (long long)clip * 1600 + 4 * tid) : (f32x4){};
     zero(0, BOFF);   // a_conv2's input image: its padding ring reads as zero
-    {
-        const float* mel = a.mel + (long long)clip * 1600;
+    zero(MEL, MEL + 83 * MP * 2);
+    __syncthreads();
+    if (tid < 400) {
+        const int iy = tid / 5, ix = 4 * (tid - 5 * iy);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int u = tid + NT * k;   // (row m, 8-tap group)
-            if (u < 1600) {
-                const int m = u >> 2, g = u & 3, oy = m / 10, ox = m - oy * 10;
-                unsigned short v[8];
-#pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    const int tap = 8 * g + e, ky = tap / 5, kx = tap - ky * 5;
-                    const int iy = 2 * oy + ky - 1, ix = 2 * ox + kx - 1;
-                    const float f = (tap < 25 && iy >= 0 && iy < 80 && ix >= 0 && ix < 20) ? mel[iy * 20 + ix] : 0.f;
-                    v[e] = __builtin_bit_cast(unsigned short, (bf16_t)f);
-                }
-                i32x4 p;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) p[e] = (int)v[2 * e] | ((int)v[2 * e + 1] << 16);
-                st16(BOFF + m * 64 + g * 16, p);
-            }
-        }
+        for (int q = 0; q < 4; ++q) *reinterpret_cast<bf16_t*>(lds + MEL + ((iy + 1) * MP + ix + 1 + q) * 2) = (bf16_t)mv[q];
     }
     __syncthreads();
+    STAMP_AT(1);
     {
+        int toff[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int tap = 8 * kg + e, ky = tap / 5, kx = tap - 5 * ky;
+            toff[e] = tap < 25 ? (ky * MP + kx) * 2 : -1;
+        }
         // M fragment f = rows 16 f .. 16 f + 15 of the 40 x 10 grid; slot i = fragment w + 8 i
         f32x4 acc[4][4];
-        i32x4 fb[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) fb[j] = *reinterpret_cast<const i32x4*>(reinterpret_cast<const char*>(a.w1) + ((16 * j + r16) * 32 + kg * 8) * 2);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int f = (w + 8 * i < 25) ? w + 8 * i : 0;
-            const i32x4 fa = lds16(lds, BOFF + (16 * f + r16) * 64 + kg * 16);
+            const int m = 16 * f + r16, oy = m / 10, ox = m - oy * 10;
+            const char* const base = lds + MEL + (2 * oy * MP + 2 * ox) * 2;
+            unsigned v[8];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) acc[i][j] = mfma(fb[j], fa, (f32x4){0.f, 0.f, 0.f, 0.f});   // W x A
+            for (int e = 0; e < 8; ++e) v[e] = toff[e] >= 0 ? *reinterpret_cast<const unsigned short*>(base + toff[e]) : 0u;
+            const i32x4 fa = {(int)(v[0] | (v[1] << 16)), (int)(v[2] | (v[3] << 16)), (int)(v[4] | (v[5] << 16)),
+                              (int)(v[6] | (v[7] << 16))};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = mfma(fb1[j], fa, (f32x4){0.f, 0.f, 0.f, 0.f});   // W x A
         }
         // -> a_conv2's input: chunk (n / 32) buffer, padded pixel (oy + 1, ox + 1); lane = pixel row r16,
         // channels 16 j + 4 kg .. + 3
@@ -158,61 +172,56 @@ __global__ __launch_bounds__(NT, 1) void k_aud_enc(AudEncArgs a) {
         }
     }
     __syncthreads();
+    STAMP_AT(2);
 
-    // ================= a_conv3..a_conv5: 128 output channels, weight slabs of 8 KB in groups of 2 =================
-    const int brow3 = tid >> 2, kq3 = tid & 3;
-    const int bst3 = BOFF + brow3 * 64 + ((kq3 ^ wsw(brow3)) << 4);   // + slot 16384 + pos 8192
-    auto st16b = [&](int addr, i32x4 v) { st16(addr, v); };
-    // generic slab loop over NS compile-time slabs: bsoff(s) = weight byte offset of slab s (+ lane part),
-    // aread(s, f) / mm(f, b) supplied per layer
-    auto run = [&](auto nss, const __amdgpu_buffer_rsrc_t& rsW, int vbl, auto bsoff, const Pre& pre, auto read_a,
-                   auto read_b, auto mm) {
-        constexpr int NS = decltype(nss)::value;
-        i32x4 pb[DA];   // pb[S % DA] holds slab S + 2 at step S
-#pragma unroll
-        for (int k = 0; k < DA; ++k) pb[k] = pre.w[k + 2];
-        st16b(bst3, pre.w[0]);
-        st16b(bst3 + 8192, pre.w[1]);
-        __syncthreads();
-        read_a(std::integral_constant<int, 0>{}, 0);
-        read_b(std::integral_constant<int, 0>{}, 0);
-        unroll(std::make_integer_sequence<int, NS>{}, [&](auto ss) {
-            constexpr int S = decltype(ss)::value;
-            __builtin_amdgcn_sched_barrier(0);
-            if constexpr (S + 2 < NS) {
-                st16b(bst3 + (((S / 2) + 1) & 1) * 16384 + (S % 2) * 8192, pb[S % DA]);   // slab S + 2
-                if constexpr (S + 2 + DA < NS)
-                    pb[S % DA] = __builtin_amdgcn_raw_buffer_load_b128(rsW, vbl + bsoff(std::integral_constant<int, S + 2 + DA>{}), 0, 0);
-            }
-            if constexpr (S % 2 == 1) __syncthreads();
-            if constexpr (S + 1 < NS) {
-                read_a(std::integral_constant<int, S + 1>{}, (S + 1) & 1);
-                read_b(std::integral_constant<int, S + 1>{}, (S + 1) & 1);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            mm(S & 1);
-        });
-    };
-    // a layer's first DA + 2 weight slabs (two to the ring, DA in flight), issued before the previous layer's epilogue
-    auto prefetch = [&](const __amdgpu_buffer_rsrc_t& rsW, int vbl, auto bsoff) {
+    // ================= a_conv3..a_conv5: 128 output channels, one 16-channel slice per wave =================
+    // A wave owns output channels 16 w .. 16 w + 15 and every M fragment of the layer, so no two waves use the same
+    // weights: each wave loads its B fragments (16 rows x 64 B per 32-deep slab) straight from global memory DA + 2
+    // slabs ahead, and the loop has no LDS weight ring and no barrier.  A fragments come from the LDS image, read
+    // two slabs ahead.  (With an LDS ring shared by waves that split M and N, a_conv3..a_conv5 ran at 20-40 % of
+    // the MFMA rate: 2-8 MFMAs per slab could not cover a barrier every two slabs.)
+    const __amdgpu_buffer_rsrc_t rsW3 = make_rsrc(a.w3, 128 * 1024 * 2), rsW4 = make_rsrc(a.w4, 128 * 512 * 2),
+                                 rsW5 = make_rsrc(a.w5, 128 * 512 * 2);
+    auto bsoff3 = [](auto ss) { constexpr int S = decltype(ss)::value; return (S % 16) * 128 + (S / 16) * 64; };
+    auto bsoff45 = [](auto ss) { constexpr int S = decltype(ss)::value; return (S % 4) * 256 + (S / 4) * 64; };
+    // a layer's first DA + 2 B fragments of this wave (weight row 16 w + r16 of rowb bytes, k-group kg)
+    auto prefetch_direct = [&](const __amdgpu_buffer_rsrc_t& rsW, int rowb, auto bsoff) {
+        const int vbw = (16 * w + r16) * rowb + kg * 16;
         Pre p;
         unroll(std::make_integer_sequence<int, DA + 2>{}, [&](auto k) {
-            p.w[decltype(k)::value] = __builtin_amdgcn_raw_buffer_load_b128(rsW, vbl + bsoff(k), 0, 0);
+            p.w[decltype(k)::value] = __builtin_amdgcn_raw_buffer_load_b128(rsW, vbw + bsoff(k), 0, 0);
         });
         return p;
     };
-    const __amdgpu_buffer_rsrc_t rsW3 = make_rsrc(a.w3, 128 * 1024 * 2), rsW4 = make_rsrc(a.w4, 128 * 512 * 2),
-                                 rsW5 = make_rsrc(a.w5, 128 * 512 * 2);
-    const int vbl34 = brow3 * 2048 + kq3 * 32;   // a_conv3 (1024-deep rows): vbl34; a_conv4/5 (512): vbl34 / 2
-    auto bsoff3 = [](auto ss) { constexpr int S = decltype(ss)::value; return (S % 16) * 128 + (S / 16) * 64; };
-    auto bsoff45 = [](auto ss) { constexpr int S = decltype(ss)::value; return (S % 4) * 256 + (S / 4) * 64; };
-    auto b_read = [&](int row0, auto ss, int nfr, i32x4* dst) {   // B fragments of rows row0 + 16 j + r16
-        constexpr int S = decltype(ss)::value;
-        for (int j = 0; j < nfr; ++j)
-            dst[j] = lds16(lds, BOFF + ((S / 2) & 1) * 16384 + (S % 2) * 8192 + (row0 + 16 * j + r16) * 64 + ((kg ^ wsw(r16)) << 4));
+    // the slab loop: NFR M fragments at LDS bases vb[i] + aimm(slab); acc = the 16 x (16 NFR) tile (W x A)
+    auto direct = [&](auto nff, auto nss, const __amdgpu_buffer_rsrc_t& rsW, int rowb, auto bsoff, auto aimm, const int* vb,
+                      const Pre& pre, f32x4* acc) {
+        constexpr int NFR = decltype(nff)::value, NS = decltype(nss)::value, DB = DA + 2, RA = NFR >= 7 ? 3 : 4;
+        const int vbw = (16 * w + r16) * rowb + kg * 16;
+        i32x4 fa[RA][NFR], pb[DB];
+#pragma unroll
+        for (int k = 0; k < DB; ++k) pb[k] = pre.w[k];
+        auto read_a = [&](auto ss) {
+            constexpr int S = decltype(ss)::value;
+            if constexpr (S < NS) {
+                const int imm = aimm(ss);
+#pragma unroll
+                for (int i = 0; i < NFR; ++i) fa[S % RA][i] = lds16(lds + imm, vb[i]);
+            }
+        };
+        unroll(std::make_integer_sequence<int, RA - 1>{}, [&](auto k) { read_a(k); });
+        unroll(std::make_integer_sequence<int, NS>{}, [&](auto ss) {
+            constexpr int S = decltype(ss)::value;
+            __builtin_amdgcn_sched_barrier(0);   // the reads of slab S + RA - 1 go out ahead of slab S's MFMAs
+            const i32x4 fb = pb[S % DB];
+            if constexpr (S + DB < NS)
+                pb[S % DB] = __builtin_amdgcn_raw_buffer_load_b128(rsW, vbw + bsoff(std::integral_constant<int, S + DB>{}), 0, 0);
+            read_a(std::integral_constant<int, S + RA - 1>{});
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 0; i < NFR; ++i) acc[i] = mfma(fb, fa[S % RA][i], S == 0 ? (f32x4){0.f, 0.f, 0.f, 0.f} : acc[i]);
+        });
     };
-
-    const int vbl3 = brow3 * 2048 + kq3 * 16;
     Pre pre3{}, pre4{}, pre5{};
 
     // ================= a_conv2: 4x4, 64 -> 64 on 40 x 10 (slab = chunk * 16 + tap) =================
@@ -251,6 +260,7 @@ __global__ __launch_bounds__(NT, 1) void k_aud_enc(AudEncArgs a) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
         __syncthreads();
+        STAMP_AT(3);
         i32x4 fa[2][4], fb[2][4];
         int vq[4];
 #pragma unroll
@@ -290,7 +300,8 @@ __global__ __launch_bounds__(NT, 1) void k_aud_enc(AudEncArgs a) {
             });
         }
         __syncthreads();   // every read of a_conv2's input done: a_conv3's image goes over it
-        pre3 = prefetch(rsW3, vbl3, bsoff3);   // a_conv3's first slabs load under this epilogue
+        STAMP_AT(4);
+        pre3 = prefetch_direct(rsW3, 2048, bsoff3);   // a_conv3's first weight fragments load under this epilogue
         zero(0, IMG3B);
         __syncthreads();
         // -> a_conv3's input, padded pixel (oy + 1, ox + 1), 8 x 2 fragment rows; lane = fragment row r16
@@ -308,99 +319,84 @@ __global__ __launch_bounds__(NT, 1) void k_aud_enc(AudEncArgs a) {
             }
         }
         __syncthreads();
+        STAMP_AT(5);
     }
 
     // ---- a_conv3: 4x4 stride 2, 64 -> 128, 40 x 10 -> 20 x 5 (100 rows, 7 fragments); slab = chunk * 16 + tap ----
     {
-        int vb[4];
+        int vb[7];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int f = 4 * mh + i, m = (16 * f + r16 < 100) ? 16 * f + r16 : 0;
+        for (int i = 0; i < 7; ++i) {
+            const int m = (16 * i + r16 < 100) ? 16 * i + r16 : 0;
             const int oy = m / 5, ox = m - oy * 5;
             vb[i] = (2 * oy * P3 + 2 * ox) * S3 + kg * 16;
         }
-        f32x4 acc[4][2];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
-        i32x4 fa[2][4], fb[2][2];
-        run(std::integral_constant<int, 32>{}, rsW3, vbl3, bsoff3, pre3,
-            [&](auto ss, int buf) {
-                constexpr int S = decltype(ss)::value, t = S % 16, c = S / 16;
-                constexpr int imm = ((t / 4) * P3 + t % 4) * S3 + c * 64;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) fa[buf][i] = lds16(lds + imm, vb[i]);
-            },
-            [&](auto ss, int buf) { b_read(32 * nq, ss, 2, fb[buf]); },
-            [&](int buf) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-#pragma unroll
-                    for (int j = 0; j < 2; ++j) acc[i][j] = mfma(fb[buf][j], fa[buf][i], acc[i][j]);   // W x A
-            });
-        __syncthreads();
-        pre4 = prefetch(rsW4, vbl34 / 2, bsoff45);   // a_conv4's first slabs load under this epilogue
+        f32x4 acc[7];
+        direct(std::integral_constant<int, 7>{}, std::integral_constant<int, 32>{}, rsW3, 2048, bsoff3, [](auto ss) {
+            constexpr int S = decltype(ss)::value, t = S % 16, c = S / 16;
+            return ((t / 4) * P3 + t % 4) * S3 + c * 64;
+        }, vb, pre3, acc);
+        __syncthreads();   // every read of a_conv3's input done: a_conv4's image goes over it
+        STAMP_AT(6);
+        pre4 = prefetch_direct(rsW4, 1024, bsoff45);   // a_conv4's first weight fragments load under this epilogue
         zero(0, IMG4B);   // a_conv4's input: column 5 reads as zero
         __syncthreads();
+        const int n = 16 * w + 4 * kg;   // lane channels n .. n + 3
+        f32x4 sc, sh;
+        bnq(2, n, sc, sh);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int m = 16 * (4 * mh + i) + r16;
+        for (int i = 0; i < 7; ++i) {
+            const int m = 16 * i + r16;
             if (m >= 100) continue;
             const int oy = m / 5, ox = m - oy * 5;
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int n = 32 * nq + 16 * j + 4 * kg;
-                f32x4 sc, sh;
-                bnq(2, n, sc, sh);
-                st8l((oy * P4 + ox) * S4 + n * 2, bn_pack4(acc[i][j], sc, sh));
-            }
+            st8l((oy * P4 + ox) * S4 + n * 2, bn_pack4(acc[i], sc, sh));
         }
         __syncthreads();
+        STAMP_AT(7);
     }
 
-    // ---- a_conv4 / a_conv5: 2x2 stride (2, 1), 128 -> 128; slab = chunk * 4 + tap; wave w: channels 16 w .. 16 w + 15 ----
+    // ---- a_conv4 / a_conv5: 2x2 stride (2, 1), 128 -> 128; slab = chunk * 4 + tap ----
     auto small = [&](auto nff, int img, const __amdgpu_buffer_rsrc_t& rsW, const Pre& pre, int layer, auto store,
                      auto next) {
         constexpr int NFR = decltype(nff)::value;   // M fragments (4: 50 rows, 2: 25 rows)
         constexpr int MR = NFR == 4 ? 50 : 25;
+        // fragment row m -> output (oy, ox): column-major on a_conv4's 10 x 5 grid (1.5-way bank conflicts
+        // against 1.75 row-major), row-major on a_conv5's 5 x 5
+        auto grid = [](int m, int& oy, int& ox) {
+            if constexpr (NFR == 4) { ox = m / 10; oy = m - ox * 10; } else { oy = m / 5; ox = m - oy * 5; }
+        };
         int vb[NFR];
 #pragma unroll
         for (int i = 0; i < NFR; ++i) {
             const int m = (16 * i + r16 < MR) ? 16 * i + r16 : 0;
-            const int oy = m / 5, ox = m - oy * 5;
+            int oy, ox;
+            grid(m, oy, ox);
             vb[i] = img + (2 * oy * P4 + ox) * S4 + kg * 16;
         }
         f32x4 acc[NFR];
-#pragma unroll
-        for (int i = 0; i < NFR; ++i) acc[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
-        i32x4 fa[2][NFR], fb[2][1];
-        run(std::integral_constant<int, 16>{}, rsW, vbl34 / 2, bsoff45, pre,
-            [&](auto ss, int buf) {
-                constexpr int S = decltype(ss)::value, t = S % 4, c = S / 4;
-                constexpr int imm = ((t / 2) * P4 + t % 2) * S4 + c * 64;
-#pragma unroll
-                for (int i = 0; i < NFR; ++i) fa[buf][i] = lds16(lds + imm, vb[i]);
-            },
-            [&](auto ss, int buf) { b_read(16 * w, ss, 1, fb[buf]); },
-            [&](int buf) {
-#pragma unroll
-                for (int i = 0; i < NFR; ++i) acc[i] = mfma(fb[buf][0], fa[buf][i], acc[i]);   // W x A
-            });
+        direct(nff, std::integral_constant<int, 16>{}, rsW, 1024, bsoff45, [](auto ss) {
+            constexpr int S = decltype(ss)::value, t = S % 4, c = S / 4;
+            return ((t / 2) * P4 + t % 2) * S4 + c * 64;
+        }, vb, pre, acc);
+        STAMP_AT(10 + (NFR == 2));
+        next();   // the next layer's first weight fragments load under this epilogue
         const int n = 16 * w + 4 * kg;   // lane channels n .. n + 3
-        __syncthreads();
-        next();   // the next layer's first weight slabs load under this epilogue
         f32x4 sc, sh;
         bnq(layer, n, sc, sh);
 #pragma unroll
         for (int i = 0; i < NFR; ++i) {
             const int m = 16 * i + r16;
-            if (m < MR) store(m / 5, m % 5, n, bn_pack4(acc[i], sc, sh));
+            int oy, ox;
+            grid(m, oy, ox);
+            if (m < MR) store(oy, ox, n, bn_pack4(acc[i], sc, sh));
         }
         __syncthreads();
+        STAMP_AT(8 + (NFR == 2));
     };
     zero(IMG5, IMG5 + IMG5B);   // a_conv5's input: column 5 reads as zero (ordered by the barriers in `small`)
     small(std::integral_constant<int, 4>{}, 0, rsW4, pre4, 3, [&](int oy, int ox, int n, i32x2 v) {
         st8l(IMG5 + (oy * P4 + ox) * S4 + n * 2, v);
-    }, [&] { pre5 = prefetch(rsW5, vbl34 / 2, bsoff45); });
+    }, [&] { pre5 = prefetch_direct(rsW5, 1024, bsoff45); });
     bf16_t* const outc = a.out + (long long)clip * a.out_clip_stride;
     small(std::integral_constant<int, 2>{}, IMG5, rsW5, pre5, 4, [&](int oy, int ox, int n, i32x2 v) {
         *reinterpret_cast<i32x2*>(outc + (oy * 5 + ox) * 128 + n) = v;   // Flatten (HWC) -> concat[0:3200]
@@ -408,6 +404,8 @@ __global__ __launch_bounds__(NT, 1) void k_aud_enc(AudEncArgs a) {
 }
 
 }  // namespace
+
+#undef STAMP_AT
 
 bool aud_enc_supported(const AudEncArgs& a) {
     const char* e = std::getenv("AVSE_NO_AUDENC");
@@ -418,10 +416,10 @@ bool aud_enc_supported(const AudEncArgs& a) {
 int launch_aud_enc(const AudEncArgs& a, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
-        AVSE_HIP_CHECK(hipFuncSetAttribute((const void*)k_aud_enc, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
+        AVSE_HIP_CHECK(hipFuncSetAttribute((const void*)k_aud_enc<0>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
         attr = true;
     }
-    hipLaunchKernelGGL(k_aud_enc, dim3(a.N), dim3(NT), LDS_BYTES, s, a);
+    hipLaunchKernelGGL(k_aud_enc<0>, dim3(a.N), dim3(NT), LDS_BYTES, s, a);
     AVSE_HIP_CHECK(hipGetLastError());
     return 0;
 }

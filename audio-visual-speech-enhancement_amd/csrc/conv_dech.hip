@@ -88,6 +88,13 @@ template <int L> struct Geo {
     static constexpr int DY0 = L == 3 ? -1 : 0, DX0 = -1;
     static constexpr int tap_dy(int p, int t) { return L == 3 ? (p >> 1) - (t >> 1) : 0; }
     static constexpr int tap_dx(int p, int t) { return L == 3 ? (p & 1) - (t & 1) : -t; }
+    // fragment row m -> grid (yq, xq): column-major for d_deconv2 / d_deconv3 (16 consecutive rows of a column: the
+    // ds_read_b128 fragment gathers are 1.5 / 1.4-way bank-conflicted instead of 1.75 / 2.0 row-major, exhaustive
+    // check over every tap), row-major for d_deconv1
+    static constexpr bool CM = L >= 2;
+    __device__ static void grid(int m, int& yq, int& xq) {
+        if constexpr (CM) { xq = m / HQ; yq = m - xq * HQ; } else { yq = m / WQ; xq = m - yq * WQ; }
+    }
 };
 
 // ABL: ablation mask for tools/dech_ablate.hip only (0 in the library): 1 = no MFMAs, 2 = no epilogue stores,
@@ -147,7 +154,8 @@ __global__ __launch_bounds__(NT, 1) void k_dec_head(DecHeadArgs a) {
         for (int i = 0; i < NI; ++i) {
             const int c = WIDE ? mh : i / G::NFR, f = WIDE ? i : i % G::NFR;
             const int m = (16 * f + r16 < G::M) ? 16 * f + r16 : 0;
-            const int yq = m / 5, xq = m - yq * 5;
+            int yq, xq;
+            G::grid(m, yq, xq);
             vb[i] = c * CLB + G::IMG + ((yq + G::PT + G::DY0) * G::P + (xq + G::PL + G::DX0)) * S + kg * 16;
         }
         // accumulator row e of channel fragment j = channel row0 + 16 j + 4 kg + e
@@ -216,7 +224,8 @@ __global__ __launch_bounds__(NT, 1) void k_dec_head(DecHeadArgs a) {
                     const int c = WIDE ? mh : i / G::NFR, f = WIDE ? i : i % G::NFR;
                     const int m = 16 * f + r16;
                     if (((ABL & 2) != 0 && a.N != -1) || (16 * f + 15 >= G::M && m >= G::M)) continue;
-                    const int yq = m / 5, xq = m - yq * 5;
+                    int yq, xq;
+                    G::grid(m, yq, xq);
 #pragma unroll
                     for (int j = 0; j < NJ; ++j) {
                         const f32x4 v = acc[i][j];

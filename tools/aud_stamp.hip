@@ -1,0 +1,77 @@
+// Phase timing of the fused audio encoder (k_aud_enc<1>, conv_aud.hip) at the bench shape (N = 512): thread 0 of every
+// workgroup stamps s_memtime at the phase boundaries; printed: mean cycles per phase over the workgroups.
+//   hipcc --offload-arch=gfx950 -O3 -std=c++20 -o _aud_stamp aud_stamp.hip
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "../audio-visual-speech-enhancement_amd/csrc/conv_aud.hip"
+
+namespace avse {
+void set_error(const std::string& msg) { std::fprintf(stderr, "error: %s\n", msg.c_str()); }
+}  // namespace avse
+
+using namespace avse;
+
+int main() {
+    const int N = 512;
+    AudEncArgs a{};
+    a.N = N;
+    a.out_clip_stride = 5248;
+    void *mel, *out, *w[5];
+    const size_t wsz[5] = {64 * 32, 64 * 1024, 128 * 1024, 128 * 512, 128 * 512};
+    (void)hipMalloc(&mel, (size_t)N * 1600 * 4);
+    (void)hipMalloc(&out, (size_t)N * 5248 * 2);
+    (void)hipMemset(mel, 0, (size_t)N * 1600 * 4);
+    for (int l = 0; l < 5; ++l) {
+        (void)hipMalloc(&w[l], wsz[l] * 2);
+        (void)hipMemset(w[l], 0, wsz[l] * 2);
+    }
+    float* par;
+    (void)hipMalloc(&par, 2048 * 4);
+    (void)hipMemset(par, 0, 2048 * 4);
+    a.mel = (const float*)mel; a.out = (bf16_t*)out;
+    a.w1 = (const bf16_t*)w[0]; a.w2 = (const bf16_t*)w[1]; a.w3 = (const bf16_t*)w[2];
+    a.w4 = (const bf16_t*)w[3]; a.w5 = (const bf16_t*)w[4];
+    for (int l = 0; l < 5; ++l) { a.sc[l] = par + 256 * l; a.sh[l] = par + 256 * l + 128; }
+    unsigned long long* st;
+    (void)hipMalloc(&st, (size_t)N * 16 * 8);
+    (void)hipMemset(st, 0, (size_t)N * 16 * 8);
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &st, sizeof(st));
+    (void)hipFuncSetAttribute((const void*)k_aud_enc<0>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)k_aud_enc<1>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    auto timed = [&](auto kern) {
+        for (int r = 0; r < 2; ++r) hipLaunchKernelGGL(kern, dim3(N), dim3(NT), LDS_BYTES, 0, a);
+        (void)hipEventRecord(e0, 0);
+        for (int r = 0; r < 20; ++r) hipLaunchKernelGGL(kern, dim3(N), dim3(NT), LDS_BYTES, 0, a);
+        (void)hipEventRecord(e1, 0);
+        (void)hipEventSynchronize(e1);
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, e0, e1);
+        return ms / 20;
+    };
+    std::printf("k_aud_enc<0> %.4f ms   <1> %.4f ms\n", timed(k_aud_enc<0>), timed(k_aud_enc<1>));
+    std::vector<unsigned long long> h((size_t)N * 16);
+    (void)hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost);
+    const char* names[10] = {"start", "im2col", "a_conv1", "a_conv2 pro", "a_conv2 loop", "a_conv2 epi",
+                             "a_conv3 loop", "a_conv3 epi", "a_conv4", "a_conv5"};
+    double tot = 0;
+    for (int k = 1; k < 10; ++k) {
+        double s = 0;
+        for (int b = 0; b < N; ++b) s += (double)(h[b * 16 + k] - h[b * 16 + k - 1]);
+        s /= N;
+        tot += s;
+        std::printf("%-14s %9.0f cycles\n", names[k], s);
+    }
+    std::printf("%-14s %9.0f cycles per workgroup\n", "total", tot);
+    double l4 = 0, l5 = 0;
+    for (int b = 0; b < N; ++b) {
+        l4 += (double)(h[b * 16 + 10] - h[b * 16 + 7]);
+        l5 += (double)(h[b * 16 + 11] - h[b * 16 + 8]);
+    }
+    std::printf("a_conv4 loop   %9.0f cycles (from a_conv3's end)\na_conv5 loop   %9.0f cycles (from a_conv4's end)\n", l4 / N, l5 / N);
+    return 0;
+}
