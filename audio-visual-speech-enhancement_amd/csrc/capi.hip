@@ -2,12 +2,15 @@
 // the layer plan of /root/reference/network.py, executed as a sequence of HIP kernel launches on
 // the caller's stream.
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
+
+#include <unistd.h>   // environ
 
 #include "../../include/avse.h"
 #include "avse_common.h"
@@ -163,6 +166,15 @@ struct avse_ctx {
     // side stream for the audio branch of the forward (runs concurrently with the video encoder)
     hipStream_t side = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
+    // avse_forward's replay cache: the whole forward captured once per argument set into a hipGraph
+    struct Graph {
+        const void* key[8];
+        int64_t n;
+        size_t env;
+        hipGraphExec_t exec;
+    };
+    std::vector<Graph> graphs;
+    hipStream_t cap = nullptr;   // capture stream
 };
 
 struct GpuLayer {
@@ -186,6 +198,7 @@ struct GpuLayer {
 struct avse_weights {
     int dtype = 0;
     int device = 0;
+    uint64_t serial = 0;                // unique per created weights object (graph-cache key: addresses get reused)
     GpuLayer layers[kNumLayers - 1];  // all but d_deconv6
     float* d6_w = nullptr;
     float d6_bias = 0.f;
@@ -747,6 +760,8 @@ void avse_ctx_destroy(avse_ctx* c) {
     (void)hipFree(c->umax);
     (void)hipFree(c->mse_partial);
     (void)hipFree(c->arena);
+    for (auto& g : c->graphs) (void)hipGraphExecDestroy(g.exec);
+    if (c->cap) (void)hipStreamDestroy(c->cap);
     if (c->side) (void)hipStreamDestroy(c->side);
     if (c->fork) (void)hipEventDestroy(c->fork);
     if (c->join) (void)hipEventDestroy(c->join);
@@ -859,6 +874,8 @@ int avse_weights_load(avse_ctx* c, const float* blob, int64_t n_floats, int dtyp
                                           std::to_string(blob_floats()));
     AVSE_HIP_CHECK(hipSetDevice(c->device));
     avse_weights* W = new avse_weights();
+    static std::atomic<uint64_t> next_serial{1};
+    W->serial = next_serial++;
     W->dtype = dtype;
     W->device = c->device;
     const float* p = blob;
@@ -950,28 +967,12 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
     // the halo-tiled v_conv1 reads the raw video and normalises it itself
     if (L(5).halo == HALO_NONE && (rc = launch_video_prep(video, vmean, vstd, buf(B_VIN), N, dt, s))) return rc;
     if ((rc = mark())) return rc;
-    // The audio branch (prep + a_conv1..5 -> concat[0:3200]) shares no buffer with the video encoder until the
-    // fusion dense: it runs on the context's side stream, forked from and joined back into s, so its short,
-    // latency-bound kernels overlap the video encoder (the profiling path keeps one stream for per-stage
-    // events; AVSE_SERIAL=1 forces it).  The fork waits for everything enqueued on s before this call.
-    const bool concurrent = ev == nullptr && !serial_forward();
-    hipStream_t sa = s;
-    if (concurrent) {
-        if (!c->side) {
-            AVSE_HIP_CHECK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
-            AVSE_HIP_CHECK(hipEventCreateWithFlags(&c->fork, hipEventDisableTiming));
-            AVSE_HIP_CHECK(hipEventCreateWithFlags(&c->join, hipEventDisableTiming));
-        }
-        AVSE_HIP_CHECK(hipEventRecord(c->fork, s));
-        AVSE_HIP_CHECK(hipStreamWaitEvent(c->side, c->fork, 0));
-        sa = c->side;
-    }
     // audio encoder (network.py:88-109): one fused kernel per clip (conv_aud.hip) when the layers have the network's
     // shapes (AVSE_NO_AUDENC=1: per-layer launches); profiled, its time shows as the audio_prep stage
     bool aud_fused = false;
+    AudEncArgs aa;
+    std::memset(&aa, 0, sizeof(aa));
     if (dt == AVSE_BF16) {
-        AudEncArgs aa;
-        std::memset(&aa, 0, sizeof(aa));
         aa.mel = audio;
         aa.out = reinterpret_cast<bf16_t*>(buf(B_CAT));
         aa.out_clip_stride = 5248;
@@ -985,16 +986,34 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
         aa.w1 = (const bf16_t*)ws[0]; aa.w2 = (const bf16_t*)ws[1]; aa.w3 = (const bf16_t*)ws[2];
         aa.w4 = (const bf16_t*)ws[3]; aa.w5 = (const bf16_t*)ws[4];
         for (int i = 0; i < 5; ++i) { aa.sc[i] = L(i).scale; aa.sh[i] = L(i).shift; }
-        if (shapes && aud_enc_supported(aa)) {
-            // on the caller's stream: beside the persistent video convolutions its 148-KB workgroups hold whole CUs
-            // they wait for (measured: concurrent 2.377 ms vs serial 2.304 ms per step); AVSE_AUD_SIDE=1 keeps the
-            // side stream
-            const char* e = std::getenv("AVSE_AUD_SIDE");
-            if ((rc = launch_aud_enc(aa, (e && e[0] == '1') ? sa : s))) return rc;
-            for (int k = 0; k < 6; ++k)
-                if ((rc = mark())) return rc;   // audio_prep (= the fused kernel), a_conv1..a_conv5
-            aud_fused = true;
+        aud_fused = shapes && aud_enc_supported(aa);
+    }
+
+    // The per-layer audio branch (prep + a_conv1..5 -> concat[0:3200]) shares no buffer with the video encoder until
+    // the fusion dense: it runs on the context's side stream, forked from and joined back into s, so its short,
+    // latency-bound kernels overlap the video encoder (the profiling path keeps one stream for per-stage events;
+    // AVSE_SERIAL=1 forces it).  The fork waits for everything enqueued on s before this call.
+    // The fused audio encoder runs on the caller's stream: beside the persistent video convolutions its 152-KB
+    // workgroups hold whole CUs they wait for (measured: concurrent 2.377 ms vs serial 2.304 ms per step), and the
+    // fork / join events alone cost ~25 us of idle GPU per step (rocprof trace); AVSE_AUD_SIDE=1 keeps the side stream.
+    const char* aud_side_env = std::getenv("AVSE_AUD_SIDE");
+    const bool aud_side = aud_side_env && aud_side_env[0] == '1';
+    const bool concurrent = ev == nullptr && !serial_forward() && (!aud_fused || aud_side);
+    hipStream_t sa = s;
+    if (concurrent) {
+        if (!c->side) {
+            AVSE_HIP_CHECK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+            AVSE_HIP_CHECK(hipEventCreateWithFlags(&c->fork, hipEventDisableTiming));
+            AVSE_HIP_CHECK(hipEventCreateWithFlags(&c->join, hipEventDisableTiming));
         }
+        AVSE_HIP_CHECK(hipEventRecord(c->fork, s));
+        AVSE_HIP_CHECK(hipStreamWaitEvent(c->side, c->fork, 0));
+        sa = c->side;
+    }
+    if (aud_fused) {
+        if ((rc = launch_aud_enc(aa, aud_side ? sa : s))) return rc;
+        for (int k = 0; k < 6; ++k)
+            if ((rc = mark())) return rc;   // audio_prep (= the fused kernel), a_conv1..a_conv5
     }
     if (!aud_fused && ((rc = launch_audio_prep(audio, buf(B_AIN), N, dt, sa)) || (rc = mark()))) return rc;
     const int a_in[5] = {B_AIN, B_A1, B_A2, B_A3, B_A4};
@@ -1115,9 +1134,65 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
 
 extern "C" {
 
+// avse_forward replays a hipGraph of the forward once the same arguments (weights, input / output pointers, N, the
+// context's scratch arena and every AVSE_* environment switch) come a second time: the first call launches directly,
+// the second captures and launches the graph, later ones replay it — the ~15 kernels then run without the per-kernel
+// dispatch gaps of stream launches.  The graph bakes the pointers in; every argument set has its own entry (at most 8
+// are kept).  Opt-in (AVSE_GRAPH=1): a torch graph of the whole bench step (spectrogram + forward) measured 2.20 ->
+// 2.14 ms (tools/graph_probe.py), but replaying the forward alone inside the same step measured 2.234 vs 2.24-2.26 ms
+// direct (bench.py A/B, same box), so direct launches stay the default.
 int avse_forward(avse_ctx* c, const avse_weights* W, const float* audio, const float* video, const float* vmean,
                  const float* vstd, int64_t N, float* out, void* stream) {
-    return forward_impl(c, W, audio, video, vmean, vstd, N, out, (hipStream_t)stream, nullptr);
+    const char* ge = std::getenv("AVSE_GRAPH");
+    if (!c || !W || N <= 0 || !(ge && ge[0] == '1'))
+        return forward_impl(c, W, audio, video, vmean, vstd, N, out, (hipStream_t)stream, nullptr);
+    AVSE_HIP_CHECK(hipSetDevice(c->device));
+    if (W->device != c->device) return fail(AVSE_ERR_INVALID, "weights and context are on different devices");
+    int rc = ensure_arena(c, N, W->dtype);   // no allocation inside the capture
+    if (rc) return rc;
+    size_t env = 1469598103934665603ull;     // FNV-1a over the AVSE_* switches the launch code reads
+    for (char** e = environ; e && *e; ++e)
+        if (std::strncmp(*e, "AVSE_", 5) == 0)
+            for (const char* q = *e; *q; ++q) env = (env ^ (unsigned char)*q) * 1099511628211ull;
+    const void* key[8] = {(const void*)W->serial, audio, video, vmean, vstd, out, c->arena, (const void*)c->arena_bytes};
+    avse_ctx::Graph* hit = nullptr;
+    for (auto& g : c->graphs)
+        if (g.n == N && g.env == env && std::memcmp(g.key, key, sizeof(key)) == 0) hit = &g;
+    if (hit && hit->exec) {
+        AVSE_HIP_CHECK(hipGraphLaunch(hit->exec, (hipStream_t)stream));
+        return 0;
+    }
+    auto evict = [&] {
+        if (c->graphs.size() < 8) return;
+        if (c->graphs.front().exec) (void)hipGraphExecDestroy(c->graphs.front().exec);
+        c->graphs.erase(c->graphs.begin());
+    };
+    if (!hit) {   // first sighting of this argument set: launch directly (a one-off call pays no capture)
+        evict();
+        avse_ctx::Graph g;
+        std::memcpy(g.key, key, sizeof(key));
+        g.n = N;
+        g.env = env;
+        g.exec = nullptr;
+        c->graphs.push_back(g);
+        return forward_impl(c, W, audio, video, vmean, vstd, N, out, (hipStream_t)stream, nullptr);
+    }
+    if (!c->cap) AVSE_HIP_CHECK(hipStreamCreateWithFlags(&c->cap, hipStreamNonBlocking));
+    AVSE_HIP_CHECK(hipStreamBeginCapture(c->cap, hipStreamCaptureModeRelaxed));
+    rc = forward_impl(c, W, audio, video, vmean, vstd, N, out, c->cap, nullptr);
+    hipGraph_t graph = nullptr;
+    const hipError_t ce = hipStreamEndCapture(c->cap, &graph);
+    if (rc || ce != hipSuccess) {
+        if (graph) (void)hipGraphDestroy(graph);
+        return rc ? rc : fail(AVSE_ERR_HIP, std::string("forward capture: ") + hipGetErrorString(ce));
+    }
+    hipGraphExec_t exec = nullptr;
+    const hipError_t ie = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    if (ie != hipSuccess) return fail(AVSE_ERR_HIP, std::string("forward graph instantiate: ") + hipGetErrorString(ie));
+    hit->exec = exec;
+    AVSE_HIP_CHECK(hipGraphLaunch(exec, (hipStream_t)stream));
+    return 0;
 }
 
 int avse_forward_profile(avse_ctx* c, const avse_weights* W, const float* audio, const float* video,

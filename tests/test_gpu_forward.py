@@ -248,3 +248,36 @@ def test_bf16_fused_per_clip_kernels_match_layer_path(gpu, N, monkeypatch):
     assert rel_rms(cat_f, cat_l) <= 1e-2, rel_rms(cat_f, cat_l)
     assert rel_rms(out_f, out_l) <= 1e-2, rel_rms(out_f, out_l)
     assert rel_rms(out_f.reshape(ref.shape), ref) <= 3e-2, rel_rms(out_f.reshape(ref.shape), ref)
+
+
+@pytest.mark.gpu
+def test_forward_graph_replay(gpu, monkeypatch):
+    """avse_forward's hipGraph cache: the first call with an argument set launches directly, the second captures, later
+    ones replay — with new input CONTENTS at the same addresses the replay computes on them (bit-identical to direct
+    launches), and a changed AVSE_* switch or N gets its own entry (AVSE_GRAPH=1 enables the cache)."""
+    import torch
+    from avse_amd import ops
+    from avse_amd.model import KerasModel
+    N = 7
+    model = KerasModel.init(seed=5, randomize=True)
+    dw = ops.DeviceWeights(model, "bfloat16")
+    mel0, video0 = make_inputs(N, 3)
+    mean, std = R.video_normalizer_fit(video0)
+    d = [ops.to_device(mel0), ops.to_device(video0), ops.to_device(mean), ops.to_device(std)]
+    out = torch.empty((N, 80, 20), dtype=torch.float32, device=d[0].device)
+    monkeypatch.setenv("AVSE_GRAPH", "1")
+    results = []
+    for seed in (3, 4, 5, 6):   # direct, capture, replay, replay
+        mel, video = make_inputs(N, seed)
+        d[0].copy_(torch.from_numpy(mel.reshape(d[0].shape)))
+        d[1].copy_(torch.from_numpy(video.reshape(d[1].shape)))
+        ops.forward(dw, *d, out=out)
+        results.append(out.cpu().numpy().copy())
+    monkeypatch.delenv("AVSE_GRAPH")
+    for k, seed in enumerate((3, 4, 5, 6)):
+        mel, video = make_inputs(N, seed)
+        d[0].copy_(torch.from_numpy(mel.reshape(d[0].shape)))
+        d[1].copy_(torch.from_numpy(video.reshape(d[1].shape)))
+        ops.forward(dw, *d, out=out)
+        np.testing.assert_array_equal(out.cpu().numpy(), results[k])
+    assert not np.array_equal(results[2], results[3])
