@@ -48,7 +48,11 @@ constexpr int kOOB = 0x7fffff00;
 constexpr int H = 40, W = 10, HW = H * W;           // d_deconv4 / d_deconv5 phase grid
 constexpr int CI4 = 128, CO = 64;                    // d_deconv4 128 -> 64, d_deconv5 64 -> 64
 constexpr int NW = 8, NT = 64 * NW;                  // waves (two per SIMD), threads
-constexpr int NF = 4, NFRAG = HW / 16;               // fragment slots per wave (8 x 4 >= 25), fragments (25)
+// fragment slots per wave: slots 0..2 = fragments w, w + 8, w + 16 x all 64 channels; slot 3 = fragment 24 x channels
+// 16 w .. 16 w + 15 on waves 0..3 only (25 fragments x 4 channel blocks = 100 pairs: 13 / 12 per wave, 25 per SIMD,
+// where 8 waves x 4 full slots computed 128 pairs and dropped 28)
+constexpr int NF = 4, NFRAG = HW / 16, FX = 24;
+constexpr int PXB = 1280;                            // d_deconv6 partials of fragment 24 (4 waves x 16 pixels, f32)
 // d_deconv4: taps t -> (dy, dx) = (1 - t / 4, 1 - t % 4); window pixel (y + dy + 2, x + dx + 2)
 constexpr int P4 = 14, ROWS4 = 43, S4 = 96, NPIX4 = ROWS4 * P4;   // 602 pixels, 96-B rows
 constexpr int NPC = 5;                                            // 16-B pieces per lane per chunk (5 x 512 >= 602 x 4)
@@ -58,7 +62,7 @@ constexpr int P5 = 14, ROWS5 = 42, S5 = 160, OIMG = ROWS5 * P5 * S5;   // 94,080
 constexpr int BOFF = 2 * WBUF;                                        // weight slab ring: 2 groups x 4 slabs x 4 KB
 constexpr int PAR = BOFF + 2 * 4 * 4096;                              // folded BN / d_deconv6 parameters (f32):
 constexpr int PSC4 = PAR, PSH4 = PAR + 256, PSC5 = PAR + 512, PSH5 = PAR + 768, PW6 = PAR + 1024;   // 64 each
-constexpr int LDS_BYTES = PAR + 1280;                                 // 149,632
+constexpr int LDS_BYTES = PAR + PXB + 256;                            // 149,888
 static_assert(OIMG <= BOFF, "d_deconv5 image must fit over the d_deconv4 windows");
 
 constexpr int ph_ny(int p) { return 2 + (p >> 1); }
@@ -104,7 +108,7 @@ __global__ __launch_bounds__(NT, 1) void k_dec_tail(DecTailArgs a) {
     int vb4[NF], vb5[NF];   // LDS byte address of this lane's row at the smallest tap offset, + 16 kg
 #pragma unroll
     for (int i = 0; i < NF; ++i) {
-        const int f = (w + NW * i < NFRAG) ? w + NW * i : 0;
+        const int f = i < 3 ? w + NW * i : FX;
         const int y = 8 * (f / 5) + (r16 >> 1), x = 2 * (f % 5) + (r16 & 1);
         vb4[i] = (y * P4 + x) * S4 + kg * 16;   // tap (-2, -2)
         vb5[i] = (y * P5 + x) * S5 + kg * 16;   // tap (-1, -1)
@@ -116,9 +120,11 @@ __global__ __launch_bounds__(NT, 1) void k_dec_tail(DecTailArgs a) {
     const int brow = tid >> 3, kq = (tid >> 1) & 3, kh = tid & 1;   // 8 B per lane: half kh of 16-B group kq
     const int bst = BOFF + brow * 64 + ((kq ^ wsw(brow)) << 4) + kh * 8;   // + slot * 16384 + pos * 4096
     const int bfr = BOFF + r16 * 64 + ((kg ^ wsw(r16)) << 4);        // + slot * 16384 + pos * 4096 + 1024 j
-    auto read_b = [&](int base, i32x4 (&f)[4]) {
+    const bool xw = w < 4;   // this wave computes slot 3 (fragment 24 x channel block w)
+    auto read_b = [&](int base, i32x4 (&f)[4], i32x4& fx) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) f[j] = lds16(lds, base + 1024 * j);
+        if (xw) fx = lds16(lds, base + 1024 * w);
     };
     auto st16 = [&](int addr, i32x4 v) { *reinterpret_cast<i32x4*>(lds + addr) = v; };
     typedef int i32x2 __attribute__((ext_vector_type(2)));
@@ -131,13 +137,16 @@ __global__ __launch_bounds__(NT, 1) void k_dec_tail(DecTailArgs a) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
     };
-    auto mfma_all = [&](const i32x4 (&fa)[NF], const i32x4 (&fb)[4]) {
+    auto mfma_all = [&](const i32x4 (&fa)[NF], const i32x4 (&fb)[4], const i32x4& fbx) {
 #pragma unroll
-        for (int i = 0; i < NF; ++i)
+        for (int i = 0; i < 3; ++i)
 #pragma unroll
             for (int j = 0; j < 4; ++j)
                 acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fb[j]),   // W x A
                                                                      __builtin_bit_cast(bf16x8, fa[i]), acc[i][j], 0, 0, 0);
+        if (xw)
+            acc[3][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fbx), __builtin_bit_cast(bf16x8, fa[3]),
+                                                                acc[3][0], 0, 0, 0);
     };
 
     // =============================== d_deconv4 ===============================
@@ -198,7 +207,7 @@ __global__ __launch_bounds__(NT, 1) void k_dec_tail(DecTailArgs a) {
         zero_acc();
         __syncthreads();
 
-        i32x4 fa[2][NF], fb[2][4];
+        i32x4 fa[2][NF], fb[2][4], fbx[2];
         i32x4 pr[4];   // next chunk's window pieces: loaded at tap k < NPC, stored at tap k + 3
         int vq[NF];    // the fragment bases of the buffer being read: vb4 + (chunk & 1) * WBUF
 #pragma unroll
@@ -207,10 +216,11 @@ __global__ __launch_bounds__(NT, 1) void k_dec_tail(DecTailArgs a) {
             constexpr int t = decltype(tt)::value % 16;
             constexpr int imm = ((3 - t / 4) * P4 + (3 - t % 4)) * S4;   // tap (1 - t/4, 1 - t%4) from (-2, -2)
 #pragma unroll
-            for (int i = 0; i < NF; ++i) f[i] = lds16(lds + imm, vq[i]);
+            for (int i = 0; i < 3; ++i) f[i] = lds16(lds + imm, vq[i]);
+            if (xw) f[3] = lds16(lds + imm, vq[3]);
         };
         read_a(std::integral_constant<int, 0>{}, fa[0]);
-        read_b(bfr, fb[0]);
+        read_b(bfr, fb[0], fbx[0]);
         // slab S = 16 c + t; group S / 4 (slot parity (t / 4) & 1: 4 groups per chunk); every 4 slabs a barrier
         // publishes the next group's weights (stored during this group) and, at t = 15, the next chunk's window
         for (int c = 0; c < 4; ++c) {
@@ -235,9 +245,9 @@ __global__ __launch_bounds__(NT, 1) void k_dec_tail(DecTailArgs a) {
                 }
                 // the next slab's fragments (LDS) go out before this slab's MFMAs
                 read_a(std::integral_constant<int, t + 1>{}, fa[(t + 1) & 1]);
-                read_b(bfr + (((t + 1) / 4) & 1) * 16384 + ((t + 1) % 4) * 4096, fb[(t + 1) & 1]);
+                read_b(bfr + (((t + 1) / 4) & 1) * 16384 + ((t + 1) % 4) * 4096, fb[(t + 1) & 1], fbx[(t + 1) & 1]);
                 __builtin_amdgcn_sched_barrier(0);
-                mfma_all(fa[t & 1], fb[t & 1]);
+                mfma_all(fa[t & 1], fb[t & 1], fbx[t & 1]);
             });
         }
         __syncthreads();   // every window read done: the d_deconv5 image goes over the windows
@@ -247,17 +257,22 @@ __global__ __launch_bounds__(NT, 1) void k_dec_tail(DecTailArgs a) {
         __syncthreads();
         // epilogue: BN + LeakyReLU -> bf16 at image pixel (y + 1, x + 1); lane = block row r16, channels
         // 16 j + 4 kg .. + 3: one 8-B store per fragment pair (i, j)
+        auto st_quad = [&](int px, int j, const f32x4& v) {   // channels 16 j + 4 kg + e
+            const f32x4 sc = par4(PSC4, j), sh = par4(PSH4, j);
+            st8(px + 32 * j, pack4(bn_lrelu(v[0], sc[0], sh[0]), bn_lrelu(v[1], sc[1], sh[1]),
+                                   bn_lrelu(v[2], sc[2], sh[2]), bn_lrelu(v[3], sc[3], sh[3])));
+        };
 #pragma unroll
         for (int i = 0; i < NF; ++i) {
-            const int f = w + NW * i;
-            if (f >= NFRAG) continue;
+            if (i == 3 && !xw) continue;
+            const int f = i < 3 ? w + NW * i : FX;
             const int y = 8 * (f / 5) + (r16 >> 1), x = 2 * (f % 5) + (r16 & 1);
             const int px = ((y + 1) * P5 + x + 1) * S5 + 8 * kg;
+            if (i < 3) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {   // channels 16 j + 4 kg + e
-                const f32x4 v = acc[i][j], sc = par4(PSC4, j), sh = par4(PSH4, j);
-                st8(px + 32 * j, pack4(bn_lrelu(v[0], sc[0], sh[0]), bn_lrelu(v[1], sc[1], sh[1]),
-                                       bn_lrelu(v[2], sc[2], sh[2]), bn_lrelu(v[3], sc[3], sh[3])));
+                for (int j = 0; j < 4; ++j) st_quad(px, j, acc[i][j]);
+            } else {
+                st_quad(px, w, acc[3][0]);
             }
         }
         __syncthreads();
@@ -285,7 +300,8 @@ __global__ __launch_bounds__(NT, 1) void k_dec_tail(DecTailArgs a) {
         constexpr int dy = (p >> 1) - tap / ph_nx(p), dx = (p & 1) - tap % ph_nx(p);
         constexpr int imm = ((dy + 1) * P5 + (dx + 1)) * S5 + c * 64;
 #pragma unroll
-        for (int i = 0; i < NF; ++i) f[i] = lds16(lds + imm, vb5[i]);
+        for (int i = 0; i < 3; ++i) f[i] = lds16(lds + imm, vb5[i]);
+        if (xw) f[3] = lds16(lds + imm, vb5[3]);
     };
     auto epilogue5 = [&](auto pp) {
         constexpr int p = decltype(pp)::value, py = p >> 1, px = p & 1;
@@ -295,10 +311,16 @@ __global__ __launch_bounds__(NT, 1) void k_dec_tail(DecTailArgs a) {
         for (int j = 0; j < 4; ++j) {   // channels 16 j + 4 kg + e
             const f32x4 sc = par5(PSC5, j), sh = par5(PSH5, j), w6 = par5(PW6, j);
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+            for (int i = 0; i < 3; ++i)
 #pragma unroll
                 for (int e = 0; e < 4; ++e)   // y rounded to bf16 as the unfused path stores it
-                    part[i] = fmaf((float)(bf16_t)bn_lrelu(acc[i < NF ? i : 0][j][e], sc[e], sh[e]), w6[e], part[i]);
+                    part[i] = fmaf((float)(bf16_t)bn_lrelu(acc[i][j][e], sc[e], sh[e]), w6[e], part[i]);
+        }
+        if (xw) {   // slot 3: fragment 24, channels 16 w + 4 kg + e
+            const f32x4 sc = par5(PSC5, w), sh = par5(PSH5, w), w6 = par5(PW6, w);
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                part[3] = fmaf((float)(bf16_t)bn_lrelu(acc[3][0][e], sc[e], sh[e]), w6[e], part[3]);
         }
         // sum over the four lane rows (kg) of a slot, three swaps for four slots: lanes 0-31 <-> 32-63 pairs slots
         // (0, 1) and (2, 3), then rows 0 / 2 <-> 1 / 3: lane row kg ends with the total of slot {0, 2, 1, 3}[kg]
@@ -309,10 +331,21 @@ __global__ __launch_bounds__(NT, 1) void k_dec_tail(DecTailArgs a) {
         auto sw32 = [](unsigned x, unsigned y) { return __builtin_amdgcn_permlane32_swap(x, y, false, false); };
         auto sw16 = [](unsigned x, unsigned y) { return __builtin_amdgcn_permlane16_swap(x, y, false, false); };
         const float tot = swap_add(swap_add(part[0], part[1], sw32), swap_add(part[2], part[3], sw32), sw16);
-        const int i = ((kg & 1) << 1) | (kg >> 1), f = w + NW * i;
-        if (i < NF && f < NFRAG) {
-            const int y = 8 * (f / 5) + (r16 >> 1), x = 2 * (f % 5) + (r16 & 1);
+        const int i = ((kg & 1) << 1) | (kg >> 1);
+        if (i < 3) {
+            const int f = w + NW * i, y = 8 * (f / 5) + (r16 >> 1), x = 2 * (f % 5) + (r16 & 1);
             outc[(2 * y + py) * (2 * W) + 2 * x + px] = tot + a.b6;
+        } else if (xw) {
+            reinterpret_cast<float*>(lds + PAR + PXB)[16 * w + r16] = tot;   // this wave's 16-channel share
+        }
+        // fragment 24: the four waves' shares, summed in a fixed order by wave 0 (the buffer is rewritten only at the
+        // next phase end, two or more slab-group barriers later)
+        __syncthreads();
+        if (w == 0 && lane < 16) {
+            const float* xb = reinterpret_cast<const float*>(lds + PAR + PXB);
+            const float v = ((xb[lane] + xb[16 + lane]) + xb[32 + lane]) + xb[48 + lane];
+            const int y = 8 * (FX / 5) + (lane >> 1), x = 2 * (FX % 5) + (lane & 1);
+            outc[(2 * y + py) * (2 * W) + 2 * x + px] = v + a.b6;
         }
     };
 
@@ -330,9 +363,9 @@ __global__ __launch_bounds__(NT, 1) void k_dec_tail(DecTailArgs a) {
     }
     zero_acc();
     __syncthreads();
-    i32x4 fa[2][NF], fb[2][4];
+    i32x4 fa[2][NF], fb[2][4], fbx[2];
     read_a5(std::integral_constant<int, 0>{}, fa[0]);
-    read_b(bfr, fb[0]);
+    read_b(bfr, fb[0], fbx[0]);
     // global padded slab g: store g + 4 -> slot ((g / 4) + 1) & 1, load g + 8, barrier every 4 slabs; the fragments of
     // g + 1 (the next phase's first slab at a phase end, read after its epilogue) go out before g's MFMAs
     unroll(std::make_integer_sequence<int, ph_pstart(4)>{}, [&](auto gg) {
@@ -344,16 +377,16 @@ __global__ __launch_bounds__(NT, 1) void k_dec_tail(DecTailArgs a) {
         if constexpr (g % 4 == 3) __syncthreads();
         if constexpr (!last && g + 1 - ph_pstart(p) < 2 * ph_nt(p)) {
             read_a5(std::integral_constant<int, g + 1>{}, fa[(g + 1) & 1]);
-            read_b(bfr + (((g + 1) / 4) & 1) * 16384 + ((g + 1) % 4) * 4096, fb[(g + 1) & 1]);
+            read_b(bfr + (((g + 1) / 4) & 1) * 16384 + ((g + 1) % 4) * 4096, fb[(g + 1) & 1], fbx[(g + 1) & 1]);
         }
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (real) mfma_all(fa[g & 1], fb[g & 1]);
+        if constexpr (real) mfma_all(fa[g & 1], fb[g & 1], fbx[g & 1]);
         if constexpr (last) {
             epilogue5(std::integral_constant<int, p>{});
             if constexpr (p < 3) {
                 zero_acc();
                 read_a5(std::integral_constant<int, g + 1>{}, fa[(g + 1) & 1]);
-                read_b(bfr + (((g + 1) / 4) & 1) * 16384 + ((g + 1) % 4) * 4096, fb[(g + 1) & 1]);
+                read_b(bfr + (((g + 1) / 4) & 1) * 16384 + ((g + 1) % 4) * 4096, fb[(g + 1) & 1], fbx[(g + 1) & 1]);
             }
         }
     });
