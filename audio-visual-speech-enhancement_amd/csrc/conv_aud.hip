@@ -236,10 +236,13 @@ __global__ __launch_bounds__(NT, 1) void k_aud_enc(AudEncArgs a) {
             return __builtin_amdgcn_raw_buffer_load_b64(rsW, vbl + decltype(tt)::value * 128, csoff, 0);
         };
         auto st8 = [&](int addr, i32x2 v) { *reinterpret_cast<i32x2*>(lds + addr) = v; };
+        // fragment slots: 0..2 = fragments w, w + 8, w + 16 x all 64 channels; 3 = fragment 24 x channels 16 w .. + 15
+        // on waves 0..3 (100 fragment pairs, 13 / 12 per wave, instead of 4 x 4 slots with 28 pairs dropped)
+        const bool xw = w < 4;
         int vb[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const int f = (w + 8 * i < 25) ? w + 8 * i : 0;
+            const int f = i < 3 ? w + 8 * i : 24;
             const int y = 8 * (f / 5) + (r16 >> 1), x = 2 * (f % 5) + (r16 & 1);
             vb[i] = (y * P2 + x) * S2 + kg * 16;
         }
@@ -261,7 +264,7 @@ __global__ __launch_bounds__(NT, 1) void k_aud_enc(AudEncArgs a) {
             for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
         __syncthreads();
         STAMP_AT(3);
-        i32x4 fa[2][4], fb[2][4];
+        i32x4 fa[2][4], fb[2][4], fbx[2];
         int vq[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) vq[i] = vb[i];
@@ -269,14 +272,16 @@ __global__ __launch_bounds__(NT, 1) void k_aud_enc(AudEncArgs a) {
             constexpr int t = decltype(tt)::value % 16;
             constexpr int imm = ((t / 4) * P2 + t % 4) * S2;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) f[i] = lds16(lds + imm, vq[i]);
+            for (int i = 0; i < 3; ++i) f[i] = lds16(lds + imm, vq[i]);
+            if (xw) f[3] = lds16(lds + imm, vq[3]);
         };
-        auto read_b = [&](int base, i32x4 (&f)[4]) {
+        auto read_b = [&](int base, i32x4 (&f)[4], i32x4& fx) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) f[j] = lds16(lds, base + 1024 * j);
+            if (xw) fx = lds16(lds, base + 1024 * w);
         };
         read_a(std::integral_constant<int, 0>{}, fa[0]);
-        read_b(bfr, fb[0]);
+        read_b(bfr, fb[0], fbx[0]);
         for (int c = 0; c < 2; ++c) {
             const int cs = c * 64, cn = (c + 1 < 2 ? c + 1 : 0) * 64;
             unroll(std::make_integer_sequence<int, 16>{}, [&](auto tt) {
@@ -291,12 +296,13 @@ __global__ __launch_bounds__(NT, 1) void k_aud_enc(AudEncArgs a) {
                     for (int i = 0; i < 4; ++i) vq[i] = vb[i] + (c + 1) * W2BUF;   // past the last chunk: unused reads
                 }
                 read_a(std::integral_constant<int, t + 1>{}, fa[(t + 1) & 1]);
-                read_b(bfr + (((t + 1) / 4) & 1) * 16384 + ((t + 1) % 4) * 4096, fb[(t + 1) & 1]);
+                read_b(bfr + (((t + 1) / 4) & 1) * 16384 + ((t + 1) % 4) * 4096, fb[(t + 1) & 1], fbx[(t + 1) & 1]);
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                for (int i = 0; i < 4; ++i)
+                for (int i = 0; i < 3; ++i)
 #pragma unroll
                     for (int j = 0; j < 4; ++j) acc[i][j] = mfma(fb[t & 1][j], fa[t & 1][i], acc[i][j]);   // W x A
+                if (xw) acc[3][0] = mfma(fbx[t & 1], fa[t & 1][3], acc[3][0]);
             });
         }
         __syncthreads();   // every read of a_conv2's input done: a_conv3's image goes over it
@@ -307,15 +313,16 @@ __global__ __launch_bounds__(NT, 1) void k_aud_enc(AudEncArgs a) {
         // -> a_conv3's input, padded pixel (oy + 1, ox + 1), 8 x 2 fragment rows; lane = fragment row r16
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const int f = w + 8 * i;
-            if (f >= 25) continue;
+            if (i == 3 && !xw) continue;
+            const int f = i < 3 ? w + 8 * i : 24;
             const int y = 8 * (f / 5) + (r16 >> 1), x = 2 * (f % 5) + (r16 & 1);
             const int px = ((y + 1) * P3 + x + 1) * S3 + kg * 8;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
+            for (int j = 0; j < (i < 3 ? 4 : 1); ++j) {
+                const int jj = i < 3 ? j : w;   // channel block
                 f32x4 sc, sh;
-                bnq(1, 16 * j + 4 * kg, sc, sh);
-                st8l(px + 32 * j, bn_pack4(acc[i][j], sc, sh));
+                bnq(1, 16 * jj + 4 * kg, sc, sh);
+                st8l(px + 32 * jj, bn_pack4(acc[i][j], sc, sh));
             }
         }
         __syncthreads();
