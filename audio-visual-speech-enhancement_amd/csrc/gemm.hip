@@ -211,6 +211,8 @@ int gemm_ksplit(int M, int N, int kpad) {
     const int tiles = ((M + 127) / 128) * ((N + 127) / 128), nslab = kpad / 32;
     int ks = 256 / tiles;
     ks = ks > nslab / 8 ? nslab / 8 : ks;
+    const char* e = std::getenv("AVSE_GEMM_KSPLIT");   // A/B: cap the split (timing experiments)
+    if (e && std::atoi(e) > 0 && std::atoi(e) < ks) ks = std::atoi(e);
     return ks < 1 ? 1 : ks;
 }
 
