@@ -123,9 +123,22 @@ __global__ __launch_bounds__(NT, 1) void k_dec_head(DecHeadArgs a) {
         if constexpr ((ABL & 8) != 0) return (i32x4){s, 0, 0, 0};
         return __builtin_amdgcn_raw_buffer_load_b128(rs, brow * (G::KPAD * 2) + kq * 16, (p * 128 * G::KPAD + sl * 32) * 2, 0);
     };
+    // d_deconv1 / d_deconv2: wave w's own B fragment of slab s (rows 16 w + r16, k-group kg), straight from global
+    // memory — no wave shares it, so these layers skip the LDS ring and its barrier every two slabs
+    auto dpiece = [&](auto ll, auto ss) -> i32x4 {
+        constexpr int LL = decltype(ll)::value, s = decltype(ss)::value;
+        using G = Geo<LL>;
+        constexpr int sv = s < G::NP * G::NSL ? s : 0, p = sv / G::NSL, sl = sv % G::NSL;
+        const __amdgpu_buffer_rsrc_t& rs = LL == 1 ? rsW1 : rsW2;
+        return __builtin_amdgcn_raw_buffer_load_b128(rs, (16 * w + r16) * (G::KPAD * 2) + kg * 16,
+                                                     (p * 128 * G::KPAD + sl * 32) * 2, 0);
+    };
     auto prefetch = [&](auto ll) {
         Pre pr;
-        unroll(std::make_integer_sequence<int, DA + 2>{}, [&](auto k) { pr.w[decltype(k)::value] = piece(ll, k); });
+        unroll(std::make_integer_sequence<int, DA + 2>{}, [&](auto k) {
+            if constexpr (decltype(ll)::value <= 2) pr.w[decltype(k)::value] = dpiece(ll, k);
+            else pr.w[decltype(k)::value] = piece(ll, k);
+        });
         return pr;
     };
 
@@ -145,6 +158,7 @@ __global__ __launch_bounds__(NT, 1) void k_dec_head(DecHeadArgs a) {
         constexpr int LL = decltype(ll)::value;
         using G = Geo<LL>;
         constexpr bool WIDE = LL == 3;                 // waves split clips and N (d_deconv3) or N only
+        constexpr bool DIRECT = !WIDE;                 // B fragments per wave from global memory (see dpiece)
         constexpr int NI = WIDE ? G::NFR : NC * G::NFR, NJ = WIDE ? 2 : 1;
         const int row0 = WIDE ? 32 * nq : 16 * w;      // this wave's first output channel
         // fragment slot i: clip (WIDE ? mh : i / NFR), M fragment (WIDE ? i : i % NFR); lane row r16 -> grid
@@ -180,18 +194,24 @@ __global__ __launch_bounds__(NT, 1) void k_dec_head(DecHeadArgs a) {
             constexpr int imm = ((G::tap_dy(p, t) - G::DY0) * G::P + (G::tap_dx(p, t) - G::DX0)) * S + c * 64;
 #pragma unroll
             for (int i = 0; i < NI; ++i) fa[buf][i] = lds16(lds + imm, vb[i]);
+            if constexpr (!DIRECT)
 #pragma unroll
             for (int j = 0; j < NJ; ++j)
                 fb[buf][j] = lds16(lds, BOFF + (((s / 2) & 1) * 16384 + (s % 2) * 8192) + (row0 + 16 * j + r16) * 64 +
                                             ((kg ^ wsw(r16)) << 4));
         };
         constexpr int NS = G::NP * G::NSL;
-        // register ring: pb[s % DA] holds slab s + 2 at step s
-        i32x4 pb[DA];
+        // register ring: pb[s % DA] holds slab s + 2 at step s (LDS ring); pd[s % (DA + 2)] holds slab s (DIRECT)
+        i32x4 pb[DA], pd[DA + 2];
+        if constexpr (DIRECT) {
 #pragma unroll
-        for (int k = 0; k < DA; ++k) pb[k] = pre.w[k + 2];
-        st16(bst, pre.w[0]);
-        st16(bst + 8192, pre.w[1]);
+            for (int k = 0; k < DA + 2; ++k) pd[k] = pre.w[k];
+        } else {
+#pragma unroll
+            for (int k = 0; k < DA; ++k) pb[k] = pre.w[k + 2];
+            st16(bst, pre.w[0]);
+            st16(bst + 8192, pre.w[1]);
+        }
         zero_acc();
         __syncthreads();
         read(std::integral_constant<int, 0>{}, 0);
@@ -199,18 +219,24 @@ __global__ __launch_bounds__(NT, 1) void k_dec_head(DecHeadArgs a) {
             constexpr int s = decltype(ss)::value, p = s / G::NSL;
             constexpr bool last = (s + 1) % G::NSL == 0;
             __builtin_amdgcn_sched_barrier(0);
-            if constexpr (s + 2 < NS) {
-                st16(bst + (((s / 2) + 1) & 1) * 16384 + (s % 2) * 8192, pb[s % DA]);    // slab s + 2
-                if constexpr (s + 2 + DA < NS) pb[s % DA] = piece(ll, std::integral_constant<int, s + 2 + DA>{});
+            i32x4 fbd;
+            if constexpr (DIRECT) {
+                fbd = pd[s % (DA + 2)];
+                if constexpr (s + DA + 2 < NS) pd[s % (DA + 2)] = dpiece(ll, std::integral_constant<int, s + DA + 2>{});
+            } else {
+                if constexpr (s + 2 < NS) {
+                    st16(bst + (((s / 2) + 1) & 1) * 16384 + (s % 2) * 8192, pb[s % DA]);    // slab s + 2
+                    if constexpr (s + 2 + DA < NS) pb[s % DA] = piece(ll, std::integral_constant<int, s + 2 + DA>{});
+                }
+                if constexpr (s % 2 == 1 && !(ABL & 4)) __syncthreads();
             }
-            if constexpr (s % 2 == 1 && !(ABL & 4)) __syncthreads();
             if constexpr (s + 1 < NS && !last) read(std::integral_constant<int, s + 1>{}, (s + 1) & 1);
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int i = 0; i < NI; ++i)
 #pragma unroll
                 for (int j = 0; j < NJ; ++j)
-                    if constexpr (!(ABL & 1)) acc[i][j] = mfma(fb[s & 1][j], fa[s & 1][i], acc[i][j]);   // W x A
+                    if constexpr (!(ABL & 1)) acc[i][j] = mfma(DIRECT ? fbd : fb[s & 1][j], fa[s & 1][i], acc[i][j]);   // W x A
                     else acc[i][j][0] += __builtin_bit_cast(float, fa[s & 1][i][0] ^ fb[s & 1][j][0]);
             if constexpr (last) {
                 if constexpr (p + 1 == G::NP) {   // layer done: the next layer's first slabs load under this epilogue
