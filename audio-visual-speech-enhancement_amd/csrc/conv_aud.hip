@@ -156,7 +156,11 @@ __global__ __launch_bounds__(NT, 1) void k_aud_enc(AudEncArgs a) {
             for (int j = 0; j < 4; ++j) acc[i][j] = mfma(fb1[j], fa, (f32x4){0.f, 0.f, 0.f, 0.f});   // W x A
         }
         // -> a_conv2's input: chunk (n / 32) buffer, padded pixel (oy + 1, ox + 1); lane = pixel row r16,
-        // channels 16 j + 4 kg .. + 3
+        // channels 16 j + 4 kg .. + 3 (scale / shift quads read once per j: the stores in between are LDS stores,
+        // so the compiler could not reuse the reads)
+        f32x4 sc[4], sh[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bnq(0, 16 * j + 4 * kg, sc[j], sh[j]);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int f = w + 8 * i;
@@ -164,11 +168,7 @@ __global__ __launch_bounds__(NT, 1) void k_aud_enc(AudEncArgs a) {
             const int m = 16 * f + r16, oy = m / 10, ox = m - oy * 10;
             const int px = ((oy + 1) * P2 + ox + 1) * S2 + kg * 8;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                f32x4 sc, sh;
-                bnq(0, 16 * j + 4 * kg, sc, sh);
-                st8l(px + (j >> 1) * W2BUF + (j & 1) * 32, bn_pack4(acc[i][j], sc, sh));
-            }
+            for (int j = 0; j < 4; ++j) st8l(px + (j >> 1) * W2BUF + (j & 1) * 32, bn_pack4(acc[i][j], sc[j], sh[j]));
         }
     }
     __syncthreads();
@@ -311,18 +311,21 @@ __global__ __launch_bounds__(NT, 1) void k_aud_enc(AudEncArgs a) {
         zero(0, IMG3B);
         __syncthreads();
         // -> a_conv3's input, padded pixel (oy + 1, ox + 1), 8 x 2 fragment rows; lane = fragment row r16
+        f32x4 sc[4], sh[4], scx, shx;   // per channel block (read once; see a_conv1)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bnq(1, 16 * j + 4 * kg, sc[j], sh[j]);
+        bnq(1, 16 * (w & 3) + 4 * kg, scx, shx);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             if (i == 3 && !xw) continue;
             const int f = i < 3 ? w + 8 * i : 24;
             const int y = 8 * (f / 5) + (r16 >> 1), x = 2 * (f % 5) + (r16 & 1);
             const int px = ((y + 1) * P3 + x + 1) * S3 + kg * 8;
+            if (i < 3) {
 #pragma unroll
-            for (int j = 0; j < (i < 3 ? 4 : 1); ++j) {
-                const int jj = i < 3 ? j : w;   // channel block
-                f32x4 sc, sh;
-                bnq(1, 16 * jj + 4 * kg, sc, sh);
-                st8l(px + 32 * jj, bn_pack4(acc[i][j], sc, sh));
+                for (int j = 0; j < 4; ++j) st8l(px + 32 * j, bn_pack4(acc[i][j], sc[j], sh[j]));
+            } else {
+                st8l(px + 32 * w, bn_pack4(acc[3][0], scx, shx));   // channel block w
             }
         }
         __syncthreads();
