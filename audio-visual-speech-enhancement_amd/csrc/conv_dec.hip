@@ -257,8 +257,11 @@ __global__ __launch_bounds__(NT, 1) void k_dec_tail(DecTailArgs a) {
         __syncthreads();
         // epilogue: BN + LeakyReLU -> bf16 at image pixel (y + 1, x + 1); lane = block row r16, channels
         // 16 j + 4 kg .. + 3: one 8-B store per fragment pair (i, j)
-        auto st_quad = [&](int px, int j, const f32x4& v) {   // channels 16 j + 4 kg + e
-            const f32x4 sc = par4(PSC4, j), sh = par4(PSH4, j);
+        // BN quads read once per channel block (the interleaved LDS stores keep the compiler from reusing reads)
+        f32x4 sc4q[4], sh4q[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { sc4q[j] = par4(PSC4, j); sh4q[j] = par4(PSH4, j); }
+        auto st_quad = [&](int px, int j, const f32x4& v, const f32x4& sc, const f32x4& sh) {   // channels 16 j + 4 kg + e
             st8(px + 32 * j, pack4(bn_lrelu(v[0], sc[0], sh[0]), bn_lrelu(v[1], sc[1], sh[1]),
                                    bn_lrelu(v[2], sc[2], sh[2]), bn_lrelu(v[3], sc[3], sh[3])));
         };
@@ -270,9 +273,9 @@ __global__ __launch_bounds__(NT, 1) void k_dec_tail(DecTailArgs a) {
             const int px = ((y + 1) * P5 + x + 1) * S5 + 8 * kg;
             if (i < 3) {
 #pragma unroll
-                for (int j = 0; j < 4; ++j) st_quad(px, j, acc[i][j]);
+                for (int j = 0; j < 4; ++j) st_quad(px, j, acc[i][j], sc4q[j], sh4q[j]);
             } else {
-                st_quad(px, w, acc[3][0]);
+                st_quad(px, w, acc[3][0], par4(PSC4, w), par4(PSH4, w));
             }
         }
         __syncthreads();
