@@ -100,6 +100,14 @@ __global__ __launch_bounds__(NT, 1) void k_gemm(GemmArgs g) {
     f32x4 acc[4][2];
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    // epilogue scale / shift of this lane's two columns, loaded now (in the epilogue their latency was exposed)
+    float esc[2], esh[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int n = n0 + 32 * wn + 16 * j + r16;
+        esc[j] = n < g.N ? g.scale[n] : 0.f;
+        esh[j] = n < g.N ? g.shift[n] : 0.f;
+    }
 
     // prologue: slabs 0..3 -> slot 0, slabs 4..7 in registers
     i32x4 ra[4], rw[4];
@@ -179,7 +187,7 @@ __global__ __launch_bounds__(NT, 1) void k_gemm(GemmArgs g) {
     for (int j = 0; j < 2; ++j) {
         const int n = n0 + 32 * wn + 16 * j + r16;
         if (n >= g.N) continue;
-        const float sc = g.scale[n], sh = g.shift[n];
+        const float sc = esc[j], sh = esh[j];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int mb = m0 + 64 * wm + 16 * i + 4 * kg;
