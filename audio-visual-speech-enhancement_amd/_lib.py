@@ -5,6 +5,7 @@ torch first makes libavse share torch's HIP runtime (one set of streams / alloca
 
 There is no fallback: if libavse.so is missing or fails to load, every entry point raises.
 """
+import contextlib
 import ctypes
 import os
 import threading
@@ -35,6 +36,8 @@ SIGNATURES = {
     "avse_ctx_create": (_int, [_int, ctypes.POINTER(_c_void_p)]),
     "avse_ctx_destroy": (None, [_c_void_p]),
     "avse_ctx_reserve": (_int, [_c_void_p, _i64, _int]),
+    "avse_ctx_set_option": (_int, [_c_void_p, ctypes.c_char_p, _int]),
+    "avse_ctx_get_option": (_int, [_c_void_p, ctypes.c_char_p, ctypes.POINTER(_int)]),
     "avse_spectrogram": (_int, [_c_void_p, _c_void_p, _i64, _i64, _int, _int, _int, _int, _flt, _flt, _flt, _flt,
                                 _int, _int, _c_void_p, _c_void_p, _c_void_p]),
     "avse_istft": (_int, [_c_void_p, _c_void_p, _c_void_p, _i64, _int, _int, _int, _int, _int, _int, _int, _flt, _flt,
@@ -94,6 +97,27 @@ class Context:
 
     def reserve(self, max_clips, dtype):
         check(load().avse_ctx_reserve(self.handle, int(max_clips), int(dtype)), "avse_ctx_reserve")
+
+    def set_option(self, name, value):
+        """avse_ctx_set_option: a kernel-path switch (include/avse.h), e.g. "no_gemm"."""
+        check(load().avse_ctx_set_option(self.handle, name.encode(), int(value)), f"avse_ctx_set_option({name})")
+
+    def get_option(self, name):
+        v = _int()
+        check(load().avse_ctx_get_option(self.handle, name.encode(), ctypes.byref(v)), f"avse_ctx_get_option({name})")
+        return v.value
+
+    @contextlib.contextmanager
+    def options(self, **switches):
+        """Temporarily set kernel-path switches: `with ctx.options(no_gemm=1): ...`."""
+        old = {k: self.get_option(k) for k in switches}
+        try:
+            for k, v in switches.items():
+                self.set_option(k, v)
+            yield self
+        finally:
+            for k, v in old.items():
+                self.set_option(k, v)
 
     def __del__(self):
         h = getattr(self, "handle", None)

@@ -13,6 +13,27 @@ namespace avse {
 
 void set_error(const std::string& msg);
 
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) for `fn` on the CURRENT device, once per (kernel, device)
+// (thread-safe; capi.hip).  Every launcher that needs more than 64 KB of dynamic LDS calls it first.
+int ensure_lds_attr(const void* fn, int bytes);
+
+// Kernel-path switches of one context.  Defaults are the production path; every field exists for an A/B
+// experiment or a layer-by-layer parity test.  Initialised once from the AVSE_* environment at
+// avse_ctx_create, changed with avse_ctx_set_option; launch code never reads the environment.
+struct Options {
+    int no_gemm = 0;          // AVSE_NO_GEMM: v_conv6 + dense layers on k_conv + split-K reduce (not k_gemm)
+    int no_audenc = 0;        // AVSE_NO_AUDENC: audio encoder layer by layer (not k_aud_enc)
+    int no_dechead = 0;       // AVSE_NO_DECHEAD: d_deconv1..3 layer by layer (not k_dec_head)
+    int no_dectail = 0;       // AVSE_NO_DECTAIL: d_deconv4..6 layer by layer (not k_dec_tail)
+    int unfused_tail = 0;     // AVSE_UNFUSED_TAIL: d_deconv6 as its own kernel (d_deconv5 activation materialised)
+    int no_halo = 0;          // AVSE_NO_HALO: video convs on k_conv (read when weights are loaded)
+    int mfma32 = 0;           // AVSE_MFMA32: 32x32x16 compute waves in the stream convolutions
+    int serial = 0;           // AVSE_SERIAL: one stream for the whole forward
+    int aud_side = 0;         // AVSE_AUD_SIDE: fused audio encoder on the side stream
+    int graph = 0;            // AVSE_GRAPH: avse_forward replays a hipGraph per argument set
+    int gemm_ksplit_cap = 0;  // AVSE_GEMM_KSPLIT: cap k_gemm's split-K factor (0 = no cap)
+};
+
 #define AVSE_HIP_CHECK(expr)                                                                   \
     do {                                                                                       \
         hipError_t _e = (expr);                                                                \
@@ -118,7 +139,6 @@ struct ConvArgs {
 };
 
 int launch_conv(const ConvArgs& a, int dtype, hipStream_t s);
-int launch_splitk_reduce(const ConvArgs& a, int dtype, hipStream_t s);   // conv.hip: split-K tail
 
 // fused decoder tail d_deconv4 -> d_deconv5 -> d_deconv6, one workgroup per clip (conv_dec.hip, bf16)
 struct DecTailArgs {
@@ -191,24 +211,14 @@ struct GemmArgs {
     float* partial;          // [tiles][ksplit][128 x 128] fp32
     int* counters;           // [tiles], zero between launches
 };
-int gemm_ksplit(int M, int N, int kpad);
-size_t gemm_ws_bytes(int M, int N, int kpad);
+int gemm_ksplit(int M, int N, int kpad, int cap);   // cap > 0 limits the split (Options::gemm_ksplit_cap)
+size_t gemm_ws_bytes(int M, int N, int kpad, int cap);
 int launch_gemm(const GemmArgs& g, int mode, hipStream_t s);
 int launch_aud_enc(const AudEncArgs& a, hipStream_t s);
 int launch_dec_tail(const DecTailArgs& a, hipStream_t s);
-int launch_igemm(const ConvArgs& a, hipStream_t s);                      // igemm.hip (bf16)
-int choose_ksplit_ws(long long M, int Co, int kpad);                     // igemm.hip split-K choice
 
-// ---- halo-tiled video convolutions (conv_halo.hip), bf16 only ----------------------------
+// ---- tiled bf16 video convolutions: conv_v1r.hip (v_conv1), conv_stream.hip (v_conv2..v_conv5) ----
 enum HaloVariant { HALO_NONE = -1, HALO_V1 = 0, HALO_K5 = 1, HALO_K3_16 = 2, HALO_K3_8 = 3 };
-
-// K-slices (32 input channels x one tap; V1: 4 taps x 8 channels) processed per barrier step.
-constexpr int HALO_NT = 2;
-// K-slices per 128-channel group: 4 x taps (V1: ceil(taps/4)), taps padded to a multiple of HALO_NT.
-__host__ __device__ constexpr int halo_slices_per_group(int ks, bool v1) {
-    return v1 ? (((ks * ks + 3) / 4 + HALO_NT - 1) / HALO_NT) * HALO_NT
-              : 4 * ks * ks;   // (4 chunks of 32 channels) x taps; a multiple of HALO_NT for ks = 3, 5
-}
 
 struct HaloArgs {
     int variant;
@@ -217,26 +227,26 @@ struct HaloArgs {
     const float* vmean;      // nullable [Hc][Wc]               (V1)
     const float* vstd;
     void* out;               // bf16, pooled [N][Hc/2][Wc/2][Co] at (clip stride, pixel stride, channel offset)
-    const void* w;           // bf16 [step][Co][32]
-    const void* w2;          // V1 only: [5][Co][32] kernel-row packing (conv_v1r.hip)
+    const void* w;           // bf16 [step][Co][32] (V1: [5 kernel rows][Co][32], conv_v1r.hip)
     const float* scale;
     const float* shift;
     int N, Hc, Wc, Ci, Co;
     long long out_clip_stride;
     int out_pix_stride;
     int out_c_off;
+    int mfma32;              // conv_stream.hip: 1 = v_mfma_f32_32x32x16_bf16 compute waves (A/B variant)
     unsigned long long* prof;   // ablation harness only (ABL & 128): per-wave cycle counters, else unused
 };
 
-int launch_conv_halo(const HaloArgs& a, hipStream_t s);
 int launch_conv_stream(const HaloArgs& a, hipStream_t s);   // conv_stream.hip (non-V1 variants)
-int launch_conv_v1(const HaloArgs& a, hipStream_t s);       // conv_v1.hip (v_conv1, dense im2col)
 int launch_conv_v1r(const HaloArgs& a, hipStream_t s);      // conv_v1r.hip (v_conv1, kernel-row runs)
 int launch_video_prep(const float* video, const float* mean, const float* stdv, void* out, int64_t N,
                       int dtype, hipStream_t s);
 int launch_audio_prep(const float* audio, void* out, int64_t N, int dtype, hipStream_t s);
 int launch_out_conv(const void* in, const float* w64, float bias, float* out, int64_t npix, int dtype,
                     hipStream_t s);
+int launch_broadcast_row(const void* src, void* dst, int64_t rows, int64_t row_bytes, int64_t stride_bytes,
+                         hipStream_t s);
 int launch_video_normalize(float* video, int64_t S, int H, int W, int F, const float* mean,
                            const float* stdv, hipStream_t s);
 int launch_mse(const float* a, const float* b, int64_t n, float* loss, float* partial, hipStream_t s);

@@ -7,10 +7,11 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
+#include <set>
 #include <string>
+#include <utility>
 #include <vector>
-
-#include <unistd.h>   // environ
 
 #include "../../include/avse.h"
 #include "avse_common.h"
@@ -18,6 +19,18 @@
 namespace avse {
 static thread_local std::string g_err;
 void set_error(const std::string& msg) { g_err = msg; }
+
+int ensure_lds_attr(const void* fn, int bytes) {
+    static std::mutex mu;
+    static std::set<std::pair<const void*, int>> done;   // (kernel, device)
+    int dev = 0;
+    AVSE_HIP_CHECK(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lock(mu);
+    if (done.count({fn, dev})) return 0;
+    AVSE_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+    done.insert({fn, dev});
+    return 0;
+}
 }  // namespace avse
 
 using namespace avse;
@@ -153,6 +166,7 @@ struct IstftTables {
 
 struct avse_ctx {
     int device = 0;
+    Options opt;                // kernel-path switches (read from AVSE_* once, at creation)
     SpecTables spec;
     IstftTables istft;
     float* frames = nullptr;    // ISTFT frame scratch
@@ -160,6 +174,7 @@ struct avse_ctx {
     unsigned* umax = nullptr;
     int64_t umax_cap = 0;
     float* mse_partial = nullptr;
+    float* zero_video = nullptr;    // one all-zero [128][128][5] clip (video == NULL forwards)
     int* gemm_counters = nullptr;   // gemm.hip split-K tickets (zero between launches)
     char* arena = nullptr;
     size_t arena_bytes = 0;
@@ -170,7 +185,7 @@ struct avse_ctx {
     struct Graph {
         const void* key[8];
         int64_t n;
-        size_t env;
+        Options opt;
         hipGraphExec_t exec;
     };
     std::vector<Graph> graphs;
@@ -188,11 +203,30 @@ struct GpuLayer {
     float* shift = nullptr;
     int2* taps = nullptr;
     int halo = HALO_NONE;     // halo-tiled kernel variant (bf16 video convs)
-    void* w_halo = nullptr;   // bf16 packing for conv_stream.hip / conv_v1.hip (see build_layer)
-    void* w_halo2 = nullptr;  // v_conv1 only: [5 kernel rows][Cout][32] packing for conv_v1r.hip
+    void* w_halo = nullptr;   // bf16 packing for conv_stream.hip / conv_v1r.hip (see build_layer)
     void* w_dense = nullptr;  // a_conv1 only (bf16): [Cout][32], k = ky * kw + kx, for conv_aud.hip
     float* scale_h = nullptr; // |scale| for w_halo: channels with a negative BN scale have negated weights
     int2 htaps[MAX_TAPS * MAX_PHASES] = {};   // host copy of taps (conv_dec.hip's kernel arguments)
+};
+
+// avse_ctx_set_option names (and the AVSE_* variables that initialise them at avse_ctx_create)
+struct OptionName {
+    const char* name;
+    const char* env;
+    int Options::*field;
+};
+const OptionName kOptionNames[] = {
+    {"no_gemm", "AVSE_NO_GEMM", &Options::no_gemm},
+    {"no_audenc", "AVSE_NO_AUDENC", &Options::no_audenc},
+    {"no_dechead", "AVSE_NO_DECHEAD", &Options::no_dechead},
+    {"no_dectail", "AVSE_NO_DECTAIL", &Options::no_dectail},
+    {"unfused_tail", "AVSE_UNFUSED_TAIL", &Options::unfused_tail},
+    {"no_halo", "AVSE_NO_HALO", &Options::no_halo},
+    {"mfma32", "AVSE_MFMA32", &Options::mfma32},
+    {"serial", "AVSE_SERIAL", &Options::serial},
+    {"aud_side", "AVSE_AUD_SIDE", &Options::aud_side},
+    {"graph", "AVSE_GRAPH", &Options::graph},
+    {"gemm_ksplit_cap", "AVSE_GEMM_KSPLIT", &Options::gemm_ksplit_cap},
 };
 
 struct avse_weights {
@@ -202,8 +236,12 @@ struct avse_weights {
     GpuLayer layers[kNumLayers - 1];  // all but d_deconv6
     float* d6_w = nullptr;
     float d6_bias = 0.f;
+    // avse_forward with video == NULL (all-zero video input, BASELINE configs[2]): the video encoder's output is
+    // then the same 2048-vector for every clip — computed once on first use and broadcast into the concat rows
+    mutable void* vzero_emb = nullptr;
     std::vector<void*> allocs;
     ~avse_weights() {
+        (void)hipFree(vzero_emb);
         for (void* p : allocs) (void)hipFree(p);
     }
 };
@@ -233,37 +271,9 @@ const size_t kBufElems[B_COUNT] = {128 * 128 * 8, 80 * 20 * 8, 40 * 10 * 64, 40 
                                    4 * 4 * 512, 5248, 1312, 1312, 3200, 10 * 5 * 128, 20 * 5 * 128,
                                    40 * 10 * 128, 40 * 10 * 64, 80 * 20 * 64};
 
-// Split-K plan for a single-phase GEMM of M rows x Co columns x kpad: double the split while the
+// Split-K plan for a single-phase GEMM of M rows x Co columns x kpad on k_conv: double the split while the
 // grid stays <= ~1024 workgroups and every split keeps >= 16 k-slabs (64-byte slabs).
-// AVSE_IGEMM=1: run the bf16 generic layers on k_igemm (igemm.hip) instead of k_conv (conv.hip).
-// Opt-in while k_igemm's loader-bound K-slab is slower than k_conv on these shapes (r01 measurements).
-bool no_igemm() {
-    static const bool v = [] {
-        const char* e = std::getenv("AVSE_IGEMM");
-        return !(e && e[0] == '1');
-    }();
-    return v;
-}
-// AVSE_UNFUSED_TAIL=1 (read per forward, for the layer-by-layer tests): run d_deconv6 as its own kernel so the
-// 64-channel d_deconv5 activation is materialised in the scratch buffer avse_debug_scratch exposes
-// AVSE_SERIAL=1 (read per forward): run the audio branch on the caller's stream too
-bool serial_forward() {
-    const char* e = std::getenv("AVSE_SERIAL");
-    return e && e[0] == '1';
-}
-
-bool unfused_tail() {
-    const char* e = std::getenv("AVSE_UNFUSED_TAIL");
-    return e && e[0] == '1';
-}
-
-int run_conv(const ConvArgs& a, int dtype, hipStream_t s) {
-    if (dtype == AVSE_BF16 && !no_igemm() && a.Ci % 32 == 0 && !a.fuse_w) return launch_igemm(a, s);
-    return launch_conv(a, dtype, s);
-}
-
 int choose_ksplit(int64_t M, int Co, int kpad, int dtype) {
-    if (dtype == AVSE_BF16 && !no_igemm()) return choose_ksplit_ws(M, Co, kpad);
     const int BN = Co <= 64 ? 64 : 128;
     const int64_t tiles = ((M + 127) / 128) * ((Co + BN - 1) / BN);
     const int nslab = kpad / (dtype == AVSE_BF16 ? 32 : 16);
@@ -273,21 +283,21 @@ int choose_ksplit(int64_t M, int Co, int kpad, int dtype) {
 }
 
 // fp32 partial-sum workspace needed by the split-K layers (enc/dec dense, v_conv6) at batch N
-size_t split_ws_bytes(int64_t N, int dtype) {
+size_t split_ws_bytes(int64_t N, int dtype, const Options& o) {
     const struct { int64_t M; int Co, kpad; } g[4] = {{N, 1312, 5248}, {N, 1312, 1312}, {N, 3200, 1312}, {N * 16, 512, 4608}};
     size_t mx = 0;
     for (const auto& x : g) {
         const int ks = choose_ksplit(x.M, x.Co, x.kpad, dtype);
-        // k_conv's partials cover whole 128 x BN tiles (MFMA-native order), igemm's are [ks][M][Co]
+        // k_conv's partials cover whole 128 x BN tiles (MFMA-native order)
         const int bn = x.Co <= 64 ? 64 : 128;
         const size_t mp = (size_t)((x.M + 127) / 128) * 128, np = (size_t)((x.Co + bn - 1) / bn) * bn;
         if (ks > 1) mx = std::max(mx, (size_t)ks * mp * np * 4);
-        if (dtype == AVSE_BF16) mx = std::max(mx, gemm_ws_bytes((int)x.M, x.Co, x.kpad));   // gemm.hip's split-K
+        if (dtype == AVSE_BF16) mx = std::max(mx, gemm_ws_bytes((int)x.M, x.Co, x.kpad, o.gemm_ksplit_cap));   // gemm.hip's split-K
     }
     return mx;
 }
 
-size_t arena_bytes(int64_t clips, int dtype, size_t* offs) {
+size_t arena_bytes(int64_t clips, int dtype, const Options& o, size_t* offs) {
     const size_t es = dtype == AVSE_BF16 ? 2 : 4;
     size_t off = 0;
     for (int b = 0; b < B_COUNT; ++b) {
@@ -295,12 +305,12 @@ size_t arena_bytes(int64_t clips, int dtype, size_t* offs) {
         off += (kBufElems[b] * es * (size_t)clips + 255) & ~(size_t)255;
     }
     if (offs) offs[B_COUNT] = off;   // split-K partials
-    off += (split_ws_bytes(clips, dtype) + 255) & ~(size_t)255;
+    off += (split_ws_bytes(clips, dtype, o) + 255) & ~(size_t)255;
     return off;
 }
 
 int ensure_arena(avse_ctx* c, int64_t clips, int dtype) {
-    const size_t need = arena_bytes(clips, dtype, nullptr);
+    const size_t need = arena_bytes(clips, dtype, c->opt, nullptr);
     if (need <= c->arena_bytes) return 0;
     if (c->arena) (void)hipFree(c->arena);
     c->arena = nullptr;
@@ -418,7 +428,8 @@ int ensure_istft_tables(avse_ctx* c, int sr, int n_fft, int n_mels, double fmin,
 }
 
 // Build phase/tap tables + packed [Cout][Kpad] weights for one layer.
-int build_layer(avse_weights* W, const LayerDef& L, const float* kernel, const float* bias, const float* bn) {
+int build_layer(avse_weights* W, const LayerDef& L, const float* kernel, const float* bias, const float* bn,
+                const Options& opt) {
     GpuLayer& G = W->layers[&L - kLayers];
     G.def = L;
     const int CHUNK_ELEMS = 8;   // channel padding so a 16-B chunk never straddles a tap (bf16: 8)
@@ -540,9 +551,8 @@ int build_layer(avse_weights* W, const LayerDef& L, const float* kernel, const f
     for (size_t t = 0; t < taps.size() && t < (size_t)(MAX_TAPS * MAX_PHASES); ++t) G.htaps[t] = taps[t];
 
     // packing for the bf16 video conv kernels: conv_stream.hip [slice][Cout][32], slice = (cg*4 + cc)*KS^2
-    // + tap; conv_v1.hip (v_conv1) [Cout][128] in im2col order
-    const char* no_halo = std::getenv("AVSE_NO_HALO");   // A/B switch: force the generic kernel
-    if (W->dtype == AVSE_BF16 && L.kind == CONV && L.pool && L.hin >= 8 && !(no_halo && no_halo[0] == '1')) {
+    // + tap; conv_v1r.hip (v_conv1) [kernel row][Cout][32].  Options::no_halo keeps the generic k_conv.
+    if (W->dtype == AVSE_BF16 && L.kind == CONV && L.pool && L.hin >= 8 && !opt.no_halo) {
         const int ntap = L.kh * L.kw;
         if (L.cin == 5) G.halo = HALO_V1;
         else if (L.kh == 5) G.halo = HALO_K5;
@@ -559,13 +569,16 @@ int build_layer(avse_weights* W, const LayerDef& L, const float* kernel, const f
         if ((rc = upload(W, scale_h, &G.scale_h))) return rc;
         std::vector<uint16_t> hp;
         if (G.halo == HALO_V1) {
-            // conv_v1.hip: [Cout][128], dense im2col order k = tap * Cin + frame (125 real, zeros after)
-            hp.assign((size_t)L.cout * 128, 0);
-            for (int n = 0; n < L.cout; ++n)
-                for (int k = 0; k < ntap * L.cin; ++k)
-                    hp[(size_t)n * 128 + k] = f2bf(sgn[n] * kernel[(size_t)k * L.cout + n]);
+            // conv_v1r.hip: slice ky, k = kx * 6 + frame (frame 5 and k = 30, 31 zero)
+            hp.assign((size_t)L.kh * L.cout * 32, 0);
+            for (int ky = 0; ky < L.kh; ++ky)
+                for (int n = 0; n < L.cout; ++n)
+                    for (int kx = 0; kx < L.kw; ++kx)
+                        for (int f = 0; f < L.cin; ++f)
+                            hp[((size_t)ky * L.cout + n) * 32 + kx * 6 + f] =
+                                f2bf(sgn[n] * kernel[((size_t)(ky * L.kw + kx) * L.cin + f) * L.cout + n]);
         } else {
-            const int nsteps = (L.cin / 128) * halo_slices_per_group(L.kh, false);
+            const int nsteps = (L.cin / 128) * 4 * ntap;   // (4 chunks of 32 channels per 128) x taps
             hp.assign((size_t)nsteps * L.cout * 32, 0);
             for (int st = 0; st < nsteps; ++st)
                 for (int n = 0; n < L.cout; ++n)
@@ -579,25 +592,13 @@ int build_layer(avse_weights* W, const LayerDef& L, const float* kernel, const f
         uint16_t* d;
         if ((rc = upload(W, hp, &d))) return rc;
         G.w_halo = d;
-        if (G.halo == HALO_V1) {
-            // conv_v1r.hip: slice ky, k = kx * 6 + frame (frame 5 and k = 30, 31 zero)
-            std::vector<uint16_t> hr((size_t)L.kh * L.cout * 32, 0);
-            for (int ky = 0; ky < L.kh; ++ky)
-                for (int n = 0; n < L.cout; ++n)
-                    for (int kx = 0; kx < L.kw; ++kx)
-                        for (int f = 0; f < L.cin; ++f)
-                            hr[((size_t)ky * L.cout + n) * 32 + kx * 6 + f] =
-                                f2bf(sgn[n] * kernel[((size_t)(ky * L.kw + kx) * L.cin + f) * L.cout + n]);
-            uint16_t* d2;
-            if ((rc = upload(W, hr, &d2))) return rc;
-            G.w_halo2 = d2;
-        }
     }
     return 0;
 }
 
 HaloArgs halo_args(const GpuLayer& G, const void* in, const float* video, const float* vmean, const float* vstd,
-                   void* out, long long out_clip_stride, int out_pix_stride, int out_c_off, int64_t N) {
+                   void* out, long long out_clip_stride, int out_pix_stride, int out_c_off, int64_t N,
+                   const Options& opt) {
     HaloArgs a;
     std::memset(&a, 0, sizeof(a));
     a.variant = G.halo;
@@ -607,7 +608,7 @@ HaloArgs halo_args(const GpuLayer& G, const void* in, const float* video, const 
     a.vstd = vstd;
     a.out = out;
     a.w = G.w_halo;
-    a.w2 = G.w_halo2;
+    a.mfma32 = opt.mfma32;
     a.scale = G.scale_h;
     a.shift = G.shift;
     a.N = (int)N;
@@ -738,6 +739,10 @@ int avse_ctx_create(int device, avse_ctx** out) {
     AVSE_HIP_CHECK(hipSetDevice(device));
     avse_ctx* c = new avse_ctx();
     c->device = device;
+    for (const OptionName& o : kOptionNames) {
+        const char* e = std::getenv(o.env);
+        if (e && *e) c->opt.*(o.field) = std::atoi(e);
+    }
     if (hipMalloc((void**)&c->mse_partial, sizeof(float) * 256) != hipSuccess ||
         hipMalloc((void**)&c->gemm_counters, sizeof(int) * 8192) != hipSuccess ||
         hipMemset(c->gemm_counters, 0, sizeof(int) * 8192) != hipSuccess) {
@@ -759,6 +764,7 @@ void avse_ctx_destroy(avse_ctx* c) {
     (void)hipFree(c->frames);
     (void)hipFree(c->umax);
     (void)hipFree(c->mse_partial);
+    (void)hipFree(c->zero_video);
     (void)hipFree(c->arena);
     for (auto& g : c->graphs) (void)hipGraphExecDestroy(g.exec);
     if (c->cap) (void)hipStreamDestroy(c->cap);
@@ -766,6 +772,26 @@ void avse_ctx_destroy(avse_ctx* c) {
     if (c->fork) (void)hipEventDestroy(c->fork);
     if (c->join) (void)hipEventDestroy(c->join);
     delete c;
+}
+
+int avse_ctx_set_option(avse_ctx* c, const char* name, int value) {
+    if (!c || !name) return fail(AVSE_ERR_INVALID, "NULL argument");
+    for (const OptionName& o : kOptionNames)
+        if (std::strcmp(o.name, name) == 0) {
+            c->opt.*(o.field) = value;
+            return 0;
+        }
+    return fail(AVSE_ERR_INVALID, std::string("unknown option '") + name + "'");
+}
+
+int avse_ctx_get_option(avse_ctx* c, const char* name, int* value) {
+    if (!c || !name || !value) return fail(AVSE_ERR_INVALID, "NULL argument");
+    for (const OptionName& o : kOptionNames)
+        if (std::strcmp(o.name, name) == 0) {
+            *value = c->opt.*(o.field);
+            return 0;
+        }
+    return fail(AVSE_ERR_INVALID, std::string("unknown option '") + name + "'");
 }
 
 int avse_ctx_reserve(avse_ctx* c, int64_t max_clips, int dtype) {
@@ -897,7 +923,7 @@ int avse_weights_load(avse_ctx* c, const float* blob, int64_t n_floats, int dtyp
             W->d6_bias = bias[0];
             continue;
         }
-        int rc = build_layer(W, L, kernel, bias, bn);
+        int rc = build_layer(W, L, kernel, bias, bn, c->opt);
         if (rc) { delete W; return rc; }
     }
     *out = W;
@@ -916,8 +942,9 @@ namespace {
 // Stage order of avse_forward_profile (include/avse.h AVSE_NUM_STAGES).
 int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const float* video, const float* vmean,
                  const float* vstd, int64_t N, float* out, hipStream_t s, hipEvent_t* ev) {
-    if (!c || !W || !audio || !video || !out) return fail(AVSE_ERR_INVALID, "NULL argument");
+    if (!c || !W || !audio || !out) return fail(AVSE_ERR_INVALID, "NULL argument");
     if ((vmean == nullptr) != (vstd == nullptr)) return fail(AVSE_ERR_INVALID, "vnorm_mean and vnorm_std must both be set or both NULL");
+    if (!video && vmean) return fail(AVSE_ERR_INVALID, "video == NULL (all-zero video) takes no normaliser");
     if (N < 0 || N > (int64_t)(1 << 30) / (128 * 128)) return fail(AVSE_ERR_INVALID, "bad N");
     if (N == 0) return 0;
     if (W->device != c->device) return fail(AVSE_ERR_INVALID, "weights and context are on different devices");
@@ -926,17 +953,19 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
     if (rc) return rc;
     const int dt = W->dtype;
     size_t off[B_COUNT + 1];
-    arena_bytes(N, dt, off);
+    arena_bytes(N, dt, c->opt, off);
+    const Options& opt = c->opt;
     auto buf = [&](int b) { return (void*)(c->arena + off[b]); };
-    // dense layers and v_conv6 on gemm.hip (bf16; AVSE_NO_GEMM=1 keeps k_conv + split-K reduce)
-    const bool use_gemm = dt == AVSE_BF16 && !(std::getenv("AVSE_NO_GEMM") && std::getenv("AVSE_NO_GEMM")[0] == '1');
-    auto gemm = [&](const GpuLayer& G, const void* in, long long lda, void* outp, long long ldo, int out_off, int mode) {
+    // dense layers and v_conv6 on gemm.hip (bf16; Options::no_gemm keeps k_conv + split-K reduce)
+    const bool use_gemm = dt == AVSE_BF16 && !opt.no_gemm;
+    auto gemm = [&](const GpuLayer& G, const void* in, long long lda, void* outp, long long ldo, int out_off, int mode,
+                    int64_t n) {
         GemmArgs g;
         std::memset(&g, 0, sizeof(g));
         g.a = reinterpret_cast<const bf16_t*>(in);
         g.lda = lda;
         g.w = reinterpret_cast<const bf16_t*>(G.w);
-        g.M = (int)(mode == 1 ? N * 16 : N);
+        g.M = (int)(mode == 1 ? n * 16 : n);
         g.N = G.def.cout;
         g.kpad = G.ph[0].kpad;
         g.scale = G.scale;
@@ -945,7 +974,7 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
         g.out = reinterpret_cast<bf16_t*>(outp);
         g.ldo = ldo;
         g.out_off = out_off;
-        g.ksplit = gemm_ksplit(g.M, g.N, g.kpad);
+        g.ksplit = gemm_ksplit(g.M, g.N, g.kpad, opt.gemm_ksplit_cap);
         g.partial = reinterpret_cast<float*>(c->arena + off[B_COUNT]);
         g.counters = c->gemm_counters;
         return launch_gemm(g, mode, s);
@@ -963,9 +992,7 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
         ++stage;
         return 0;
     };
-    if ((rc = mark())) return rc;
-    // the halo-tiled v_conv1 reads the raw video and normalises it itself
-    if (L(5).halo == HALO_NONE && (rc = launch_video_prep(video, vmean, vstd, buf(B_VIN), N, dt, s))) return rc;
+    if ((rc = mark())) return rc;   // video_prep stage: now the video encoder's first launch (k_conv path only)
     if ((rc = mark())) return rc;
     // audio encoder (network.py:88-109): one fused kernel per clip (conv_aud.hip) when the layers have the network's
     // shapes (AVSE_NO_AUDENC=1: per-layer launches); profiled, its time shows as the audio_prep stage
@@ -986,7 +1013,7 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
         aa.w1 = (const bf16_t*)ws[0]; aa.w2 = (const bf16_t*)ws[1]; aa.w3 = (const bf16_t*)ws[2];
         aa.w4 = (const bf16_t*)ws[3]; aa.w5 = (const bf16_t*)ws[4];
         for (int i = 0; i < 5; ++i) { aa.sc[i] = L(i).scale; aa.sh[i] = L(i).shift; }
-        aud_fused = shapes && aud_enc_supported(aa);
+        aud_fused = shapes && !opt.no_audenc && aud_enc_supported(aa);
     }
 
     // The per-layer audio branch (prep + a_conv1..5 -> concat[0:3200]) shares no buffer with the video encoder until
@@ -996,9 +1023,8 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
     // The fused audio encoder runs on the caller's stream: beside the persistent video convolutions its 152-KB
     // workgroups hold whole CUs they wait for (measured: concurrent 2.377 ms vs serial 2.304 ms per step), and the
     // fork / join events alone cost ~25 us of idle GPU per step (rocprof trace); AVSE_AUD_SIDE=1 keeps the side stream.
-    const char* aud_side_env = std::getenv("AVSE_AUD_SIDE");
-    const bool aud_side = aud_side_env && aud_side_env[0] == '1';
-    const bool concurrent = ev == nullptr && !serial_forward() && (!aud_fused || aud_side);
+    const bool aud_side = opt.aud_side != 0;
+    const bool concurrent = ev == nullptr && !opt.serial && (!aud_fused || aud_side);
     hipStream_t sa = s;
     if (concurrent) {
         if (!c->side) {
@@ -1022,47 +1048,83 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
         const long long in_cs = (long long)G.def.hin * G.def.win * (i == 0 ? G.cin_pad : G.def.cin);
         ConvArgs a = (i < 4) ? conv_args(G, buf(a_in[i]), in_cs, buf(a_in[i + 1]), (long long)G.ho * G.wo * G.def.cout, G.def.cout, 0, N)
                              : conv_args(G, buf(a_in[i]), in_cs, buf(B_CAT), 5248, G.def.cout, 0, N);   // Flatten -> concat[0:3200]
-        if ((rc = run_conv(a, dt, sa)) || (rc = mark())) return rc;
+        if ((rc = launch_conv(a, dt, sa)) || (rc = mark())) return rc;
     }
     if (concurrent) AVSE_HIP_CHECK(hipEventRecord(c->join, sa));
-    // video encoder (network.py:138-175)
-    const int v_in[6] = {B_VIN, B_V1, B_V2, B_V3, B_V4, B_V5};
-    for (int i = 0; i < 6; ++i) {
-        const GpuLayer& G = L(5 + i);
-        if (G.halo != HALO_NONE) {
-            HaloArgs h = (i < 5) ? halo_args(G, buf(v_in[i]), video, vmean, vstd, buf(v_in[i + 1]),
-                                             (long long)G.ho * G.wo * G.def.cout, G.def.cout, 0, N)
-                                 : halo_args(G, buf(v_in[i]), video, vmean, vstd, buf(B_CAT), 5248, G.def.cout, 3200, N);
-            if ((rc = launch_conv_halo(h, s)) || (rc = mark())) return rc;
-            continue;
+    // video encoder (network.py:138-175) over n clips, activations at the arena offsets o, embedding into cat
+    auto video_encoder = [&](const float* vid, const float* vm, const float* vs, int64_t n, const size_t* o,
+                             void* cat) -> int {
+        auto vb = [&](int b) { return (void*)(c->arena + o[b]); };
+        const int v_in[6] = {B_VIN, B_V1, B_V2, B_V3, B_V4, B_V5};
+        if (L(5).halo == HALO_NONE && (rc = launch_video_prep(vid, vm, vs, vb(B_VIN), n, dt, s))) return rc;
+        for (int i = 0; i < 6; ++i) {
+            const GpuLayer& G = L(5 + i);
+            if (G.halo != HALO_NONE) {
+                HaloArgs h = (i < 5) ? halo_args(G, vb(v_in[i]), vid, vm, vs, vb(v_in[i + 1]),
+                                                 (long long)G.ho * G.wo * G.def.cout, G.def.cout, 0, n, opt)
+                                     : halo_args(G, vb(v_in[i]), vid, vm, vs, cat, 5248, G.def.cout, 3200, n, opt);
+                rc = G.halo == HALO_V1 ? launch_conv_v1r(h, s) : launch_conv_stream(h, s);
+                if (rc || (rc = mark())) return rc;
+                continue;
+            }
+            const long long in_cs = (long long)G.def.hin * G.def.win * (i == 0 ? G.cin_pad : G.def.cin);
+            if (i == 5 && use_gemm && G.def.hin == 4 && G.def.win == 4 && G.def.cin == 512 && G.def.kh == 3 && G.def.pool &&
+                G.ph[0].kpad == 9 * 512) {
+                if ((rc = gemm(G, vb(v_in[i]), in_cs, cat, 5248, 3200, 1, n)) || (rc = mark())) return rc;   // concat[3200:5248]
+                continue;
+            }
+            ConvArgs a = (i < 5) ? conv_args(G, vb(v_in[i]), in_cs, vb(v_in[i + 1]), (long long)G.ho * G.wo * G.def.cout, G.def.cout, 0, n)
+                                 : conv_args(G, vb(v_in[i]), in_cs, cat, 5248, G.def.cout, 3200, n);  // concat[3200:5248]
+            if (i == 5) split(a);
+            if ((rc = launch_conv(a, dt, s)) || (rc = mark())) return rc;
         }
-        const long long in_cs = (long long)G.def.hin * G.def.win * (i == 0 ? G.cin_pad : G.def.cin);
-        if (i == 5 && use_gemm && G.def.hin == 4 && G.def.win == 4 && G.def.cin == 512 && G.def.kh == 3 && G.def.pool &&
-            G.ph[0].kpad == 9 * 512) {
-            if ((rc = gemm(G, buf(v_in[i]), in_cs, buf(B_CAT), 5248, 3200, 1)) || (rc = mark())) return rc;   // concat[3200:5248]
-            continue;
+        return 0;
+    };
+    if (video) {
+        if ((rc = video_encoder(video, vmean, vstd, N, off, buf(B_CAT)))) return rc;
+    } else {
+        // all-zero video: the embedding is one constant 2048-vector, computed once per weights object (clip 0 of an
+        // N = 1 run whose activations use the N = 1 arena layout, stream-ordered before this forward's buffers)
+        const size_t es = dt == AVSE_BF16 ? 2 : 4;
+        if (!W->vzero_emb) {
+            if (!c->zero_video) {
+                AVSE_HIP_CHECK(hipMalloc((void**)&c->zero_video, sizeof(float) * 128 * 128 * 5));
+                AVSE_HIP_CHECK(hipMemsetAsync(c->zero_video, 0, sizeof(float) * 128 * 128 * 5, s));
+            }
+            void* emb = nullptr;
+            AVSE_HIP_CHECK(hipMalloc(&emb, 2048 * es));
+            size_t o1[B_COUNT + 1];
+            arena_bytes(1, dt, opt, o1);
+            hipEvent_t* keep = ev;
+            const int keep_stage = stage;
+            ev = nullptr;   // the one-off N = 1 encoder is not a profiled stage
+            rc = video_encoder(c->zero_video, nullptr, nullptr, 1, o1, c->arena + o1[B_CAT]);
+            ev = keep;
+            stage = keep_stage;
+            if (rc) { (void)hipFree(emb); return rc; }
+            AVSE_HIP_CHECK(hipMemcpyAsync(emb, c->arena + o1[B_CAT] + 3200 * es, 2048 * es, hipMemcpyDeviceToDevice, s));
+            W->vzero_emb = emb;
         }
-        ConvArgs a = (i < 5) ? conv_args(G, buf(v_in[i]), in_cs, buf(v_in[i + 1]), (long long)G.ho * G.wo * G.def.cout, G.def.cout, 0, N)
-                             : conv_args(G, buf(v_in[i]), in_cs, buf(B_CAT), 5248, G.def.cout, 3200, N);  // concat[3200:5248]
-        if (i == 5) split(a);
-        if ((rc = run_conv(a, dt, s)) || (rc = mark())) return rc;
+        if ((rc = launch_broadcast_row(W->vzero_emb, (char*)buf(B_CAT) + 3200 * es, N, 2048 * es, 5248 * es, s))) return rc;
+        for (int k = 0; k < 6; ++k)
+            if ((rc = mark())) return rc;   // v_conv1..v_conv6 stages (the broadcast shows as v_conv1)
     }
     if (concurrent) AVSE_HIP_CHECK(hipStreamWaitEvent(s, c->join, 0));
     // fusion + decoder dense (network.py:53-58, :66-78)
     if (use_gemm) {
-        if ((rc = gemm(L(11), buf(B_CAT), 5248, buf(B_E1), 1312, 0, 0)) || (rc = mark())) return rc;
-        if ((rc = gemm(L(12), buf(B_E1), 1312, buf(B_E2), 1312, 0, 0)) || (rc = mark())) return rc;
-        if ((rc = gemm(L(13), buf(B_E2), 1312, buf(B_E3), 3200, 0, 0)) || (rc = mark())) return rc;
+        if ((rc = gemm(L(11), buf(B_CAT), 5248, buf(B_E1), 1312, 0, 0, N)) || (rc = mark())) return rc;
+        if ((rc = gemm(L(12), buf(B_E1), 1312, buf(B_E2), 1312, 0, 0, N)) || (rc = mark())) return rc;
+        if ((rc = gemm(L(13), buf(B_E2), 1312, buf(B_E3), 3200, 0, 0, N)) || (rc = mark())) return rc;
     } else {
         ConvArgs a = conv_args(L(11), buf(B_CAT), 5248, buf(B_E1), 1312, 1312, 0, N);
         split(a);
-        if ((rc = run_conv(a, dt, s)) || (rc = mark())) return rc;
+        if ((rc = launch_conv(a, dt, s)) || (rc = mark())) return rc;
         a = conv_args(L(12), buf(B_E1), 1312, buf(B_E2), 1312, 1312, 0, N);
         split(a);
-        if ((rc = run_conv(a, dt, s)) || (rc = mark())) return rc;
+        if ((rc = launch_conv(a, dt, s)) || (rc = mark())) return rc;
         a = conv_args(L(13), buf(B_E2), 1312, buf(B_E3), 3200, 3200, 0, N);
         split(a);
-        if ((rc = run_conv(a, dt, s)) || (rc = mark())) return rc;
+        if ((rc = launch_conv(a, dt, s)) || (rc = mark())) return rc;
     }
     // audio decoder (network.py:112-135)
     const int d_in[6] = {B_E3, B_D1, B_D2, B_D3, B_D4, B_D5};
@@ -1096,13 +1158,13 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
             ha.N = (int)N;
             ha.w1 = (const bf16_t*)L(14).w; ha.w2 = (const bf16_t*)L(15).w; ha.w3 = (const bf16_t*)L(16).w;
             for (int k = 0; k < 3; ++k) { ha.sc[k] = L(14 + k).scale; ha.sh[k] = L(14 + k).shift; }
-            if (shapes && dec_head_supported(ha)) {
+            if (shapes && !opt.no_dechead && dec_head_supported(ha)) {
                 if ((rc = launch_dec_head(ha, s)) || (rc = mark()) || (rc = mark()) || (rc = mark())) return rc;
                 i = 2;   // continue with d_deconv4
                 continue;
             }
         }
-        if (i == 3 && dt == AVSE_BF16 && !unfused_tail()) {
+        if (i == 3 && dt == AVSE_BF16 && !opt.unfused_tail && !opt.no_dectail) {
             // d_deconv4 + d_deconv5 + d_deconv6 in one kernel, one workgroup per clip (conv_dec.hip)
             const DecTailArgs da = dec_tail_args(L(17), L(18), W, buf(d_in[3]), out, N);
             if (dec_tail_supported(da)) {
@@ -1110,20 +1172,20 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
                 break;
             }
         }
-        if (i == 4 && !unfused_tail()) {
+        if (i == 4 && !opt.unfused_tail) {
             // d_deconv5 with d_deconv6 (1x1, 64 -> 1, network.py:133) fused into its epilogue: the 64-channel
             // [N, 80, 20] activation is never written; orow addresses the float output pixel directly
             ConvArgs a = conv_args(G, buf(d_in[i]), in_cs, nullptr, (long long)G.ho * G.wo, 1, 0, N);
             a.fuse_w = W->d6_w;
             a.fuse_bias = W->d6_bias;
             a.fuse_out = out;
-            if ((rc = run_conv(a, dt, s)) || (rc = mark())) return rc;
+            if ((rc = launch_conv(a, dt, s)) || (rc = mark())) return rc;
             continue;
         }
         ConvArgs a = conv_args(G, buf(d_in[i]), in_cs, buf(d_in[i + 1]), (long long)G.ho * G.wo * G.def.cout, G.def.cout, 0, N);
-        if ((rc = run_conv(a, dt, s)) || (rc = mark())) return rc;
+        if ((rc = launch_conv(a, dt, s)) || (rc = mark())) return rc;
     }
-    if (unfused_tail()) {
+    if (opt.unfused_tail) {
         if ((rc = launch_out_conv(buf(B_D5), W->d6_w, W->d6_bias, out, N * 80 * 20, dt, s)) || (rc = mark())) return rc;
     } else if ((rc = mark())) {   // d_deconv6: fused into d_deconv5 above
         return rc;
@@ -1135,7 +1197,7 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
 extern "C" {
 
 // avse_forward replays a hipGraph of the forward once the same arguments (weights, input / output pointers, N, the
-// context's scratch arena and every AVSE_* environment switch) come a second time: the first call launches directly,
+// context's scratch arena and its Options) come a second time: the first call launches directly,
 // the second captures and launches the graph, later ones replay it — the ~15 kernels then run without the per-kernel
 // dispatch gaps of stream launches.  The graph bakes the pointers in; every argument set has its own entry (at most 8
 // are kept).  Opt-in (AVSE_GRAPH=1): a torch graph of the whole bench step (spectrogram + forward) measured 2.20 ->
@@ -1143,21 +1205,17 @@ extern "C" {
 // direct (bench.py A/B, same box), so direct launches stay the default.
 int avse_forward(avse_ctx* c, const avse_weights* W, const float* audio, const float* video, const float* vmean,
                  const float* vstd, int64_t N, float* out, void* stream) {
-    const char* ge = std::getenv("AVSE_GRAPH");
-    if (!c || !W || N <= 0 || !(ge && ge[0] == '1'))
+    if (!c || !W || N <= 0 || !c->opt.graph)
         return forward_impl(c, W, audio, video, vmean, vstd, N, out, (hipStream_t)stream, nullptr);
     AVSE_HIP_CHECK(hipSetDevice(c->device));
     if (W->device != c->device) return fail(AVSE_ERR_INVALID, "weights and context are on different devices");
     int rc = ensure_arena(c, N, W->dtype);   // no allocation inside the capture
     if (rc) return rc;
-    size_t env = 1469598103934665603ull;     // FNV-1a over the AVSE_* switches the launch code reads
-    for (char** e = environ; e && *e; ++e)
-        if (std::strncmp(*e, "AVSE_", 5) == 0)
-            for (const char* q = *e; *q; ++q) env = (env ^ (unsigned char)*q) * 1099511628211ull;
     const void* key[8] = {(const void*)W->serial, audio, video, vmean, vstd, out, c->arena, (const void*)c->arena_bytes};
     avse_ctx::Graph* hit = nullptr;
     for (auto& g : c->graphs)
-        if (g.n == N && g.env == env && std::memcmp(g.key, key, sizeof(key)) == 0) hit = &g;
+        if (g.n == N && std::memcmp(&g.opt, &c->opt, sizeof(Options)) == 0 && std::memcmp(g.key, key, sizeof(key)) == 0)
+            hit = &g;
     if (hit && hit->exec) {
         AVSE_HIP_CHECK(hipGraphLaunch(hit->exec, (hipStream_t)stream));
         return 0;
@@ -1172,7 +1230,7 @@ int avse_forward(avse_ctx* c, const avse_weights* W, const float* audio, const f
         avse_ctx::Graph g;
         std::memcpy(g.key, key, sizeof(key));
         g.n = N;
-        g.env = env;
+        g.opt = c->opt;
         g.exec = nullptr;
         c->graphs.push_back(g);
         return forward_impl(c, W, audio, video, vmean, vstd, N, out, (hipStream_t)stream, nullptr);
@@ -1233,7 +1291,7 @@ int avse_mse(avse_ctx* c, const float* pred, const float* target, int64_t n, flo
 int avse_debug_scratch(avse_ctx* c, int64_t N, int dtype, void** base, int64_t* offsets) {
     if (!c || !base || !offsets || N <= 0) return fail(AVSE_ERR_INVALID, "bad debug_scratch args");
     size_t off[B_COUNT + 1];
-    const size_t need = arena_bytes(N, dtype, off);
+    const size_t need = arena_bytes(N, dtype, c->opt, off);
     if (!c->arena || need > c->arena_bytes) return fail(AVSE_ERR_INVALID, "no forward scratch of that size yet");
     *base = c->arena;
     for (int b = 0; b < B_COUNT; ++b) offsets[b] = (int64_t)off[b];

@@ -413,43 +413,6 @@ __global__ __launch_bounds__(256, (conv_occupancy<BN, FAST>())) void k_conv(Conv
     }
 }
 
-// split-K tail: sum the partial slabs, then scale/shift, [2x2 max pool], LeakyReLU, strided store.
-// One thread per (output pixel, channel); single phase (dense layers, forward convs).
-template <typename T>
-__global__ void k_splitk_reduce(ConvArgs a) {
-    const int M = a.N * a.Hq * a.Wq;
-    const int Mo = a.pool ? M / 4 : M;
-    const long long total = (long long)Mo * a.Co;
-    T* out = reinterpret_cast<T*>(a.out);
-    for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total; idx += (long long)gridDim.x * blockDim.x) {
-        const int n = (int)(idx % a.Co);
-        const int p = (int)(idx / a.Co);
-        const float sc = a.scale[n], sh = a.shift[n];
-        float x = -INFINITY;
-        const int nr = a.pool ? 4 : 1;
-        for (int r = 0; r < nr; ++r) {
-            const int m = a.pool ? 4 * p + r : p;
-            float acc = 0.f;
-            for (int z = 0; z < a.ksplit; ++z) acc += a.partial[((size_t)z * M + m) * a.Co + n];
-            x = fmaxf(x, acc * sc + sh);
-        }
-        if (a.act) x = x >= 0.f ? x : LRELU * x;
-        long long o;
-        if (a.pool) {
-            const int pw = a.Wq >> 1, phh = a.Hq >> 1;
-            const int clip = p / (phh * pw);
-            const int rr = p - clip * phh * pw;
-            o = clip * a.out_clip_stride + (long long)rr * a.out_pix_stride + a.out_c_off + n;
-        } else {
-            const int clip = p / (a.Hq * a.Wq);
-            const int rr = p - clip * a.Hq * a.Wq;
-            const int oy = (rr / a.Wq) * a.oys, ox = (rr % a.Wq) * a.oxs;
-            o = clip * a.out_clip_stride + (long long)(oy * a.Wo + ox) * a.out_pix_stride + a.out_c_off + n;
-        }
-        out[o] = from_f<T>(x);
-    }
-}
-
 // split-K tail for k_conv's MFMA-native partials: one thread per f32x4 unit (4 rows of one column of one
 // fragment), summed over the splits, then scale/shift, [2x2 max pool: the 4 rows are one window],
 // LeakyReLU, strided store.  Single phase (dense layers, v_conv6).
@@ -586,12 +549,6 @@ inline unsigned grid_for(long long n, int block) {
 
 }  // namespace
 
-// AVSE_SLOW_CONV=1: force the generic (per-slab tap decode) k_conv path — A/B switch and test coverage
-bool no_fast_conv() {
-    const char* e = std::getenv("AVSE_SLOW_CONV");
-    return e && e[0] == '1';
-}
-
 int launch_conv(const ConvArgs& a, int dtype, hipStream_t s) {
     const int M = a.N * a.Hq * a.Wq;
     const int BN = (a.Co <= 64) ? 64 : 128;
@@ -609,7 +566,7 @@ int launch_conv(const ConvArgs& a, int dtype, hipStream_t s) {
             return 3;
         }
     dim3 grid((M + BM - 1) / BM, (a.Co + BN - 1) / BN, a.nphase * a.ksplit);
-    const bool fast = a.Ci % (dtype == 1 ? 32 : 16) == 0 && !no_fast_conv();
+    const bool fast = a.Ci % (dtype == 1 ? 32 : 16) == 0;   // else the per-slab tap decode (a_conv1, v_conv1)
     if (dtype == 1) {
         if (fast) {
             if (BN == 64) hipLaunchKernelGGL((k_conv<bf16_t, 64, true>), grid, dim3(256), 0, s, a);
@@ -643,12 +600,22 @@ int launch_conv(const ConvArgs& a, int dtype, hipStream_t s) {
     return 0;
 }
 
-// row-major [ksplit][M][Co] partials (igemm.hip's split-K)
-int launch_splitk_reduce(const ConvArgs& a, int dtype, hipStream_t s) {
-    const int M = a.N * a.Hq * a.Wq;
-    const long long total = (long long)(a.pool ? M / 4 : M) * a.Co;
-    if (dtype == 1) hipLaunchKernelGGL(k_splitk_reduce<bf16_t>, dim3(grid_for(total, 256)), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL(k_splitk_reduce<float>, dim3(grid_for(total, 256)), dim3(256), 0, s, a);
+// dst[r * stride + j] = src[j] for r < rows, j < row_bytes (16-B units when every address and size allows)
+__global__ void k_broadcast_row(const char* __restrict__ src, char* __restrict__ dst, long long rows, long long row_bytes,
+                                long long stride, int vec) {
+    const long long units = row_bytes / vec, total = rows * units;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+        const long long r = i / units, j = (i - r * units) * vec;
+        if (vec == 16) *reinterpret_cast<i32x4*>(dst + r * stride + j) = *reinterpret_cast<const i32x4*>(src + j);
+        else dst[r * stride + j] = src[j];
+    }
+}
+
+int launch_broadcast_row(const void* src, void* dst, int64_t rows, int64_t row_bytes, int64_t stride_bytes, hipStream_t s) {
+    const bool v16 = ((uintptr_t)src % 16 == 0) && ((uintptr_t)dst % 16 == 0) && row_bytes % 16 == 0 && stride_bytes % 16 == 0;
+    const int vec = v16 ? 16 : 1;
+    hipLaunchKernelGGL(k_broadcast_row, dim3(grid_for(rows * (row_bytes / vec), 256)), dim3(256), 0, s, (const char*)src,
+                       (char*)dst, (long long)rows, (long long)row_bytes, (long long)stride_bytes, vec);
     AVSE_HIP_CHECK(hipGetLastError());
     return 0;
 }

@@ -418,17 +418,11 @@ __global__ __launch_bounds__(NT, 1) void k_aud_enc(AudEncArgs a) {
 #undef STAMP_AT
 
 bool aud_enc_supported(const AudEncArgs& a) {
-    const char* e = std::getenv("AVSE_NO_AUDENC");
-    if (e && e[0] == '1') return false;
     return a.N > 0 && a.w1 && a.w2 && a.w3 && a.w4 && a.w5;
 }
 
 int launch_aud_enc(const AudEncArgs& a, hipStream_t s) {
-    static bool attr = false;
-    if (!attr) {
-        AVSE_HIP_CHECK(hipFuncSetAttribute((const void*)k_aud_enc<0>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
-        attr = true;
-    }
+    if (int rc = ensure_lds_attr((const void*)k_aud_enc<0>, LDS_BYTES)) return rc;
     hipLaunchKernelGGL(k_aud_enc<0>, dim3(a.N), dim3(NT), LDS_BYTES, s, a);
     AVSE_HIP_CHECK(hipGetLastError());
     return 0;

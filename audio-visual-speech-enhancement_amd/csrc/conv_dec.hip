@@ -398,8 +398,6 @@ __global__ __launch_bounds__(NT, 1) void k_dec_tail(DecTailArgs a) {
 }  // namespace
 
 bool dec_tail_supported(const DecTailArgs& a) {
-    const char* e = std::getenv("AVSE_NO_DECTAIL");
-    if (e && e[0] == '1') return false;
     // the compile-time geometry above: window / image extents and tap grids of network.py's layers
     if (a.N <= 0 || a.nt4 != 16 || a.kpad4 != 16 * CI4 || a.dy4 != 1 || a.dx4 != 1 || a.nx4 != 4) return false;
     if (a.pt4 != 2 || a.pl4 != 2 || a.rows4 != 43 || a.pitch4 > P4 || a.pt5 != 1 || a.pl5 != 1 || a.rows5 != 42 || a.pitch5 > P5)
@@ -412,11 +410,7 @@ bool dec_tail_supported(const DecTailArgs& a) {
 }
 
 int launch_dec_tail(const DecTailArgs& a, hipStream_t s) {
-    static bool attr = false;
-    if (!attr) {
-        AVSE_HIP_CHECK(hipFuncSetAttribute((const void*)k_dec_tail, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
-        attr = true;
-    }
+    if (int rc = ensure_lds_attr((const void*)k_dec_tail, LDS_BYTES)) return rc;
     hipLaunchKernelGGL(k_dec_tail, dim3(a.N), dim3(NT), LDS_BYTES, s, a);
     AVSE_HIP_CHECK(hipGetLastError());
     return 0;

@@ -291,17 +291,11 @@ __global__ __launch_bounds__(NT, 1) void k_dec_head(DecHeadArgs a) {
 }  // namespace
 
 bool dec_head_supported(const DecHeadArgs& a) {
-    const char* e = std::getenv("AVSE_NO_DECHEAD");
-    if (e && e[0] == '1') return false;
     return a.N > 0 && a.w1 && a.w2 && a.w3;
 }
 
 int launch_dec_head(const DecHeadArgs& a, hipStream_t s) {
-    static bool attr = false;
-    if (!attr) {
-        AVSE_HIP_CHECK(hipFuncSetAttribute((const void*)k_dec_head<0>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
-        attr = true;
-    }
+    if (int rc = ensure_lds_attr((const void*)k_dec_head<0>, LDS_BYTES)) return rc;
     hipLaunchKernelGGL(k_dec_head<0>, dim3((a.N + NC - 1) / NC), dim3(NT), LDS_BYTES, s, a);
     AVSE_HIP_CHECK(hipGetLastError());
     return 0;

@@ -594,12 +594,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
 template <int KS, int TH, int TW, int NCLIP, bool M16>
 int launch_stream(const HaloArgs& a, hipStream_t s) {
     using G = StreamGeom<KS, TH, TW, NCLIP>;
-    static bool attr = false;
-    if (!attr) {
-        AVSE_HIP_CHECK(hipFuncSetAttribute((const void*)k_conv_stream<KS, TH, TW, NCLIP, M16>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS + 1024));
-        attr = true;
-    }
+    if (int rc = ensure_lds_attr((const void*)k_conv_stream<KS, TH, TW, NCLIP, M16>, G::LDS + 1024)) return rc;
     if (a.Hc % TH || a.Wc % TW || a.Co % 128 || a.Ci % 64) {   // an even number of 32-channel chunks
         set_error("stream conv: tile does not divide the layer");
         return 3;
@@ -620,14 +615,8 @@ int launch_stream(const HaloArgs& a, hipStream_t s) {
 
 }  // namespace
 
-// AVSE_MFMA32=1 (read per launch): the v_mfma_f32_32x32x16_bf16 compute waves (A/B switch)
-static bool use_mfma32() {
-    const char* e = std::getenv("AVSE_MFMA32");
-    return e && e[0] == '1';
-}
-
 int launch_conv_stream(const HaloArgs& a, hipStream_t s) {
-    const bool m32 = use_mfma32();
+    const bool m32 = a.mfma32 != 0;   // v_mfma_f32_32x32x16_bf16 compute waves (A/B variant, Options::mfma32)
     switch (a.variant) {
         case HALO_K5: return m32 ? launch_stream<5, 16, 16, 1, false>(a, s) : launch_stream<5, 16, 16, 1, true>(a, s);
         case HALO_K3_16: return m32 ? launch_stream<3, 16, 16, 1, false>(a, s) : launch_stream<3, 16, 16, 1, true>(a, s);

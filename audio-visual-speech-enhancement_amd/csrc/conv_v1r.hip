@@ -320,11 +320,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_v1r(HaloArgs a) {
 }  // namespace
 
 int launch_conv_v1r(const HaloArgs& a, hipStream_t s) {
-    static bool attr = false;
-    if (!attr) {
-        AVSE_HIP_CHECK(hipFuncSetAttribute((const void*)k_conv_v1r<0>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
-        attr = true;
-    }
+    if (int rc = ensure_lds_attr((const void*)k_conv_v1r<0>, LDS_BYTES)) return rc;
     if (a.Hc % TH || a.Wc % TW || a.Co != 128 || a.Ci != NF || !a.w) {
         set_error("v_conv1 row-run kernel: unexpected layer shape or missing packing");
         return 3;

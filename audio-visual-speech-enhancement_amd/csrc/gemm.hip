@@ -215,28 +215,23 @@ __global__ __launch_bounds__(NT, 1) void k_gemm(GemmArgs g) {
 
 // split-K factor: as many workgroups as fit one round on the 256 CUs (one 128-KB workgroup per CU: 264
 // workgroups took two rounds), at least 8 slabs each
-int gemm_ksplit(int M, int N, int kpad) {
+int gemm_ksplit(int M, int N, int kpad, int cap) {
     const int tiles = ((M + 127) / 128) * ((N + 127) / 128), nslab = kpad / 32;
     int ks = 256 / tiles;
     ks = ks > nslab / 8 ? nslab / 8 : ks;
-    const char* e = std::getenv("AVSE_GEMM_KSPLIT");   // A/B: cap the split (timing experiments)
-    if (e && std::atoi(e) > 0 && std::atoi(e) < ks) ks = std::atoi(e);
+    if (cap > 0 && cap < ks) ks = cap;   // A/B: cap the split (timing experiments, ksplit == 1 parity test)
     return ks < 1 ? 1 : ks;
 }
 
-size_t gemm_ws_bytes(int M, int N, int kpad) {
-    const int ks = gemm_ksplit(M, N, kpad);
+size_t gemm_ws_bytes(int M, int N, int kpad, int cap) {
+    const int ks = gemm_ksplit(M, N, kpad, cap);
     const size_t tiles = (size_t)((M + 127) / 128) * ((N + 127) / 128);
     return ks > 1 ? tiles * ks * 128 * 128 * 4 : 0;
 }
 
 int launch_gemm(const GemmArgs& g, int mode, hipStream_t s) {
-    static bool attr = false;
-    if (!attr) {
-        AVSE_HIP_CHECK(hipFuncSetAttribute((const void*)k_gemm<0>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
-        AVSE_HIP_CHECK(hipFuncSetAttribute((const void*)k_gemm<1>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
-        attr = true;
-    }
+    if (int rc = ensure_lds_attr((const void*)k_gemm<0>, LDS_BYTES)) return rc;
+    if (int rc = ensure_lds_attr((const void*)k_gemm<1>, LDS_BYTES)) return rc;
     if (g.kpad % 32 || g.M <= 0 || g.N <= 0 || g.ksplit < 1 || (g.ksplit > 1 && (!g.partial || !g.counters)) ||
         (mode == 1 && (g.M % 16 || g.kpad != 9 * 512))) {
         set_error("gemm: bad arguments");

@@ -32,22 +32,25 @@ def n_frames(n_samples, hop, n_fft):
 
 
 def spectrogram(sig, sample_rate=16000, n_fft=640, hop_length=160, n_mels=80, fmin=0.0, fmax=8000.0,
-                amin=1e-5, top_db=80.0, pad_mode="reflect", frames_per_slice=0, return_stft=False):
+                amin=1e-5, top_db=80.0, pad_mode="reflect", frames_per_slice=0, return_stft=False, out=None):
     """K1: STFT -> mel -> dB for a batch of utterances.
 
     sig [U, L] float32 device tensor.  Returns mel_db [U, n_mels, T] (frames_per_slice == 0) or
-    [U, n_slices, n_mels, frames_per_slice]; with return_stft also the complex64 STFT [U, 1+n_fft//2, T].
+    [U, n_slices, n_mels, frames_per_slice] (into `out` when given); with return_stft also the complex64 STFT
+    [U, 1+n_fft//2, T].
     """
     _dev_f32(sig, "sig")
     if sig.dim() != 2:
         raise ValueError("sig must be [n_utterances, n_samples]")
     U, L = sig.shape
     T = n_frames(L, hop_length, n_fft)
-    if frames_per_slice:
-        ns = T // frames_per_slice
-        out = torch.empty((U, ns, n_mels, frames_per_slice), dtype=torch.float32, device=sig.device)
+    shape = (U, T // frames_per_slice, n_mels, frames_per_slice) if frames_per_slice else (U, n_mels, T)
+    if out is None:
+        out = torch.empty(shape, dtype=torch.float32, device=sig.device)
     else:
-        out = torch.empty((U, n_mels, T), dtype=torch.float32, device=sig.device)
+        _dev_f32(out, "out")
+        if tuple(out.shape) != shape or out.device != sig.device:
+            raise ValueError(f"out must be {shape} on {sig.device}")
     stft = torch.empty((U, 1 + n_fft // 2, T, 2), dtype=torch.float32, device=sig.device) if return_stft else None
     pm = {"reflect": _lib.AVSE_PAD_REFLECT, "constant": _lib.AVSE_PAD_CONSTANT}[pad_mode]
     ctx = _lib.context(sig.device)
@@ -120,21 +123,39 @@ class DeviceWeights:
             self.handle = None
 
 
-def forward(weights, audio, video, vnorm_mean=None, vnorm_std=None, out=None):
-    """K2-K5: network forward.  audio [N, 80, 20], video [N, 128, 128, 5] float32 device tensors
-    (video un-normalised when vnorm_* are given).  Returns [N, 80, 20] float32."""
+def _check_forward_args(weights, audio, video, vnorm_mean, vnorm_std):
     _dev_f32(audio, "audio", (80, 20))
-    _dev_f32(video, "video", (128, 128, 5))
     N = audio.shape[0]
-    if video.shape[0] != N:
-        raise ValueError("audio and video batch sizes differ")
+    if video is not None:
+        _dev_f32(video, "video", (128, 128, 5))
+        if video.shape[0] != N:
+            raise ValueError("audio and video batch sizes differ")
     if (vnorm_mean is None) != (vnorm_std is None):
         raise ValueError("vnorm_mean and vnorm_std must both be given")
     if vnorm_mean is not None:
+        if video is None:
+            raise ValueError("video=None (all-zero video) takes no normaliser")
         _dev_f32(vnorm_mean, "vnorm_mean", (128, 128))
         _dev_f32(vnorm_std, "vnorm_std", (128, 128))
+    devs = {weights.ctx.device_index, audio.device.index} | ({video.device.index} if video is not None else set())
+    if len(devs) != 1:
+        raise ValueError(f"weights live on cuda:{weights.ctx.device_index} but audio / video are on "
+                         f"{audio.device} / {None if video is None else video.device}")
+    return N
+
+
+def forward(weights, audio, video, vnorm_mean=None, vnorm_std=None, out=None):
+    """K2-K5: network forward.  audio [N, 80, 20], video [N, 128, 128, 5] float32 device tensors
+    (video un-normalised when vnorm_* are given).  Returns [N, 80, 20] float32.
+
+    video=None means an all-zero video input (BASELINE configs[2], the audio branch alone): the video
+    encoder's output is then one constant vector, computed once per weights object and broadcast."""
+    N = _check_forward_args(weights, audio, video, vnorm_mean, vnorm_std)
     if out is None:
         out = torch.empty((N, 80, 20), dtype=torch.float32, device=audio.device)
+    _dev_f32(out, "out", (80, 20))
+    if out.device != audio.device or out.shape[0] != N:
+        raise ValueError("out must be [N, 80, 20] on the inputs' device")
     with torch.cuda.device(audio.device):
         _lib.check(_lib.load().avse_forward(weights.ctx.handle, weights.handle, _lib.ptr(audio), _lib.ptr(video),
                                             _lib.ptr(vnorm_mean), _lib.ptr(vnorm_std), N, _lib.ptr(out),
@@ -144,7 +165,7 @@ def forward(weights, audio, video, vnorm_mean=None, vnorm_std=None, out=None):
 
 def forward_profile(weights, audio, video, vnorm_mean=None, vnorm_std=None, out=None):
     """forward() with HIP events between kernel launches (synchronises); returns (out, {stage: ms})."""
-    N = audio.shape[0]
+    N = _check_forward_args(weights, audio, video, vnorm_mean, vnorm_std)
     if out is None:
         out = torch.empty((N, 80, 20), dtype=torch.float32, device=audio.device)
     ms = (ctypes.c_float * _lib.AVSE_NUM_STAGES)()

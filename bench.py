@@ -3,17 +3,24 @@
 One "step" = one pass of the hot path over one batch of synthetic 200-ms clips already resident in
 HBM: K1 spectrogram of B x 3200 samples -> mel-dB [B, 80, 20] -> full fusion forward (BASELINE.json
 configs[3], bf16, batch 512 per GPU) -> [B, 80, 20] predicted speech spectrograms; for N > 1 the
-outputs are all-gathered over RCCL (the north star's final gather).  Weak scaling: every rank
-processes B clips per step.
+outputs are all-gathered over RCCL (the north star's final gather).  Weak scaling by default (every
+rank processes B clips per step); --strong splits a fixed global batch of B clips over the ranks.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--strong]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
-Rank 0 prints ONE JSON line (see README / DESIGN.md "Measurement").
+Rank 0 prints ONE JSON line.  At N = 1 the line also carries the other BASELINE
+configs as extra legs, each timed with HIP events on the stream its kernels run on:
+  configs[1] STFT only, 4096 segments, >= 4 rotated buffer sets (past the 256 MB MALL) -> HBM roofline
+  configs[2] audio branch fp32, batch 256, all-zero video (embedding computed once)   -> fp32 MFMA roofline
+and the cpu_baseline leg (the CPU oracle on a bounded sample of the same inputs), which also reports the
+timed output's RMS against the oracle.
 """
 import argparse
+import glob
 import json
 import os
+import statistics
 import sys
 import time
 
@@ -27,45 +34,123 @@ import avse_pkg  # noqa: E402
 
 avse_pkg.load()
 from avse_amd import _lib, ops  # noqa: E402
-from avse_amd.model import KerasModel  # noqa: E402
+from avse_amd.model import KerasModel, tensor_names  # noqa: E402
 
 METRIC = "clips/sec (STFT+CNN forward) on 200-ms@16kHz segments, 1/2/4/8 MI355X"
 SR, SEG = 16000, 3200
 # algorithmic work per clip
+MMAC = {"a_conv": 0.640 + 26.214 + 13.107 + 3.277 + 1.638, "dense": 6.885 + 1.721 + 4.198,
+        "deconv": 1.638 + 3.277 + 26.214 + 52.429 + 40.960 + 0.102}
 FLOP_PER_CLIP = 2 * 2688.4e6                     # whole forward, 5.377 GFLOP
+FLOP_AUDIO_BRANCH = 2e6 * sum(MMAC.values())     # configs[2]: audio encoder + dense + decoder, 0.3646 GFLOP
 FLOP_V_CONV2 = 2 * 64 * 64 * 128 * 3200          # dominant kernel: v_conv2 implicit GEMM (M=4096, N=128, K=3200)
 STFT_BYTES_PER_CLIP = SEG * 4 + 80 * 20 * 4      # 12,800 B in + 6,400 B out
 PEAK_TFLOPS = {"bf16": 256 * 4 * 2.4e9 * 1024 / 1e12, "fp32": 256 * 4 * 2.4e9 * 64 / 1e12}   # 2516.6 / 157.3
 PEAK_HBM_GBS = 8000.0
 
 
-def synth(rng, B):
+def synth(rng, B, video=True):
+    """SURVEY.md §8(d) synthetic inputs: int16-scale noise + a 200-3000 Hz tone, uint8-valued mouth crops."""
     t = np.arange(SEG) / SR
     f0 = rng.uniform(200, 3000, size=(B, 1))
     audio = rng.normal(0, 3000, (B, SEG)) + 3000 * np.sin(2 * np.pi * f0 * t[None, :])
     audio = np.clip(np.round(audio), -32768, 32767).astype(np.float32)
-    video = rng.integers(0, 256, (B, 128, 128, 5), dtype=np.uint8).astype(np.float32)
-    return audio, video
+    vid = rng.integers(0, 256, (B, 128, 128, 5), dtype=np.uint8).astype(np.float32) if video else None
+    return audio, vid
 
 
-def pmc_traffic(B, dtype):
-    """HBM bytes per launch of the dominant kernel from the newest committed PMC summary
-    (profiles/<round>_pmc_traffic.json, written by tools/profile.sh from separate FETCH_SIZE /
-    WRITE_SIZE rocprofv3 passes at this batch), or None when no matching profile exists."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
-    for f in reversed(files):
+def pmc_summary(B):
+    """Per-kernel PMC summary of the newest committed profile at this batch (profiles/<tag>_pmc.json, written by
+    tools/pmc_summary.py from separate rocprofv3 FETCH_SIZE / WRITE_SIZE / MFMA-busy passes of this code)."""
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")), reverse=True):
         try:
             d = json.load(open(f))
         except ValueError:
             continue
-        if d.get("batch") == B and dtype == "bf16" and "traffic_bytes_per_launch" in d:
-            return int(d["traffic_bytes_per_launch"])
-    return None
+        if d.get("batch") == B and "kernels" in d:
+            return os.path.basename(f), d
+    return None, None
 
 
-def cpu_baseline(audio, video, mean, std, model, budget_s=12.0, max_s=30.0):
-    """The CPU oracle (numpy librosa restatement + torch-CPU fp32 Keras graph) on a bounded sample."""
+class Windows:
+    """HIP events between groups of steps inside the timed region (recording an event does not synchronise):
+    per-window ms/step, so a claim smaller than the window spread reads as unresolved."""
+
+    def __init__(self, steps, per):
+        self.per = max(1, per)
+        self.ev = [torch.cuda.Event(enable_timing=True) for _ in range(steps // self.per + 1)]
+
+    def mark(self, i):
+        if i % self.per == 0 and i // self.per < len(self.ev):
+            self.ev[i // self.per].record()
+
+    def summary(self):
+        ms = [a.elapsed_time(b) / self.per for a, b in zip(self.ev[:-1], self.ev[1:])]
+        if not ms:
+            return None
+        return {"steps_per_window": self.per, "n": len(ms), "min": round(min(ms), 4),
+                "median": round(statistics.median(ms), 4), "max": round(max(ms), 4)}
+
+
+def leg_stft(dev, reps=50, B=4096, sets=5):
+    """configs[1]: STFT only at B = 4096 segments; `sets` input/output buffer sets (5 x 78.6 MB > 256 MB MALL)
+    rotated so every launch streams from HBM.  HBM roofline on the algorithmic 19,200 B per segment."""
+    rng = np.random.default_rng(4096)
+    ins = [torch.from_numpy(synth(rng, B, video=False)[0]).to(dev) for _ in range(sets)]
+    outs = [torch.empty((B, 1, 80, 20), dtype=torch.float32, device=dev) for _ in range(sets)]
+
+    def run(k):
+        ops.spectrogram(ins[k % sets], frames_per_slice=20, out=outs[k % sets])
+
+    for k in range(2 * sets):
+        run(k)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for k in range(reps):
+        run(k)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    gbs = STFT_BYTES_PER_CLIP * B / (ms * 1e-3) / 1e9
+    return {"config": "BASELINE configs[1]: STFT only (n_fft 640, hop 160, 80 mel, dB, top_db), batch 4096 segments",
+            "kernel": "k_spec640", "ms_per_launch": round(ms, 4), "clips_per_s": round(B / (ms * 1e-3), 1),
+            "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": round(gbs / PEAK_HBM_GBS, 4), "bytes_per_launch": STFT_BYTES_PER_CLIP * B},
+            "buffer_sets": sets, "working_set_mb": round(sets * B * STFT_BYTES_PER_CLIP / 1e6, 1), "reps": reps}
+
+
+def leg_audio_fp32(dev, model, reps=50, B=256):
+    """configs[2]: the audio branch alone, fp32, batch 256, all-zero video (video=None: the video embedding is
+    computed once per weights object and broadcast).  fp32 MFMA roofline on 0.3646 GFLOP per clip."""
+    dw = ops.DeviceWeights(model, "float32", dev)
+    rng = np.random.default_rng(256)
+    audio = torch.from_numpy(synth(rng, B, video=False)[0]).to(dev)
+    mel = ops.spectrogram(audio, frames_per_slice=20).view(B, 80, 20)
+    out = torch.empty((B, 80, 20), dtype=torch.float32, device=dev)
+    for _ in range(3):
+        ops.forward(dw, mel, None, out=out)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(reps):
+        ops.forward(dw, mel, None, out=out)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    tf = FLOP_AUDIO_BRANCH * B / (ms * 1e-3) / 1e12
+    _, st = ops.forward_profile(dw, mel, None, out=out)
+    return {"config": "BASELINE configs[2]: audio-branch CNN forward, fp32 (exact-fp32 MFMA), batch 256, video zeros",
+            "ms_per_forward": round(ms, 4), "clips_per_s": round(B / (ms * 1e-3), 1),
+            "roofline": {"bound": "mfma", "achieved": round(tf, 2), "peak": round(PEAK_TFLOPS["fp32"], 1),
+                         "unit": "TFLOP/s", "frac": round(tf / PEAK_TFLOPS["fp32"], 4),
+                         "flop_per_clip": FLOP_AUDIO_BRANCH},
+            "stage_ms": {k: round(v, 4) for k, v in st.items() if v > 0.0005}, "reps": reps}
+
+
+def cpu_baseline(audio, video, mean, std, model, gpu_out, budget_s=12.0, max_s=30.0):
+    """The CPU oracle (numpy librosa restatement + torch-CPU fp32 Keras graph) on a bounded sample of the same
+    inputs; also the parity of the timed GPU output against the float64 oracle pipeline on those clips."""
     from oracle import keras_ref, librosa_ref
     cores = len(os.sched_getaffinity(0))
     env = os.environ.get("OMP_NUM_THREADS")
@@ -79,24 +164,35 @@ def cpu_baseline(audio, video, mean, std, model, budget_s=12.0, max_s=30.0):
     clips, t0 = 0, time.perf_counter()
     while True:
         mel = np.stack([librosa_ref.preprocess_audio_signal(a[i], SR, 200, 1, 25.0)[0] for i in range(sample)])
-        keras_ref.forward(wd, mel.astype(np.float32), vn, dtype=torch.float32)
+        out32 = keras_ref.forward(wd, mel.astype(np.float32), vn, dtype=torch.float32)
         clips += sample
         el = time.perf_counter() - t0
         if el >= budget_s or el >= max_s:
             break
-    return {"value": clips / el, "unit": "clips/s", "cores": cores, "kind": "port",
+    ref = keras_ref.forward(wd, mel.astype(np.float32), vn, dtype=torch.float64)
+    g = np.asarray(gpu_out[:sample], np.float64)
+    rms = float(np.sqrt(np.mean(ref ** 2)))
+    parity = {"clips": sample, "vs": "float64 oracle pipeline (numpy STFT/mel/dB + Keras-semantics forward)",
+              "output_rel_rms": float(np.sqrt(np.mean((g - ref) ** 2)) / rms),
+              "output_abs_rms": float(np.sqrt(np.mean((g - ref) ** 2))),
+              "output_rel_rms_vs_cpu_fp32": float(np.sqrt(np.mean((g - out32) ** 2)) / rms),
+              "reference_output_rms": rms}
+    base = {"value": clips / el, "unit": "clips/s", "cores": cores, "kind": "port",
             "sample": f"{sample} clips x {clips // sample} reps ({el:.1f} s): numpy STFT/mel/dB + torch-CPU fp32 "
-                      "Keras-semantics forward (oracle/), same synthetic inputs"}
+                      "Keras-semantics forward (oracle/), same synthetic inputs as the timed batch"}
+    return base, parity
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=512, help="clips per GPU per step")
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=512, help="clips per GPU per step (global batch with --strong)")
+    ap.add_argument("--strong", action="store_true", help="split a fixed global batch of --batch clips over the ranks")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-legs", action="store_true", help="skip the configs[1] / configs[2] legs")
     ap.add_argument("--profile-reps", type=int, default=5)
     args = ap.parse_args()
 
@@ -107,13 +203,17 @@ def main():
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
-    B = args.batch
+    from avse_amd.parallel import shard_bounds
+    if args.strong:
+        lo, hi = shard_bounds(args.batch, world, rank)
+        B, global_batch = hi - lo, args.batch
+    else:
+        lo, B, global_batch = 0, args.batch, world * args.batch
 
     # weights: seeded Keras-layout init on rank 0, broadcast once over RCCL (not timed)
     blob = torch.from_numpy(KerasModel.init(seed=0, randomize=True).to_blob()).to(dev)
     if world > 1:
         dist.broadcast(blob, 0)
-    from avse_amd.model import tensor_names
     host = blob.cpu().numpy()
     tensors, off = {}, 0
     for name, shape in tensor_names():
@@ -122,32 +222,41 @@ def main():
         off += n
     model = KerasModel(tensors)
     dw = ops.DeviceWeights(model, args.dtype, dev)
-    dw.ctx.reserve(B, dw.dtype)
+    dw.ctx.reserve(max(B, 1), dw.dtype)
 
-    rng = np.random.default_rng(1234 + rank)
-    audio_np, video_np = synth(rng, B)
+    # every rank draws the same global batch and keeps its block (weak: its own seeded batch)
+    rng = np.random.default_rng(1234 + (0 if args.strong else rank))
+    audio_np, video_np = synth(rng, args.batch if args.strong else B)
+    audio_np, video_np = audio_np[lo:lo + B], video_np[lo:lo + B]
     mean_np = video_np.mean(axis=(0, 3)).astype(np.float32)
     std_np = video_np.std(axis=(0, 3)).astype(np.float32)
     audio = torch.from_numpy(audio_np).to(dev)
     video = torch.from_numpy(video_np).to(dev)
     mean, std = torch.from_numpy(mean_np).to(dev), torch.from_numpy(std_np).to(dev)
     out = torch.empty((B, 80, 20), dtype=torch.float32, device=dev)
-    gathered = torch.empty((world * B, 80, 20), dtype=torch.float32, device=dev) if world > 1 else None
+    mel = torch.empty((B, 1, 80, 20), dtype=torch.float32, device=dev)
+    per = -(-global_batch // world)
+    padded = torch.zeros((per, 80, 20), dtype=torch.float32, device=dev)
+    gathered = torch.empty((world * per, 80, 20), dtype=torch.float32, device=dev) if world > 1 else None
 
     def step():
-        mel = ops.spectrogram(audio, frames_per_slice=20)          # [B, 1, 80, 20]
+        ops.spectrogram(audio, frames_per_slice=20, out=mel)          # [B, 1, 80, 20]
         ops.forward(dw, mel.view(B, 80, 20), video, mean, std, out=out)
         if world > 1:
-            dist.all_gather_into_tensor(gathered, out)
+            padded[:B].copy_(out)
+            dist.all_gather_into_tensor(gathered, padded)
 
     for _ in range(args.warmup):
         step()
+    win = Windows(args.steps, 10)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
+        win.mark(i)
         step()
+    win.mark(args.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -156,20 +265,21 @@ def main():
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    value = world * B * args.steps / elapsed
+    value = global_batch * args.steps / elapsed
     ms_per_step = 1e3 * elapsed / args.steps
+    timed_out = out.cpu().numpy()
 
     # ---- live per-kernel durations (HIP events on the launch stream) for the roofline ----
     stage_ms = {}
     for _ in range(args.profile_reps):
-        mel = ops.spectrogram(audio, frames_per_slice=20)
+        ops.spectrogram(audio, frames_per_slice=20, out=mel)
         _, st = ops.forward_profile(dw, mel.view(B, 80, 20), video, mean, std, out=out)
         for k, v in st.items():
             stage_ms[k] = stage_ms.get(k, 0.0) + v / args.profile_reps
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(args.profile_reps):
-        ops.spectrogram(audio, frames_per_slice=20)
+        ops.spectrogram(audio, frames_per_slice=20, out=mel)
     e1.record()
     torch.cuda.synchronize()
     stft_ms = e0.elapsed_time(e1) / args.profile_reps
@@ -177,7 +287,8 @@ def main():
     dom = "v_conv2"
     achieved = FLOP_V_CONV2 * B / (stage_ms[dom] * 1e-3) / 1e12
     peak = PEAK_TFLOPS[args.dtype]
-    traffic = pmc_traffic(B, args.dtype)
+    pmc_file, pmc = pmc_summary(B) if args.dtype == "bf16" else (None, None)
+    kp = (pmc or {}).get("kernels", {}).get(dom, {})
     fwd_ms = sum(stage_ms.values())
     result = {
         "metric": METRIC,
@@ -188,31 +299,39 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.strong else "weak",
         "vs_baseline": None,
         "dtype": args.dtype,
         "data": "synthetic: seeded int16-scale noise+harmonic audio (3200 samples/clip), uint8-valued 128x128x5 "
                 "mouth crops, random-init Keras-layout weights with randomised BN; inputs resident in HBM",
         "config": {"workload": "STFT (n_fft 640, hop 160, 80 mel, dB) + full audio-visual fusion forward "
                                "(BASELINE configs[3]) on 200-ms@16kHz clips",
-                   "global_batch": world * B, "per_gpu_batch": B, "parallelism": f"dp{world}"},
+                   "global_batch": global_batch, "per_gpu_batch": B, "parallelism": f"dp{world}"},
+        "window_ms_per_step": win.summary(),
         "roofline": {"kernel": f"{dom} (k_conv_stream<5,16,16,1>: persistent warp-specialised implicit GEMM "
                                "M=4096/clip N=128 K=3200, fused BN+LReLU+2x2 maxpool)" if args.dtype == "bf16" else
                                f"{dom} (k_conv<float,128> implicit GEMM, exact-fp32 MFMA)",
                      "bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
-                     "frac": round(achieved / peak, 4), "traffic": traffic,
+                     "frac": round(achieved / peak, 4), "traffic": kp.get("traffic_bytes"),
+                     "algorithmic_bytes": kp.get("algorithmic_bytes"),
+                     "mfma_busy_frac": kp.get("mfma_busy_frac"), "eff_clock_ghz": kp.get("eff_clock_ghz"),
+                     "pmc_source": pmc_file,
                      "per_launch_flop": FLOP_V_CONV2 * B, "avg_launch_ms": round(stage_ms[dom], 4)},
         "breakdown": {
             "stft_ms": round(stft_ms, 4),
             "stft_hbm_gbs": round(STFT_BYTES_PER_CLIP * B / (stft_ms * 1e-3) / 1e9, 1),
-            "stft_hbm_frac": round(STFT_BYTES_PER_CLIP * B / (stft_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
             "forward_ms": round(fwd_ms, 4),
             "forward_tflops": round(FLOP_PER_CLIP * B / (fwd_ms * 1e-3) / 1e12, 2),
+            "step_frac_of_peak": round(FLOP_PER_CLIP * B / (ms_per_step * 1e-3) / 1e12 / peak, 4),
             "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
         },
     }
+    if rank == 0 and world == 1 and not args.no_legs:
+        result["legs"] = {"stft_b4096": leg_stft(dev), "audio_fp32_b256": leg_audio_fp32(dev, model)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(audio_np, video_np, mean_np, std_np, model)
+        base, parity = cpu_baseline(audio_np, video_np, mean_np, std_np, model, timed_out)
+        result["cpu_baseline"] = base
+        result["parity"] = parity
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -53,6 +53,22 @@ const char* avse_last_error(void);
 int avse_ctx_create(int device, avse_ctx** out);
 void avse_ctx_destroy(avse_ctx* ctx);
 
+/* Kernel-path switches of a context, by name (A/B experiments and layer-by-layer parity tests; the
+ * defaults are the production path).  Each is initialised at avse_ctx_create from an AVSE_*
+ * environment variable and never re-read afterwards:
+ *   no_gemm (AVSE_NO_GEMM)           v_conv6 + dense layers on k_conv + split-K reduce, not k_gemm
+ *   no_audenc (AVSE_NO_AUDENC)       audio encoder layer by layer, not the fused k_aud_enc
+ *   no_dechead / no_dectail          decoder head (d_deconv1..3) / tail (d_deconv4..6) layer by layer
+ *   unfused_tail (AVSE_UNFUSED_TAIL) d_deconv6 as its own kernel (d_deconv5 activation materialised)
+ *   no_halo (AVSE_NO_HALO)           video convs on k_conv (applies to weights loaded afterwards)
+ *   mfma32 (AVSE_MFMA32)             32x32x16 compute waves in the stream convolutions
+ *   serial / aud_side                one stream / audio encoder on the side stream
+ *   graph (AVSE_GRAPH)               avse_forward replays a hipGraph per argument set
+ *   gemm_ksplit_cap (AVSE_GEMM_KSPLIT) cap on k_gemm's split-K factor (0 = none)
+ * Unknown names return AVSE_ERR_INVALID. */
+int avse_ctx_set_option(avse_ctx* ctx, const char* name, int value);
+int avse_ctx_get_option(avse_ctx* ctx, const char* name, int* value);
+
 /* Pre-size the forward scratch for up to max_clips clips so that later avse_forward calls never
  * allocate (required before capturing avse_forward into a hipGraph). */
 int avse_ctx_reserve(avse_ctx* ctx, int64_t max_clips, int compute_dtype);
@@ -119,7 +135,10 @@ void avse_weights_destroy(avse_weights* w);
  * VideoNormalizer.normalize it is preceded by (data_processor.py:208-212,
  * speech_enhancer.py:74), fused:
  *   audio      [N][80][20]        mixed mel-dB spectrograms (the expand_dims(-1) is implicit)
- *   video      [N][128][128][5]   mouth crops, NOT normalised
+ *   video      [N][128][128][5]   mouth crops, NOT normalised; NULL = an all-zero video input (the audio
+ *                                 branch alone, BASELINE configs[2]: the video encoder's output is then one
+ *                                 constant vector, computed once per weights object and broadcast;
+ *                                 vnorm_* must be NULL)
  *   vnorm_mean [128][128]         nullable: VideoNormalizer mean image (applied in-kernel)
  *   vnorm_std  [128][128]         nullable: VideoNormalizer std image
  *   out        [N][80][20]        predicted speech mel-dB spectrograms (float32)

@@ -94,7 +94,9 @@ def forward(weights, mixed_spectrograms, video_samples, dtype=torch.float64, thr
 
     weights: dict name -> dict of Keras-layout arrays ('kernel', 'bias'; BN layers under
     name + '_bn' with gamma/beta/moving_mean/moving_variance).
-    mixed_spectrograms [N, 80, 20]; video_samples [N, 128, 128, 5] (already normalised).
+    mixed_spectrograms [N, 80, 20]; video_samples [N, 128, 128, 5] (already normalised), or None for an
+    all-zero video input (BASELINE configs[2]): the video branch then runs once on one zero clip and its
+    embedding is shared by every clip, which is what a zero batch computes clip by clip.
     intermediates: optional dict, filled with each layer's NHWC output (after BN/LReLU/pool).
     """
     def keep(name, t):
@@ -105,6 +107,8 @@ def forward(weights, mixed_spectrograms, video_samples, dtype=torch.float64, thr
         torch.set_num_threads(threads)
     with torch.no_grad():
         a = _t(mixed_spectrograms, dtype)[:, None, :, :]          # expand_dims(-1) -> NCHW, C=1
+        if video_samples is None:
+            video_samples = np.zeros((1, 128, 128, 5), np.float32)
         v = _t(video_samples, dtype).permute(0, 3, 1, 2)           # NHWC -> NCHW
         for name, kind, f, k, s, has_bn, pool, _ in AUDIO_ENCODER:
             a = lrelu(bn(conv_same(a, weights[name]["kernel"], weights[name]["bias"], s, dtype), weights[name + "_bn"], dtype))
@@ -115,7 +119,10 @@ def forward(weights, mixed_spectrograms, video_samples, dtype=torch.float64, thr
             keep(name, v)
         N = a.shape[0]
         a_emb_shape = a.shape[1:]
-        x = torch.cat([a.permute(0, 2, 3, 1).reshape(N, -1), v.permute(0, 2, 3, 1).reshape(N, -1)], dim=1)
+        vflat = v.permute(0, 2, 3, 1).reshape(v.shape[0], -1)
+        if vflat.shape[0] != N:                                     # the shared all-zero-video embedding
+            vflat = vflat.expand(N, -1)
+        x = torch.cat([a.permute(0, 2, 3, 1).reshape(N, -1), vflat], dim=1)
         keep("concat", x)
         x = lrelu(bn(x @ _t(weights["enc_dense"]["kernel"], dtype) + _t(weights["enc_dense"]["bias"], dtype), weights["enc_dense_bn"], dtype))
         keep("enc_dense", x)

@@ -1,9 +1,11 @@
 """K2-K5 parity: libavse forward vs the Keras-semantics oracle (oracle/keras_ref.py, float64).
 
 Tolerances (DESIGN.md "Parity"):
-  fp32 path  — relative RMS  ||gpu - ref||_2 / ||ref||_2 <= 1e-5 and absolute RMS <= 1e-4 x max(1, RMS(ref))
-               (the north star's "enhanced magnitude within 1e-4 RMS"; exact-fp32 MFMA, fp32 accumulation)
-  bf16 path  — relative RMS <= 3e-2 (bf16 operands, fp32 accumulation; SURVEY.md §7 "Tolerance vs bf16")
+  fp32 path  — ABSOLUTE RMS ||gpu - ref||_rms <= 1e-4 (the north star's "enhanced magnitude within 1e-4 RMS"),
+               checked on dB-scale outputs (RMS ~ 40, DB_SCALE below) as well as on the raw random-init model,
+               plus relative RMS <= 1e-5 (exact-fp32 MFMA, fp32 accumulation)
+  bf16 path  — relative RMS <= BF16_REL (bf16 operands, fp32 accumulation; SURVEY.md §7 "Tolerance vs bf16")
+Kernel-path switches (fused vs layer-by-layer kernels) are the context's options (avse_ctx_set_option).
 """
 import ctypes
 
@@ -16,6 +18,10 @@ from oracle import keras_ref as K
 from oracle import librosa_ref as R
 
 pytestmark = pytest.mark.gpu
+
+FP32_ABS = 1e-4     # north star: enhanced magnitude within 1e-4 RMS of the CPU reference
+FP32_REL = 1e-5
+BF16_REL = 3e-2
 
 BUF_NAMES = ["video_in", "audio_in", "a_conv1", "a_conv2", "a_conv3", "a_conv4", "v_conv1", "v_conv2", "v_conv3",
              "v_conv4", "v_conv5", "concat", "enc_dense", "dec_dense1", "dec_dense2", "d_deconv1", "d_deconv2",
@@ -43,32 +49,49 @@ def rel_rms(a, b):
     return float(np.sqrt(np.mean((a - b) ** 2)) / max(np.sqrt(np.mean(b ** 2)), 1e-30))
 
 
-def scratch(dw, N):
-    """Read libavse's intermediate activations (avse_debug_scratch) as float32 numpy arrays."""
+def scratch(dw, N, clips=None, names=None):
+    """Read libavse's intermediate activations (avse_debug_scratch) as float32 numpy arrays — only the listed
+    clips (every buffer is clip-major) and buffers, so a 512-clip batch does not copy gigabytes."""
     from avse_amd import _lib
     base = ctypes.c_void_p()
     offs = (ctypes.c_int64 * 20)()
     _lib.check(_lib.load().avse_debug_scratch(dw.ctx.handle, N, dw.dtype, ctypes.byref(base), offs), "debug")
     dt = torch.bfloat16 if dw.dtype == _lib.AVSE_BF16 else torch.float32
     es = 2 if dw.dtype == _lib.AVSE_BF16 else 4
-    out = {}
+    clips = list(range(N)) if clips is None else list(clips)
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
     torch.cuda.synchronize()
+    out = {}
     for i, name in enumerate(BUF_NAMES):
-        n = N * int(np.prod(BUF_SHAPES[name]))
-        t = torch.empty(n, dtype=dt, device="cuda")
-        from avse_amd import _lib as L
-        hip = ctypes.CDLL("libamdhip64.so.7")
-        hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
-        rc = hip.hipMemcpy(ctypes.c_void_p(t.data_ptr()), ctypes.c_void_p(base.value + offs[i]), n * es, 3)
-        assert rc == 0
-        out[name] = t.float().cpu().numpy().reshape((N,) + BUF_SHAPES[name])
+        if names is not None and name not in names:
+            continue
+        per = int(np.prod(BUF_SHAPES[name]))
+        t = torch.empty(len(clips) * per, dtype=dt, device="cuda")
+        for j, c in enumerate(clips):
+            rc = hip.hipMemcpy(ctypes.c_void_p(t.data_ptr() + j * per * es),
+                               ctypes.c_void_p(base.value + offs[i] + c * per * es), per * es, 3)
+            assert rc == 0
+        out[name] = t.float().cpu().numpy().reshape((len(clips),) + BUF_SHAPES[name])
     return out
 
 
-def run_case(gpu, N, dtype, seed=0, normalize=False):
+def db_scale(model, mean=-40.0, gain=150.0):
+    """Rescale d_deconv6 (network.py:133, the 64 -> 1 output layer) so the network emits dB-scale values
+    (mean ~ -40 dB, std ~ 10 dB) like a trained mel-dB predictor: the absolute 1e-4 RMS bound is then tested
+    where it is hardest (an output RMS of ~40, not the ~0.3 of a random-init model)."""
+    k = model.tensors["d_deconv6/kernel"]
+    model.tensors["d_deconv6/kernel"] = (k * gain).astype(np.float32)
+    model.tensors["d_deconv6/bias"] = np.full_like(model.tensors["d_deconv6/bias"], mean)
+    return model
+
+
+def run_case(gpu, N, dtype, seed=0, normalize=False, db=False):
     from avse_amd import ops
     from avse_amd.model import KerasModel
     model = KerasModel.init(seed=seed, randomize=True)
+    if db:
+        db_scale(model)
     mel, video = make_inputs(N, seed + 100)
     mean = std = None
     vref = video
@@ -85,37 +108,95 @@ def run_case(gpu, N, dtype, seed=0, normalize=False):
     return got, ref, inter, dw
 
 
-@pytest.mark.parametrize("N", [1, 3, 37])
-def test_forward_fp32_matches_oracle(gpu, N):
-    got, ref, inter, dw = run_case(gpu, N, "float32", seed=N)
+def abs_rms(a, b):
+    return float(np.sqrt(np.mean((np.asarray(a, np.float64) - np.asarray(b, np.float64)) ** 2)))
+
+
+@pytest.mark.parametrize("N,db", [(1, False), (3, False), (37, False), (3, True), (37, True)])
+def test_forward_fp32_matches_oracle(gpu, N, db):
+    got, ref, inter, dw = run_case(gpu, N, "float32", seed=N, db=db)
     err = rel_rms(got, ref)
-    abs_rms = float(np.sqrt(np.mean((got.astype(np.float64) - ref) ** 2)))
-    if err > 1e-5:
+    ae = abs_rms(got, ref)
+    print(f"fp32 N={N} db={db}: output RMS {np.sqrt(np.mean(ref ** 2)):.3g}, abs RMS err {ae:.3e}, rel {err:.3e}")
+    if err > FP32_REL:
         sc = scratch(dw, N)
         report = {k: rel_rms(sc[k], inter[k]) for k in inter if k in sc}
         pytest.fail(f"rel RMS {err:.3e}; per-layer rel RMS: {report}")
-    assert abs_rms <= 1e-4 * max(1.0, float(np.sqrt(np.mean(ref ** 2)))), abs_rms
+    assert ae <= FP32_ABS, ae
 
 
 def test_forward_fp32_fused_normalizer(gpu):
-    got, ref, inter, dw = run_case(gpu, 4, "float32", seed=7, normalize=True)
-    assert rel_rms(got, ref) <= 1e-5
+    got, ref, inter, dw = run_case(gpu, 4, "float32", seed=7, normalize=True, db=True)
+    assert rel_rms(got, ref) <= FP32_REL
+    assert abs_rms(got, ref) <= FP32_ABS
 
 
 @pytest.mark.parametrize("N", [2, 130])
 def test_forward_bf16_matches_oracle(gpu, N):
     got, ref, inter, dw = run_case(gpu, N, "bfloat16", seed=11 + N, normalize=True)
     err = rel_rms(got, ref)
-    if err > 3e-2:
+    print(f"bf16 N={N}: rel RMS {err:.3e}")
+    if err > BF16_REL:
         sc = scratch(dw, N)
         report = {k: rel_rms(sc[k], inter[k]) for k in inter if k in sc}
         pytest.fail(f"rel RMS {err:.3e}; per-layer rel RMS: {report}")
 
 
+def spread_clips(N, k=24):
+    """First, last, the tile / workgroup boundaries of the persistent kernels and k_gemm's 128-row tiles
+    (multiples of 8 clips), and seeded random clips in between — at most k distinct clips."""
+    fixed = [0, 1, 2, 3, 7, 8, 15, 16, 63, 64, 127, 128, N // 2, N - 9, N - 8, N - 5, N - 4, N - 3, N - 2, N - 1]
+    c = sorted({x for x in fixed if 0 <= x < N})
+    rng = np.random.default_rng(N)
+    while len(c) < min(k, N):
+        c = sorted(set(c) | {int(rng.integers(0, N))})
+    return c[:k] if len(c) > k else c
+
+
+CHECKED = ["v_conv1", "v_conv2", "v_conv3", "v_conv4", "v_conv5", "concat", "enc_dense", "dec_dense1", "dec_dense2",
+           "d_deconv3"]
+
+
+@pytest.mark.parametrize("N", [301, 512])
+def test_bf16_bench_batch_matches_oracle(gpu, N):
+    """The launch bench.py times (BASELINE configs[3]: bf16, 512 clips, its inputs and normaliser), and N=301
+    (k_gemm's v_conv6 at ksplit == 1 with a ragged 64-row last tile; v_conv5's 4-clip tiles ragged): the output
+    and every materialised layer of 24 spread clips against the float64 oracle, the mel input against the
+    librosa restatement."""
+    import bench
+    from avse_amd import ops
+    from avse_amd.model import KerasModel
+    rng = np.random.default_rng(1234)
+    audio_np, video_np = bench.synth(rng, N)
+    mean_np = video_np.mean(axis=(0, 3)).astype(np.float32)
+    std_np = video_np.std(axis=(0, 3)).astype(np.float32)
+    model = KerasModel.init(seed=0, randomize=True)
+    dw = ops.DeviceWeights(model, "bf16")
+    assert dw.ctx.get_option("gemm_ksplit_cap") == 0
+    mel = ops.spectrogram(ops.to_device(audio_np), frames_per_slice=20).view(N, 80, 20)
+    out = ops.forward(dw, mel, ops.to_device(video_np), ops.to_device(mean_np), ops.to_device(std_np)).cpu().numpy()
+    clips = spread_clips(N)
+    mel_np = mel.cpu().numpy()[clips]
+    mel_ref = np.stack([R.preprocess_audio_signal(audio_np[i], 16000, 200, 1, 25.0)[0] for i in clips])
+    assert np.abs(mel_np - mel_ref).max() <= 1e-3
+    inter = {}
+    vn = R.video_normalize(video_np[clips], mean_np, std_np).astype(np.float32)
+    ref = K.forward(model.layer_dict(), mel_np, vn, intermediates=inter)
+    err = rel_rms(out[clips], ref)
+    sc = scratch(dw, N, clips, CHECKED)
+    layers = {k: rel_rms(sc[k], inter[k]) for k in CHECKED}
+    print(f"bf16 N={N}: output rel RMS {err:.3e}; per layer {layers}")
+    assert np.isfinite(out).all()
+    assert err <= BF16_REL, (err, layers)
+    for k, e in layers.items():
+        assert e <= 1.5e-2, (k, e)
+
+
 @pytest.mark.parametrize("N", [1, 5])
-def test_bf16_halo_video_convs_match_generic_kernel(gpu, N, monkeypatch):
-    """The halo-tiled video convs (conv_halo.hip) against the generic implicit-GEMM kernel and the
-    oracle, layer by layer (N=5 exercises the 4-clip tiles of v_conv5 with a ragged last tile)."""
+def test_bf16_halo_video_convs_match_generic_kernel(gpu, N):
+    """The tiled video convs (conv_v1r.hip, conv_stream.hip) against the generic implicit-GEMM kernel (option
+    no_halo, applied when weights are loaded) and the oracle, layer by layer (N=5 exercises the 4-clip tiles of
+    v_conv5 with a ragged last tile)."""
     from avse_amd import ops
     from avse_amd.model import KerasModel
     model = KerasModel.init(seed=3, randomize=True)
@@ -127,31 +208,32 @@ def test_bf16_halo_video_convs_match_generic_kernel(gpu, N, monkeypatch):
     dw_h = ops.DeviceWeights(model, "bfloat16")
     out_h = ops.forward(dw_h, *args).cpu().numpy()
     sc_h = scratch(dw_h, N)
-    monkeypatch.setenv("AVSE_NO_HALO", "1")
-    dw_g = ops.DeviceWeights(model, "bfloat16")
+    with dw_h.ctx.options(no_halo=1):
+        dw_g = ops.DeviceWeights(model, "bfloat16")
     out_g = ops.forward(dw_g, *args).cpu().numpy()
     sc_g = scratch(dw_g, N)
     for k in ["v_conv1", "v_conv2", "v_conv3", "v_conv4", "v_conv5"]:
         assert rel_rms(sc_h[k], inter[k]) <= 1.5e-2, (k, rel_rms(sc_h[k], inter[k]))
         assert rel_rms(sc_h[k], sc_g[k]) <= 1.5e-2, (k, rel_rms(sc_h[k], sc_g[k]))
-    assert rel_rms(out_h, ref) <= 3e-2
-    assert rel_rms(out_h, out_g) <= 3e-2
+    assert rel_rms(out_h, ref) <= BF16_REL
+    assert rel_rms(out_h, out_g) <= BF16_REL
 
 
-def test_intermediates_fp32(gpu, monkeypatch):
+def test_intermediates_fp32(gpu):
     """Every layer's activation, not only the output, matches the oracle (catches compensating bugs).
     d_deconv6 runs unfused here so the d_deconv5 activation is materialised; the fused path is covered by
     every output comparison and by test_fused_tail_matches_unfused."""
-    monkeypatch.setenv("AVSE_UNFUSED_TAIL", "1")
-    got, ref, inter, dw = run_case(gpu, 2, "float32", seed=21)
-    sc = scratch(dw, 2)
+    from avse_amd import _lib
+    with _lib.context().options(unfused_tail=1):
+        got, ref, inter, dw = run_case(gpu, 2, "float32", seed=21)
+        sc = scratch(dw, 2)
     for k in inter:
         if k in sc:
-            assert rel_rms(sc[k], inter[k]) <= 1e-5, (k, rel_rms(sc[k], inter[k]))
+            assert rel_rms(sc[k], inter[k]) <= FP32_REL, (k, rel_rms(sc[k], inter[k]))
 
 
 @pytest.mark.parametrize("dtype,tol", [("float32", 1e-6), ("bfloat16", 2e-3)])
-def test_fused_tail_matches_unfused(gpu, monkeypatch, dtype, tol):
+def test_fused_tail_matches_unfused(gpu, dtype, tol):
     """d_deconv5 + d_deconv6 fused (the 64 -> 1 dot in d_deconv5's epilogue) against the two-kernel path;
     both round the d_deconv5 activation to the compute dtype, only the summation order differs."""
     from avse_amd import ops
@@ -161,8 +243,8 @@ def test_fused_tail_matches_unfused(gpu, monkeypatch, dtype, tol):
     args = [ops.to_device(mel), ops.to_device(video)]
     dw = ops.DeviceWeights(model, dtype)
     fused = ops.forward(dw, *args).cpu().numpy()
-    monkeypatch.setenv("AVSE_UNFUSED_TAIL", "1")
-    unfused = ops.forward(dw, *args).cpu().numpy()
+    with dw.ctx.options(unfused_tail=1):
+        unfused = ops.forward(dw, *args).cpu().numpy()
     assert rel_rms(fused, unfused) <= tol, rel_rms(fused, unfused)
 
 
@@ -197,10 +279,22 @@ def test_network_api_shapes(gpu):
     assert isinstance(loss, float) and np.isfinite(loss)
 
 
-@pytest.mark.parametrize("env", ["AVSE_V1_IM2COL", "AVSE_MFMA32"])
-def test_bf16_video_kernel_variants_agree(gpu, env, monkeypatch):
-    """A/B kernel variants of the bf16 video encoder (conv_v1r.hip kernel-row runs vs conv_v1.hip dense
-    im2col; 16x16x32 vs 32x32x16 stream-conv compute waves) give the same layer outputs and match the oracle."""
+def test_forward_rejects_mismatched_inputs(gpu):
+    from avse_amd import ops
+    from avse_amd.model import KerasModel
+    dw = ops.DeviceWeights(KerasModel.init(seed=0), "float32")
+    mel, video = make_inputs(2, 1)
+    with pytest.raises(ValueError):
+        ops.forward(dw, ops.to_device(mel), ops.to_device(video[:1]))
+    with pytest.raises(ValueError):
+        ops.forward(dw, ops.to_device(mel), ops.to_device(video), out=torch.empty((3, 80, 20), device="cuda"))
+    with pytest.raises(TypeError):
+        ops.forward(dw, torch.from_numpy(mel), ops.to_device(video))
+
+
+def test_bf16_mfma32_variant_agrees(gpu):
+    """The A/B variant of the stream convolutions (32x32x16 compute waves, option mfma32) gives the same layer
+    outputs as the production 16x16x32 waves and matches the oracle."""
     from avse_amd import ops
     from avse_amd.model import KerasModel
     N = 3
@@ -213,23 +307,22 @@ def test_bf16_video_kernel_variants_agree(gpu, env, monkeypatch):
     dw = ops.DeviceWeights(model, "bfloat16")
     out_a = ops.forward(dw, *args).cpu().numpy()
     sc_a = scratch(dw, N)
-    monkeypatch.setenv(env, "1")
-    out_b = ops.forward(dw, *args).cpu().numpy()
-    sc_b = scratch(dw, N)
+    with dw.ctx.options(mfma32=1):
+        out_b = ops.forward(dw, *args).cpu().numpy()
+        sc_b = scratch(dw, N)
     for k in ["v_conv1", "v_conv2", "v_conv3", "v_conv4", "v_conv5"]:
         assert rel_rms(sc_a[k], inter[k]) <= 1.5e-2, (k, rel_rms(sc_a[k], inter[k]))
         assert rel_rms(sc_a[k], sc_b[k]) <= 1e-2, (k, rel_rms(sc_a[k], sc_b[k]))
     assert rel_rms(out_a, out_b) <= 1e-2
 
 
-@pytest.mark.gpu
 @pytest.mark.parametrize("N", [1, 5, 37])
-def test_bf16_fused_per_clip_kernels_match_layer_path(gpu, N, monkeypatch):
+def test_bf16_fused_per_clip_kernels_match_layer_path(gpu, N):
     """The per-clip fused kernels (conv_aud.hip: a_conv1..a_conv5; conv_dech.hip: d_deconv1..d_deconv3; conv_dec.hip:
-    d_deconv4..d_deconv6) and gemm.hip (v_conv6, dense) against the layer-by-layer k_conv launches
-    (AVSE_NO_AUDENC / AVSE_NO_DECHEAD / AVSE_NO_DECTAIL / AVSE_NO_GEMM = 1) and the float64 oracle: the audio
-    embedding (concat[0:3200]) and the network output.  Both paths round every activation to bf16, so they differ
-    only in fp32 summation order."""
+    d_deconv4..d_deconv6) and gemm.hip (v_conv6, dense) against the layer-by-layer k_conv launches (options
+    no_audenc / no_dechead / no_dectail / no_gemm) and the float64 oracle: the audio embedding (concat[0:3200])
+    and the network output.  Both paths round every activation to bf16, so they differ only in fp32 summation
+    order."""
     from avse_amd import ops
     from avse_amd.model import KerasModel
     model = KerasModel.init(seed=11, randomize=True)
@@ -240,22 +333,37 @@ def test_bf16_fused_per_clip_kernels_match_layer_path(gpu, N, monkeypatch):
     ref = K.forward(model.layer_dict(), mel, R.video_normalize(video, mean, std).astype(np.float32), intermediates=inter)
     dw = ops.DeviceWeights(model, "bfloat16")
     out_f = ops.forward(dw, *args).cpu().numpy()
-    cat_f = scratch(dw, N)["concat"][:, :3200].copy()
-    for env in ("AVSE_NO_AUDENC", "AVSE_NO_DECHEAD", "AVSE_NO_DECTAIL", "AVSE_NO_GEMM"):
-        monkeypatch.setenv(env, "1")
-    out_l = ops.forward(dw, *args).cpu().numpy()
-    cat_l = scratch(dw, N)["concat"][:, :3200].copy()
+    cat_f = scratch(dw, N, names=["concat"])["concat"][:, :3200].copy()
+    with dw.ctx.options(no_audenc=1, no_dechead=1, no_dectail=1, no_gemm=1):
+        out_l = ops.forward(dw, *args).cpu().numpy()
+        cat_l = scratch(dw, N, names=["concat"])["concat"][:, :3200].copy()
     assert rel_rms(cat_f, cat_l) <= 1e-2, rel_rms(cat_f, cat_l)
     assert rel_rms(out_f, out_l) <= 1e-2, rel_rms(out_f, out_l)
-    assert rel_rms(out_f.reshape(ref.shape), ref) <= 3e-2, rel_rms(out_f.reshape(ref.shape), ref)
+    assert rel_rms(out_f.reshape(ref.shape), ref) <= BF16_REL, rel_rms(out_f.reshape(ref.shape), ref)
 
 
-@pytest.mark.gpu
-def test_forward_graph_replay(gpu, monkeypatch):
+def test_gemm_ksplit1_small_batch(gpu):
+    """k_gemm's unsplit epilogue (ksplit == 1, option gemm_ksplit_cap=1) at a small batch against the split
+    path and the oracle: every dense layer and v_conv6 then run the non-split store."""
+    from avse_amd import ops
+    from avse_amd.model import KerasModel
+    N = 9
+    model = KerasModel.init(seed=12, randomize=True)
+    mel, video = make_inputs(N, 32)
+    args = [ops.to_device(mel), ops.to_device(video)]
+    ref = K.forward(model.layer_dict(), mel, video)
+    dw = ops.DeviceWeights(model, "bfloat16")
+    out_s = ops.forward(dw, *args).cpu().numpy()
+    with dw.ctx.options(gemm_ksplit_cap=1):
+        out_1 = ops.forward(dw, *args).cpu().numpy()
+    assert rel_rms(out_1, out_s) <= 1e-2, rel_rms(out_1, out_s)
+    assert rel_rms(out_1, ref) <= BF16_REL
+
+
+def test_forward_graph_replay(gpu):
     """avse_forward's hipGraph cache: the first call with an argument set launches directly, the second captures, later
     ones replay — with new input CONTENTS at the same addresses the replay computes on them (bit-identical to direct
-    launches), and a changed AVSE_* switch or N gets its own entry (AVSE_GRAPH=1 enables the cache)."""
-    import torch
+    launches), and a changed option or N gets its own entry (option graph=1 enables the cache)."""
     from avse_amd import ops
     from avse_amd.model import KerasModel
     N = 7
@@ -265,15 +373,14 @@ def test_forward_graph_replay(gpu, monkeypatch):
     mean, std = R.video_normalizer_fit(video0)
     d = [ops.to_device(mel0), ops.to_device(video0), ops.to_device(mean), ops.to_device(std)]
     out = torch.empty((N, 80, 20), dtype=torch.float32, device=d[0].device)
-    monkeypatch.setenv("AVSE_GRAPH", "1")
     results = []
-    for seed in (3, 4, 5, 6):   # direct, capture, replay, replay
-        mel, video = make_inputs(N, seed)
-        d[0].copy_(torch.from_numpy(mel.reshape(d[0].shape)))
-        d[1].copy_(torch.from_numpy(video.reshape(d[1].shape)))
-        ops.forward(dw, *d, out=out)
-        results.append(out.cpu().numpy().copy())
-    monkeypatch.delenv("AVSE_GRAPH")
+    with dw.ctx.options(graph=1):
+        for seed in (3, 4, 5, 6):   # direct, capture, replay, replay
+            mel, video = make_inputs(N, seed)
+            d[0].copy_(torch.from_numpy(mel.reshape(d[0].shape)))
+            d[1].copy_(torch.from_numpy(video.reshape(d[1].shape)))
+            ops.forward(dw, *d, out=out)
+            results.append(out.cpu().numpy().copy())
     for k, seed in enumerate((3, 4, 5, 6)):
         mel, video = make_inputs(N, seed)
         d[0].copy_(torch.from_numpy(mel.reshape(d[0].shape)))
@@ -281,3 +388,27 @@ def test_forward_graph_replay(gpu, monkeypatch):
         ops.forward(dw, *d, out=out)
         np.testing.assert_array_equal(out.cpu().numpy(), results[k])
     assert not np.array_equal(results[2], results[3])
+
+
+def test_config3_audio_branch_fp32_b256(gpu):
+    """BASELINE configs[2]: the audio branch alone in fp32 at batch 256 with all-zero video (video=None: the video
+    embedding computed once and broadcast) against the float64 oracle, on dB-scale outputs — absolute RMS <= 1e-4;
+    and the video=None path equals an explicit zero-video forward."""
+    import bench
+    from avse_amd import ops
+    from avse_amd.model import KerasModel
+    N = 256
+    model = db_scale(KerasModel.init(seed=2, randomize=True))
+    audio_np, _ = bench.synth(np.random.default_rng(256), N, video=False)
+    dw = ops.DeviceWeights(model, "float32")
+    mel = ops.spectrogram(ops.to_device(audio_np), frames_per_slice=20).view(N, 80, 20)
+    out = ops.forward(dw, mel, None).cpu().numpy()
+    ref = K.forward(model.layer_dict(), mel.cpu().numpy(), None)
+    ae, re_ = abs_rms(out, ref), rel_rms(out, ref)
+    print(f"config3 fp32 B=256: output RMS {np.sqrt(np.mean(ref ** 2)):.3g}, abs RMS err {ae:.3e}, rel {re_:.3e}")
+    assert ae <= FP32_ABS and re_ <= FP32_REL, (ae, re_)
+    zeros = torch.zeros((4, 128, 128, 5), dtype=torch.float32, device="cuda")
+    explicit = ops.forward(dw, mel[:4].contiguous(), zeros).cpu().numpy()
+    assert rel_rms(explicit, out[:4]) <= 1e-6
+    with pytest.raises(ValueError):
+        ops.forward(dw, mel, None, zeros[0, :, :, 0].contiguous(), zeros[0, :, :, 0].contiguous())

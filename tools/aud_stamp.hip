@@ -9,6 +9,9 @@
 
 namespace avse {
 void set_error(const std::string& msg) { std::fprintf(stderr, "error: %s\n", msg.c_str()); }
+int ensure_lds_attr(const void* fn, int bytes) {
+    return hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) == hipSuccess ? 0 : 2;
+}
 }  // namespace avse
 
 using namespace avse;

@@ -1,0 +1,14 @@
+#!/bin/bash
+# One GPU call: the -m gpu suite, the default bench, then the rocprof recipe.  Each step has its own time limit;
+# a test FAILURE (exit 1) still lets the bench run, anything else (fault, abort, timeout) ends the call.
+TAG=${1:-r02}
+OUT=gpurun_out
+mkdir -p $OUT
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $OUT/gputest_$TAG.log 2>&1
+rc=$?
+echo "pytest rc=$rc"
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+timeout -k 10 400 python bench.py > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err || exit $?
+echo bench ok
+if [ "$2" = "prof" ]; then bash tools/profile.sh $TAG || exit $?; fi
+tail -3 $OUT/gputest_$TAG.log

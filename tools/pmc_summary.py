@@ -1,9 +1,14 @@
-"""Summarise a tools/profile.sh run into profiles/<tag>_kernel_stats.csv and profiles/<tag>_pmc_traffic.json.
+"""Summarise a tools/profile.sh run into profiles/<tag>_kernel_stats.csv and profiles/<tag>_pmc.json.
 
-HBM traffic per launch of the dominant kernel, corrected as MI355X_MICROARCH.md §HBM prescribes:
-FETCH_SIZE / WRITE_SIZE are KiB; on gfx950 FETCH_SIZE reports exactly half the bytes of a wide
-(16 B/lane) coalesced streaming read, so the read side is doubled; WRITE_SIZE is taken as is.
+Per forward kernel (labelled by its position in the launch sequence) the median over dispatches of:
+  * HBM traffic, corrected as MI355X_MICROARCH.md §HBM prescribes: FETCH_SIZE / WRITE_SIZE are KiB; on gfx950
+    FETCH_SIZE reports exactly half the bytes of a wide (16 B/lane) coalesced streaming read, so the read side is
+    doubled; WRITE_SIZE is taken as is;
+  * MFMA busy: SQ_VALU_MFMA_BUSY_CYCLES is summed over the 1,024 SIMDs (= 16 cycles per 16x16x32 bf16 MFMA);
+    GRBM_GUI_ACTIVE is summed over the 8 XCDs, so active cycles = GUI / 8 and
+    mfma_busy_frac = BUSY / (1024 * GUI / 8); eff_clock = (GUI / 8) / dispatch duration (profiled run).
 """
+import collections
 import csv
 import glob
 import json
@@ -13,39 +18,101 @@ import statistics
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# kernel-name prefix -> labels in launch order within one forward
+LABELS = [("k_spec640", ["stft"]), ("k_spec_dft", ["stft"]), ("k_aud_enc", ["audio_enc"]), ("k_conv_v1r", ["v_conv1"]),
+          ("k_conv_stream<5,", ["v_conv2"]), ("k_conv_stream<3, 16, 16", ["v_conv3", "v_conv4"]),
+          ("k_conv_stream<3, 8, 8", ["v_conv5"]), ("k_gemm<1>", ["v_conv6"]),
+          ("k_gemm<0>", ["enc_dense", "dec_dense1", "dec_dense2"]), ("k_dec_head", ["dec_head"]),
+          ("k_dec_tail", ["dec_tail"]), ("k_conv<", ["k_conv"]), ("k_istft", ["istft"]), ("k_ola", ["istft_ola"])]
+ALGO_BYTES = {  # algorithmic HBM bytes per launch
+    ("v_conv2", 512): 512 * (64 * 64 * 128 * 2 + 32 * 32 * 128 * 2) + 128 * 3200 * 2,
+    ("stft", 4096): 4096 * (3200 * 4 + 80 * 20 * 4),
+    ("stft", 512): 512 * (3200 * 4 + 80 * 20 * 4),
+}
 
 
-def counter(path, name):
-    vals = {}
+def short(name):
+    return name.split("::")[-1].replace("(anonymous namespace)", "")
+
+
+def label_dispatches(rows):
+    """rows: {dispatch_id: (kernel_name, duration_ns, {counter: value})} -> {label: [counters dicts]}"""
+    seen = collections.Counter()
+    out = collections.defaultdict(list)
+    for d in sorted(rows):
+        name, dur, ctr = rows[d]
+        k = short(name)
+        if "avse" not in name:
+            continue
+        for prefix, labels in LABELS:
+            if k.startswith(prefix):
+                lab = labels[seen[prefix] % len(labels)]
+                seen[prefix] += 1
+                out[lab].append((dur, ctr))
+                break
+    return out
+
+
+def read_pass(path):
+    rows = {}
     for f in glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if r["Counter_Name"] == name:
-                vals[r["Dispatch_Id"]] = vals.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
-    return list(vals.values())
+            d = int(r["Dispatch_Id"])
+            dur = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+            if d not in rows:
+                rows[d] = (r["Kernel_Name"], dur, {})
+            c = rows[d][2]
+            c[r["Counter_Name"]] = c.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    return label_dispatches(rows)
+
+
+def med(xs):
+    return statistics.median(xs) if xs else None
 
 
 def main():
-    tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
+    tag = sys.argv[1] if len(sys.argv) > 1 else "r02"
     out = os.path.join(ROOT, "gpurun_out")
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
     stats = glob.glob(os.path.join(out, f"prof_{tag}", "**", "*kernel_stats.csv"), recursive=True)
     if stats:
         shutil.copy(stats[0], os.path.join(prof, f"{tag}_kernel_stats.csv"))
-    fetch = counter(os.path.join(out, f"pmc_{tag}_fetch"), "FETCH_SIZE")
-    write = counter(os.path.join(out, f"pmc_{tag}_write"), "WRITE_SIZE")
-    res = {"kernel": "k_conv_stream<5, 16, 16, 1, 10, 0> (v_conv2)", "batch": 512,
-           "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, tools/fwd_loop.py (B=512 bf16)",
-           "dispatches": [len(fetch), len(write)]}
-    if fetch and write:
-        f = statistics.median(fetch) * 1024
-        w = statistics.median(write) * 1024
-        res.update({"fetch_size_bytes_raw": f, "fetch_bytes_corrected": 2 * f, "write_bytes": w,
-                    "traffic_bytes_per_launch": 2 * f + w,
-                    "algorithmic_bytes_per_launch": 512 * (64 * 64 * 128 * 2 + 32 * 32 * 128 * 2) + 128 * 3200 * 2})
-    with open(os.path.join(prof, f"{tag}_pmc_traffic.json"), "w") as fh:
+    kern = collections.defaultdict(dict)
+    for batch, (pf, pw, pm) in ((512, ("fetch", "write", "mfma")), (4096, ("sfetch", "swrite", None))):
+        fetch = read_pass(os.path.join(out, f"pmc_{tag}_{pf}"))
+        write = read_pass(os.path.join(out, f"pmc_{tag}_{pw}"))
+        mfma = read_pass(os.path.join(out, f"pmc_{tag}_{pm}")) if pm else {}
+        for lab in sorted(set(fetch) | set(write) | set(mfma)):
+            key = lab if batch == 512 else f"{lab}_b{batch}"
+            e = kern[key]
+            e["batch"] = batch
+            f = med([c.get("FETCH_SIZE", 0.0) * 1024 for _, c in fetch.get(lab, [])])
+            w = med([c.get("WRITE_SIZE", 0.0) * 1024 for _, c in write.get(lab, [])])
+            if f is not None:
+                e["fetch_bytes_raw"] = f
+                e["fetch_bytes_corrected"] = 2 * f
+            if w is not None:
+                e["write_bytes"] = w
+            if f is not None and w is not None:
+                e["traffic_bytes"] = 2 * f + w
+            if (lab, batch) in ALGO_BYTES:
+                e["algorithmic_bytes"] = ALGO_BYTES[(lab, batch)]
+            if lab in mfma:
+                busy = med([c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) for _, c in mfma[lab]])
+                gui = med([c.get("GRBM_GUI_ACTIVE", 0.0) for _, c in mfma[lab]])
+                dur = med([d for d, _ in mfma[lab]])
+                e.update({"mfma_busy_cycles": busy, "grbm_gui_active": gui, "profiled_ns": dur})
+                if gui:
+                    e["mfma_busy_frac"] = round(busy / (1024 * gui / 8), 4)
+                    e["eff_clock_ghz"] = round(gui / 8 / dur, 3) if dur else None
+            e["dispatches"] = len(fetch.get(lab, []))
+    res = {"tag": tag, "batch": 512, "source": "rocprofv3 --pmc passes FETCH_SIZE | WRITE_SIZE | "
+           "SQ_VALU_MFMA_BUSY_CYCLES+GRBM_GUI_ACTIVE over tools/fwd_loop.py (B=512 bf16 spectrogram + forward) and "
+           "FETCH_SIZE | WRITE_SIZE over AVSE_MODE=stft (B=4096, 5 rotated buffer sets)", "kernels": kern}
+    with open(os.path.join(prof, f"{tag}_pmc.json"), "w") as fh:
         json.dump(res, fh, indent=1)
-    print(json.dumps(res))
+    print(json.dumps(res)[:3000])
 
 
 if __name__ == "__main__":

@@ -1,21 +1,29 @@
 #!/bin/bash
-# Round profiling recipe (run on the GPU box from the repo root):
-#   bash tools/profile.sh r01
-# 1. rocprofv3 --kernel-trace --stats of the bench command          -> gpurun_out/prof_<tag>/
-# 2. two separate PMC passes (FETCH_SIZE, WRITE_SIZE: they do not fit one TCC pass) over the
-#    dominant kernel (v_conv2 = k_conv_stream<5,16,16,1,...>) at the bench shape
-# 3. tools/pmc_summary.py turns them into profiles/<tag>_*.{csv,json}
+# Round profiling recipe (run on the GPU box from the repo root):   bash tools/profile.sh r02
+# 1. rocprofv3 --kernel-trace --stats of a short bench run                 -> gpurun_out/prof_<tag>/
+# 2. separate PMC passes over tools/fwd_loop.py (B = 512 bf16 forward + spectrogram): FETCH_SIZE, WRITE_SIZE
+#    (they do not fit one TCC pass), SQ_VALU_MFMA_BUSY_CYCLES + GRBM_GUI_ACTIVE
+# 3. FETCH_SIZE / WRITE_SIZE over the configs[1] STFT (B = 4096, rotated buffers: AVSE_MODE=stft)
+# 4. tools/pmc_summary.py -> profiles/<tag>_kernel_stats.csv, profiles/<tag>_pmc.json
+# Every step has its own time limit and the chain stops at the first failure.
 set -e
-TAG=${1:-r01}
+TAG=${1:-r02}
 ROOT=$(pwd)
 OUT=$ROOT/gpurun_out
 mkdir -p $OUT
+rm -rf $OUT/prof_$TAG $OUT/pmc_${TAG}_*
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run -- \
-    python3 $ROOT/bench.py --steps 10 --warmup 3 --no-cpu-baseline > $OUT/prof_${TAG}_bench.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_conv_stream<5, 16, 16, 1" --output-format csv \
-    -d $OUT/pmc_${TAG}_fetch -o pmc -- python3 $ROOT/tools/fwd_loop.py > $OUT/pmc_${TAG}_fetch.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_conv_stream<5, 16, 16, 1" --output-format csv \
-    -d $OUT/pmc_${TAG}_write -o pmc -- python3 $ROOT/tools/fwd_loop.py > $OUT/pmc_${TAG}_write.log 2>&1
+    python3 $ROOT/bench.py --steps 20 --warmup 3 --no-cpu-baseline > $OUT/prof_${TAG}_bench.log 2>&1
+for pass in "fetch:FETCH_SIZE" "write:WRITE_SIZE" "mfma:SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
+    name=${pass%%:*}; ctr=${pass#*:}
+    timeout -s KILL 120 rocprofv3 --pmc $ctr --output-format csv -d $OUT/pmc_${TAG}_$name -o pmc -- \
+        python3 $ROOT/tools/fwd_loop.py > $OUT/pmc_${TAG}_$name.log 2>&1
+done
+for pass in "sfetch:FETCH_SIZE" "swrite:WRITE_SIZE"; do
+    name=${pass%%:*}; ctr=${pass#*:}
+    AVSE_MODE=stft timeout -s KILL 120 rocprofv3 --pmc $ctr --output-format csv -d $OUT/pmc_${TAG}_$name -o pmc -- \
+        python3 $ROOT/tools/fwd_loop.py > $OUT/pmc_${TAG}_$name.log 2>&1
+done
 cd $ROOT
 python3 tools/pmc_summary.py $TAG
