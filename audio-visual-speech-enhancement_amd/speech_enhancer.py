@@ -4,7 +4,7 @@
     python -m avse_amd.speech_enhancer -bd BASE train -mn MODEL -tdn NAME ... -vdn NAME ... --init-only
     python -m avse_amd.speech_enhancer -bd BASE predict -mn MODEL -dn NAME [-g GPUS]
 
-Same cache / output layout as the reference (AssetManager :91-142, PredictionStorage :145-184).
+Same cache / output layout as the reference (speech_enhancer.py:91-184; corpus.py).
 Differences (host plumbing outside the hot path):
   * video: the reference decodes with ffmpeg and crops the mouth with dlib (data_processor.py:12-32);
     this build reads pre-cropped mouth stacks <name>.npy [frames, 128, 128] (25 fps unless a
@@ -27,17 +27,13 @@ import json
 import logging
 import os
 import random
-import shutil
-import subprocess
 from collections import namedtuple
-from datetime import datetime
-from shutil import copy2
 
 import numpy as np
 
 from . import data_processor
 from .audio_io import AudioMixer, AudioSignal
-from .dataset import AudioDataset, AudioVisualDataset
+from .corpus import Layout, pair_speech_with_noise, speakers, write_prediction
 from .network import SpeechEnhancementNetwork
 
 Sample = namedtuple("Sample", ["speaker_id", "video_file_path", "speech_file_path", "noise_file_path", "video_samples",
@@ -97,86 +93,6 @@ def preprocess_data(speech_entries, noise_file_paths):
     return samples
 
 
-# ------------------------------------------------------------------------ asset layout
-class AssetManager:
-    def __init__(self, base_dir):
-        self.__base_dir = base_dir
-        self.__cache_dir = os.path.join(base_dir, "cache")
-        self.__preprocessed_dir = os.path.join(self.__cache_dir, "preprocessed")
-        self.__models_dir = os.path.join(self.__cache_dir, "models")
-        self.__out_dir = os.path.join(base_dir, "out")
-        for d in (self.__cache_dir, self.__preprocessed_dir, self.__models_dir, self.__out_dir):
-            os.makedirs(d, exist_ok=True)
-
-    def get_preprocessed_blob_path(self, data_name):
-        return os.path.join(self.__preprocessed_dir, data_name + ".npz")
-
-    def create_model(self, model_name):
-        os.makedirs(os.path.join(self.__models_dir, model_name), exist_ok=True)
-
-    def get_model_cache_path(self, model_name):
-        return os.path.join(self.__models_dir, model_name, "model.safetensors")
-
-    def get_keras_model_path(self, model_name):
-        return os.path.join(self.__models_dir, model_name, "model.h5py")   # the reference's file (speech_enhancer.py:120-122)
-
-    def get_normalization_cache_path(self, model_name):
-        return os.path.join(self.__models_dir, model_name, "normalization.npz")
-
-    def create_prediction_storage(self, model_name, data_name):
-        d = os.path.join(self.__out_dir, model_name, data_name)
-        os.makedirs(d, exist_ok=True)
-        return d
-
-
-class PredictionStorage(object):
-    def __init__(self, storage_dir):
-        self.__base_dir = os.path.join(storage_dir, "{:%Y-%m-%d_%H-%M-%S}".format(datetime.now()))
-        os.makedirs(self.__base_dir)
-
-    def save_prediction(self, sample, predicted_speech_signal):
-        speaker_dir = os.path.join(self.__base_dir, sample.speaker_id)
-        os.makedirs(speaker_dir, exist_ok=True)
-        speech_name = os.path.splitext(os.path.basename(sample.video_file_path))[0]
-        noise_name = os.path.splitext(os.path.basename(sample.noise_file_path))[0]
-        d = os.path.join(speaker_dir, speech_name + "_" + noise_name)
-        os.mkdir(d)
-        copy2(sample.speech_file_path, os.path.join(d, "source.wav"))
-        copy2(sample.noise_file_path, os.path.join(d, "noise.wav"))
-        sample.mixed_signal.save_to_wav_file(os.path.join(d, "mixture.wav"))
-        predicted_speech_signal.save_to_wav_file(os.path.join(d, "enhanced.wav"))
-        if shutil.which("ffmpeg") and not sample.video_file_path.endswith(".npy"):
-            ext = os.path.splitext(sample.video_file_path)[1]
-            for name in ("mixture", "enhanced"):
-                subprocess.run(["ffmpeg", "-y", "-loglevel", "error", "-i", sample.video_file_path, "-i",
-                                os.path.join(d, name + ".wav"), "-c:v", "copy", "-map", "0:v:0", "-map", "1:a:0",
-                                os.path.join(d, name + ext)], check=False)
-        return d
-
-
-# ------------------------------------------------------------------------ listing
-def list_speakers(args):
-    speaker_ids = AudioVisualDataset(args.dataset_dir).list_speakers() if args.speakers is None else list(args.speakers)
-    if args.ignored_speakers is not None:
-        for speaker_id in args.ignored_speakers:
-            speaker_ids.remove(speaker_id)
-    return speaker_ids
-
-
-def list_data(dataset_dir, speaker_ids, noise_dirs, max_files=None, shuffle=True, augmentation_factor=1):
-    """speech_enhancer.py:201-220 (speech/noise zipped and truncated to the shorter list)."""
-    speech_subset = AudioVisualDataset(dataset_dir).subset(speaker_ids, max_files, shuffle)
-    noise_file_paths = AudioDataset(noise_dirs).subset(max_files, shuffle)
-    n_files = min(len(speech_subset), len(noise_file_paths))
-    speech_entries = speech_subset[:n_files]
-    noise_file_paths = noise_file_paths[:n_files]
-    all_speech, all_noise = list(speech_entries), list(noise_file_paths)
-    for _ in range(augmentation_factor - 1):
-        all_speech += speech_entries
-        all_noise += random.sample(noise_file_paths, len(noise_file_paths))
-    return all_speech, all_noise
-
-
 SAMPLE_ARRAYS = ("video_samples", "mixed_spectrograms", "speech_spectrograms", "noise_spectrograms")
 
 
@@ -228,13 +144,18 @@ def make_sample_set(samples, max_samples=None):
 
 
 # ------------------------------------------------------------------------ subcommands
+def selected_speakers(args):
+    """-s / -is flags: the listed speakers (default: every speaker directory) minus the ignored ones."""
+    chosen = list(args.speakers) if args.speakers is not None else speakers(args.dataset_dir)
+    return [s for s in chosen if s not in set(args.ignored_speakers or ())]
+
+
 def preprocess(args):
-    assets = AssetManager(args.base_dir)
-    speaker_ids = list_speakers(args)
-    speech_entries, noise_file_paths = list_data(args.dataset_dir, speaker_ids, args.noise_dirs, max_files=1000,
-                                                 shuffle=True, augmentation_factor=1)
+    layout = Layout(args.base_dir)
+    speech_entries, noise_file_paths = pair_speech_with_noise(args.dataset_dir, selected_speakers(args),
+                                                              args.noise_dirs, limit=1000, shuffle=True)
     samples = preprocess_data(speech_entries, noise_file_paths)
-    save_preprocessed_blob(assets.get_preprocessed_blob_path(args.data_name), samples)
+    save_preprocessed_blob(layout.preprocessed(args.data_name), samples)
     print("preprocessed %d samples" % len(samples))
 
 
@@ -242,27 +163,25 @@ def train(args):
     if not args.init_only:
         raise NotImplementedError("training (network.py:177-206) is outside this build's hot path; "
                                   "use --init-only to write an initialised model + normalizer")
-    assets = AssetManager(args.base_dir)
-    assets.create_model(args.model)
-    samples = load_preprocessed_blobs([assets.get_preprocessed_blob_path(d) for d in args.train_data_names])
+    layout = Layout(args.base_dir)
+    samples = load_preprocessed_blobs([layout.preprocessed(d) for d in args.train_data_names])
     video, mixed, _ = make_sample_set(samples)
     normalizer = data_processor.VideoNormalizer(video)
-    normalizer.save(assets.get_normalization_cache_path(args.model))
+    normalizer.save(layout.normalizer_file(args.model))
     network = SpeechEnhancementNetwork.build(mixed.shape[1:], video.shape[1:], seed=args.seed)
-    network.save(assets.get_model_cache_path(args.model))
+    network.save(layout.model_file(args.model))
 
 
 def predict(args):
-    assets = AssetManager(args.base_dir)
-    storage = PredictionStorage(assets.create_prediction_storage(args.model, args.data_name))
-    model_path = assets.get_model_cache_path(args.model)
-    if not os.path.exists(model_path) and os.path.exists(assets.get_keras_model_path(args.model)):
+    layout = Layout(args.base_dir)
+    run_dir = layout.prediction_run_dir(args.model, args.data_name)
+    model_path, keras_path = layout.model_file(args.model), layout.keras_model_file(args.model)
+    if not os.path.exists(model_path) and os.path.exists(keras_path):
         raise SystemExit("%s is a Keras model: convert it once with\n  /opt/conda/bin/python3.9 tools/keras_h5_to_avse.py "
-                         "%s %s" % (assets.get_keras_model_path(args.model), assets.get_keras_model_path(args.model),
-                                    model_path))
+                         "%s %s" % (keras_path, keras_path, model_path))
     network = SpeechEnhancementNetwork.load(model_path, compute_dtype=args.dtype)
-    video_normalizer = data_processor.VideoNormalizer.load(assets.get_normalization_cache_path(args.model))
-    samples = load_preprocessed_blob(assets.get_preprocessed_blob_path(args.data_name))
+    video_normalizer = data_processor.VideoNormalizer.load(layout.normalizer_file(args.model))
+    samples = load_preprocessed_blob(layout.preprocessed(args.data_name))
     for sample in samples:
         try:
             print("predicting (%s, %s)..." % (sample.video_file_path, sample.noise_file_path))
@@ -271,7 +190,7 @@ def predict(args):
                                                       sample.speech_spectrograms, video_normalizer=video_normalizer)
             print("loss: %f" % loss)
             signal = data_processor.reconstruct_speech_signal(sample.mixed_signal, pred, sample.video_frame_rate)
-            storage.save_prediction(sample, signal)
+            write_prediction(run_dir, sample, signal)
         except Exception:  # noqa: BLE001 — mirrors speech_enhancer.py:87-88
             logging.exception("failed to predict %s. skipping" % sample.video_file_path)
 

@@ -12,6 +12,7 @@ import collections
 import csv
 import glob
 import json
+import re
 import os
 import shutil
 import statistics
@@ -32,7 +33,9 @@ ALGO_BYTES = {  # algorithmic HBM bytes per launch
 
 
 def short(name):
-    return name.split("::")[-1].replace("(anonymous namespace)", "")
+    """'void avse::(anonymous namespace)::k_conv_stream<5, 16, ...>(avse::HaloArgs)' -> 'k_conv_stream<5, 16, ...>'"""
+    m = re.search(r"\b(k_\w+(<[^>]*>)?)", name)
+    return m.group(1) if m else name
 
 
 def label_dispatches(rows):
