@@ -63,10 +63,17 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, lo
 // (a wave issues at most one instruction per 4 cycles), so the short-K layers were issue-bound.
 // occupancy: more resident workgroups hide the per-tile load latency of the short-K layers (8-18 slabs per
 // tile for the decoder): 4 per CU for BN = 64 (<= 128 VGPRs, 36 KB LDS), 3 for BN = 128 (<= 168, 48 KB)
-template <int BN, bool FAST> constexpr int conv_occupancy() { return !FAST ? 2 : BN == 64 ? 4 : 3; }
+// fp32: one workgroup per CU fewer (the blocked-summation partials below need another 32 / 64 VGPRs)
+template <typename T, int BN, bool FAST> constexpr int conv_occupancy() {
+    return !FAST ? 2 : (BN == 64 ? 4 : 3) - (sizeof(T) == 4 ? 1 : 0);
+}
+// fp32 blocked summation: the K loop accumulates FP32_BLOCK slabs (FP32_BLOCK * 16 products per output) into a
+// zeroed partial that is then added to the running sum, so the running sum takes K / 128 roundings instead of
+// K / 4 (one per 16x16x4 MFMA).
+constexpr int FP32_BLOCK = 8;
 
 template <typename T, int BN, bool FAST>
-__global__ __launch_bounds__(256, (conv_occupancy<BN, FAST>())) void k_conv(ConvArgs a) {
+__global__ __launch_bounds__(256, (conv_occupancy<T, BN, FAST>())) void k_conv(ConvArgs a) {
     constexpr int CH = 16 / sizeof(T);          // elements per 16-byte chunk
     constexpr int SLAB = 64 / sizeof(T);        // elements per 64-byte k-slab
     constexpr int WN = BN / 2;                  // wave tile N
@@ -231,11 +238,12 @@ __global__ __launch_bounds__(256, (conv_occupancy<BN, FAST>())) void k_conv(Conv
         }
     };
 
-    f32x4 acc[NI][NJ];
+    f32x4 acc[NI][NJ], part[NI][NJ];   // part: fp32 blocked summation only
 #pragma unroll
     for (int i = 0; i < NI; ++i)
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < NJ; ++j) acc[i][j] = part[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    int nblk = 0;
 
     const int fr = lane & 15, fg = lane >> 4;
     if (s_begin < s_end) {
@@ -273,9 +281,21 @@ __global__ __launch_bounds__(256, (conv_occupancy<BN, FAST>())) void k_conv(Conv
                     const f32x4 bv = __builtin_bit_cast(f32x4, fb[j]);
 #pragma unroll
                     for (int e = 0; e < 4; ++e)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], bv[e], acc[i][j], 0, 0, 0);
+                        part[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], bv[e], part[i][j], 0, 0, 0);
                 }
             }
+        if constexpr (sizeof(T) == 4) {
+            if (++nblk == FP32_BLOCK) {
+                nblk = 0;
+#pragma unroll
+                for (int i = 0; i < NI; ++i)
+#pragma unroll
+                    for (int j = 0; j < NJ; ++j) {
+                        acc[i][j] += part[i][j];
+                        part[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+                    }
+            }
+        }
         if constexpr (FAST) {
             // unconditional: past s_end the loads read zeros / unused rows and the buffer is never read
             // (buffer qn held slab s-2, read before the barrier of step s-2)
@@ -296,6 +316,12 @@ __global__ __launch_bounds__(256, (conv_occupancy<BN, FAST>())) void k_conv(Conv
 
 #undef AS
 #undef BS
+    if constexpr (sizeof(T) == 4) {
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) acc[i][j] += part[i][j];
+    }
     // ---- epilogue: scale/shift (bias + BN), [pool], LeakyReLU, strided NHWC store ----
     if (a.ksplit > 1) {
         // raw fp32 partial sums in MFMA-native order, consumed only by k_splitk_reduce_tiles: unit
