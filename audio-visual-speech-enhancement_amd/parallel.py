@@ -51,12 +51,34 @@ def gather_clips(local, n_total):
     return torch.cat([p[: (lambda ab: ab[1] - ab[0])(shard_bounds(n_total, world, r))] for r, p in enumerate(parts)])
 
 
-def sharded_predict(network, mixed, video, video_normalizer=None):
-    """Every rank holds the full batch (or the same seeded inputs); each computes its block on its
-    own GPU and the blocks are all-gathered, so every rank returns the full [n, 80, 20]."""
-    n = mixed.shape[0]
+def _local_block(x, n_total):
+    """(this rank's rows, the global row count): x is either the full batch (n_total None) or already this
+    rank's contiguous block of an n_total-row batch (data loaded per rank)."""
     world = dist.get_world_size() if dist.is_initialized() else 1
     rank = dist.get_rank() if dist.is_initialized() else 0
-    a, b = shard_bounds(n, world, rank)
-    local = network.predict_device(mixed[a:b], video[a:b], video_normalizer)
+    if n_total is None:
+        a, b = shard_bounds(x.shape[0], world, rank)
+        return x[a:b], x.shape[0]
+    a, b = shard_bounds(n_total, world, rank)
+    if x.shape[0] != b - a:
+        raise ValueError(f"rank {rank} holds {x.shape[0]} rows, its block of {n_total} is {b - a}")
+    return x, n_total
+
+
+def sharded_predict(network, mixed, video, video_normalizer=None, n_total=None):
+    """Clip-sharded SpeechEnhancementNetwork.predict (network.py:208-212): each rank runs the forward on its
+    contiguous block of clips on its own GPU and the blocks are all-gathered, so every rank returns the full
+    [n_total, 80, 20] in clip order.  mixed / video: the full batch (n_total None) or this rank's block."""
+    local_mixed, n = _local_block(mixed, n_total)
+    local_video, _ = _local_block(video, n_total)
+    local = network.predict_device(local_mixed, local_video, video_normalizer)
     return gather_clips(local, n)
+
+
+def sharded_enhance(enhancer, signals, video, vmean=None, vstd=None, n_total=None):
+    """Utterance-sharded end-to-end enhancement (pipeline.Enhancer, BASELINE configs[4]): the STFT's top_db
+    is per utterance, so whole utterances are the unit; every rank enhances its block and the enhanced
+    signals are all-gathered in utterance order.  signals / video: all utterances or this rank's block."""
+    local_sig, n = _local_block(signals, n_total)
+    local_vid, _ = _local_block(video, n_total)
+    return gather_clips(enhancer(local_sig, local_vid, vmean, vstd), n)

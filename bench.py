@@ -7,6 +7,7 @@ outputs are all-gathered over RCCL (the north star's final gather).  Weak scalin
 rank processes B clips per step); --strong splits a fixed global batch of B clips over the ranks.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--strong]
+    python bench.py --e2e [--steps K]        (BASELINE configs[4], its own JSON line)
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
 Rank 0 prints ONE JSON line.  At N = 1 the line also carries the other BASELINE
@@ -183,6 +184,82 @@ def cpu_baseline(audio, video, mean, std, model, gpu_out, budget_s=12.0, max_s=3
     return base, parity
 
 
+E2E_UTTERANCES, E2E_SLICES = 667, 15           # BASELINE configs[4]: 10,005 clips = 667 3-s utterances x 15
+
+
+def run_e2e(args, world, rank, dev, model):
+    """BASELINE configs[4]: end-to-end predict (K1 STFT -> bf16 fusion CNN -> K6 ISTFT) of 667 synthetic 3-s
+    utterances (10,005 clips), strong-scaled over the ranks at utterance granularity (top_db is per utterance),
+    the enhanced signals all-gathered over RCCL.  Prints its own JSON line (workload 'e2e')."""
+    from avse_amd.parallel import gather_clips, shard_bounds
+    from avse_amd.pipeline import Enhancer
+    U = args.utterances
+    lo, hi = shard_bounds(U, world, rank)
+    n_local = hi - lo
+    S, L = E2E_SLICES, E2E_SLICES * SEG
+    g = torch.Generator(device=dev).manual_seed(4242 + rank)
+    t = torch.arange(L, device=dev, dtype=torch.float32) / SR
+    f0 = torch.rand((n_local, 1), generator=g, device=dev) * 2800 + 200
+    sig = torch.randn((n_local, L), generator=g, device=dev) * 3000 + 3000 * torch.sin(2 * np.pi * f0 * t)
+    sig = sig.round().clamp(-32768, 32767).contiguous()
+    video = torch.randint(0, 256, (n_local, S, 128, 128, 5), generator=g, device=dev, dtype=torch.uint8).float()
+    flat = video.view(-1, 128, 128, 5)
+    vmean = flat.mean(dim=(0, 3)).contiguous()
+    vstd = flat.std(dim=(0, 3), unbiased=False).contiguous()
+    dw = ops.DeviceWeights(model, args.dtype, dev)
+    enh = Enhancer(dw, chunk=args.e2e_chunk)
+    dw.ctx.reserve(min(args.e2e_chunk, n_local * S), dw.dtype)
+
+    def step():
+        out = enh(sig, video, vmean, vstd)
+        return gather_clips(out, U) if world > 1 else out
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    clips = U * S
+    stage = {}
+    for _ in range(3):
+        tm = {}
+        enh(sig, video, vmean, vstd, timings=tm)
+        for k, v in tm.items():
+            stage[k] = stage.get(k, 0.0) + v / 3
+    # K6 algorithmic HBM bytes per utterance: predicted mel-dB slices + the mixture STFT (phase source) read,
+    # the enhanced signal written (the frame scratch round trip is overhead, not algorithmic)
+    T = 1 + L // 160
+    istft_bytes = n_local * (S * 80 * 20 * 4 + 321 * T * 8 + 160 * (S * 20 - 1) * 4)
+    istft_gbs = istft_bytes / (stage["istft_ms"] * 1e-3) / 1e9
+    fwd_tf = FLOP_PER_CLIP * n_local * S / (stage["forward_ms"] * 1e-3) / 1e12
+    res = {"metric": "clips/sec end-to-end predict (STFT -> fusion CNN -> ISTFT) on 200-ms@16kHz segments",
+           "value": round(clips * args.steps / elapsed, 1), "unit": "clips/s", "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True,
+           "scaling": "strong", "vs_baseline": None, "dtype": args.dtype,
+           "data": "synthetic on device: int16-scale noise+tone 3-s utterances, uint8-valued mouth crops; "
+                   "random-init Keras-layout weights",
+           "config": {"workload": "e2e: BASELINE configs[4], %d utterances x %d slices = %d clips, utterance-sharded"
+                                  % (U, S, clips), "global_batch": clips, "per_gpu_utterances": n_local,
+                      "forward_chunk": args.e2e_chunk, "parallelism": f"dp{world}"},
+           "stage_ms_rank0": {k: round(v, 3) for k, v in stage.items()},
+           "forward_tflops": round(fwd_tf, 1),
+           "istft_roofline": {"bound": "hbm", "achieved": round(istft_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                              "frac": round(istft_gbs / PEAK_HBM_GBS, 4), "bytes_per_launch": istft_bytes}}
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -194,6 +271,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-legs", action="store_true", help="skip the configs[1] / configs[2] legs")
     ap.add_argument("--profile-reps", type=int, default=5)
+    ap.add_argument("--e2e", action="store_true", help="BASELINE configs[4]: end-to-end predict, utterance-sharded")
+    ap.add_argument("--utterances", type=int, default=E2E_UTTERANCES)
+    ap.add_argument("--e2e-chunk", type=int, default=1024, help="clips per forward launch in --e2e")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -221,6 +301,11 @@ def main():
         tensors[name] = host[off:off + n].reshape(shape)
         off += n
     model = KerasModel(tensors)
+    if args.e2e:
+        run_e2e(args, world, rank, dev, model)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     dw = ops.DeviceWeights(model, args.dtype, dev)
     dw.ctx.reserve(max(B, 1), dw.dtype)
 

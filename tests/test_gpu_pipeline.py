@@ -1,0 +1,65 @@
+"""End-to-end predict path (BASELINE configs[4]; pipeline.Enhancer): whole 3-s utterances through K1 -> forward ->
+K6 against the oracle pipeline (librosa restatement preprocess -> float64 Keras-semantics forward -> librosa
+restatement reconstruct_speech_signal, i.e. speech_enhancer.py:61-88 per sample).
+
+Tolerance: fp32 weights — the enhanced waveform within relative RMS 1e-4 of the oracle (the ISTFT's own bound,
+DESIGN.md "Parity"); bf16 — relative RMS of the predicted mel-dB slices within the bf16 forward bound (3e-2).
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import synth_audio, synth_video
+from oracle import keras_ref as K
+from oracle import librosa_ref as R
+
+pytestmark = pytest.mark.gpu
+
+
+def rel_rms(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.sqrt(np.mean((a - b) ** 2)) / np.sqrt(np.mean(b ** 2)))
+
+
+def oracle_enhance(model, x, video, mean, std):
+    """speech_enhancer.predict for one sample, restated on the oracle."""
+    sl = R.preprocess_audio_signal(x, 16000, 200, video.shape[0], 25.0)
+    vn = R.video_normalize(video, mean, std).astype(np.float32)
+    pred = K.forward(model.layer_dict(), sl.astype(np.float32), vn)
+    return R.reconstruct_speech_signal(x, 16000, pred.astype(np.float32), 25.0), pred
+
+
+@pytest.mark.parametrize("dtype,n_samples", [("float32", 48000), ("float32", 47000), ("bfloat16", 48000)])
+def test_enhancer_matches_oracle_pipeline(gpu, dtype, n_samples):
+    from avse_amd import ops
+    from avse_amd.model import KerasModel
+    from avse_amd.pipeline import Enhancer
+    U, S = 3, 15
+    rng = np.random.default_rng(5)
+    x = synth_audio(rng, U, n_samples)
+    video = synth_video(rng, U * S).reshape(U, S, 128, 128, 5)
+    mean, std = R.video_normalizer_fit(video.reshape(U * S, 128, 128, 5))
+    model = KerasModel.init(seed=8, randomize=True)
+    enh = Enhancer(ops.DeviceWeights(model, dtype), chunk=16)      # chunk < U*S: several forward launches
+    timings = {}
+    got = enh(ops.to_device(x), ops.to_device(video), ops.to_device(mean), ops.to_device(std), timings=timings)
+    got = got.cpu().numpy()
+    assert got.shape == (U, 160 * (S * 20 - 1))
+    assert set(timings) == {"stft_ms", "forward_ms", "istft_ms"}
+    for u in range(U):
+        xu = R.fit_length(x[u], 3200 * S)
+        ref, _ = oracle_enhance(model, xu, video[u], mean, std)
+        err = rel_rms(got[u], ref)
+        print(f"{dtype} utterance {u}: waveform rel RMS {err:.3e}")
+        assert err <= (1e-4 if dtype == "float32" else 3e-2), (u, err)
+
+
+def test_enhancer_rejects_mismatched_geometry(gpu):
+    from avse_amd import ops
+    from avse_amd.model import KerasModel
+    from avse_amd.pipeline import Enhancer
+    enh = Enhancer(ops.DeviceWeights(KerasModel.init(seed=0), "float32"))
+    sig = torch.zeros((2, 48000), device="cuda")
+    with pytest.raises(ValueError):
+        enh(sig, torch.zeros((3, 15, 128, 128, 5), device="cuda"))
