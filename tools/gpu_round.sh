@@ -1,6 +1,7 @@
 #!/bin/bash
-# One GPU call: the -m gpu suite, the default bench, then the rocprof recipe.  Each step has its own time limit;
-# a test FAILURE (exit 1) still lets the bench run, anything else (fault, abort, timeout) ends the call.
+# One GPU call: the -m gpu suite, the default bench, the end-to-end bench, then (optionally) the rocprof recipe.
+# Each step has its own time limit; a test FAILURE (exit 1) still lets the bench run, anything else (fault, abort,
+# timeout) ends the call.
 TAG=${1:-r02}
 OUT=gpurun_out
 mkdir -p $OUT
@@ -10,5 +11,7 @@ echo "pytest rc=$rc"
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 400 python bench.py > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err || exit $?
 echo bench ok
+timeout -k 10 300 python bench.py --e2e --steps 5 --warmup 2 > $OUT/bench_e2e_$TAG.json 2> $OUT/bench_e2e_$TAG.err || exit $?
+echo e2e ok
 if [ "$2" = "prof" ]; then bash tools/profile.sh $TAG || exit $?; fi
 tail -3 $OUT/gputest_$TAG.log
