@@ -32,6 +32,7 @@ struct Options {
     int aud_side = 0;         // AVSE_AUD_SIDE: fused audio encoder on the side stream
     int graph = 0;            // AVSE_GRAPH: avse_forward replays a hipGraph per argument set
     int gemm_ksplit_cap = 0;  // AVSE_GEMM_KSPLIT: cap k_gemm's split-K factor (0 = no cap)
+    int dense_istft = 0;      // AVSE_DENSE_ISTFT: ISTFT through the dense pinv + scratch frames + k_ola (not fused)
 };
 
 #define AVSE_HIP_CHECK(expr)                                                                   \
@@ -90,8 +91,12 @@ struct IstftArgs {
     const float* pinvT;       // [n_mels][nb] pinv(mel)^T
     const float2* twiddle;    // [N] e^{-2 pi i k / N}
     const float* window;      // [N] periodic Hann
-    float* frames;            // scratch [n_utt][T][N]
+    float* frames;            // scratch [n_utt][T][N] (unfused path only)
     float* sig;               // [n_utt][hop (T - 1)]
+    // fused n_fft 640 / hop 160 path: pinv(M) y = M^T (M M^T)^{-1} y with M M^T tridiagonal (adjacent Slaney
+    // triangles overlap, nothing else does), so the 321 x 80 dense pinv becomes a Thomas solve + a 2-tap expansion
+    const float4* tri;        // [n_mels] (sub-diagonal a_i, 1 / pivot_i, c'_i, 0) of the Thomas recurrence; null = dense
+    const float4* bins;       // [nb] (M[j0][k], M[j0+1][k], j0 as int bits, 0): the <= 2 filters covering bin k
 };
 
 int launch_istft(const IstftArgs& a, hipStream_t s);

@@ -162,6 +162,8 @@ struct IstftTables {
     float* pinvT = nullptr;     // [n_mels][nb]
     float2* twiddle = nullptr;  // [N]
     float* window = nullptr;    // [N]
+    float4* tri = nullptr;      // [n_mels] Thomas coefficients of M M^T (null when it is not tridiagonal)
+    float4* bins = nullptr;     // [nb] the <= 2 adjacent filters covering each bin
 };
 
 struct avse_ctx {
@@ -227,6 +229,7 @@ const OptionName kOptionNames[] = {
     {"aud_side", "AVSE_AUD_SIDE", &Options::aud_side},
     {"graph", "AVSE_GRAPH", &Options::graph},
     {"gemm_ksplit_cap", "AVSE_GEMM_KSPLIT", &Options::gemm_ksplit_cap},
+    {"dense_istft", "AVSE_DENSE_ISTFT", &Options::dense_istft},
 };
 
 struct avse_weights {
@@ -344,6 +347,7 @@ int ensure_spec_tables(avse_ctx* c, int sr, int n_fft, int n_mels, double fmin, 
         wd[m] = lo < 0 ? 0 : hi - lo + 1;
         if (wd[m] > maxw) maxw = wd[m];
     }
+    if (maxw <= 24) maxw = 24;   // rows padded to the STFT kernel's compile-time band width (16-B staging copies)
     std::vector<float> wt((size_t)n_mels * maxw, 0.f);
     for (int m = 0; m < n_mels; ++m)
         for (int j = 0; j < wd[m]; ++j) wt[(size_t)m * maxw + j] = (float)fb[(size_t)m * nb + st[m] + j];
@@ -368,6 +372,7 @@ int ensure_istft_tables(avse_ctx* c, int sr, int n_fft, int n_mels, double fmin,
     IstftTables& t = c->istft;
     if (t.sr == sr && t.n_fft == n_fft && t.n_mels == n_mels && t.fmin == fmin && t.fmax == fmax) return 0;
     (void)hipFree(t.pinvT); (void)hipFree(t.twiddle); (void)hipFree(t.window);
+    (void)hipFree(t.tri); (void)hipFree(t.bins);
     t = IstftTables();
     const int nb = 1 + n_fft / 2, N = 2 * (nb - 1);
     const std::vector<double> M = mel_filterbank(sr, n_fft, n_mels, fmin, fmax);
@@ -423,6 +428,53 @@ int ensure_istft_tables(avse_ctx* c, int sr, int n_fft, int n_mels, double fmin,
     AVSE_HIP_CHECK(hipMemcpy(t.pinvT, pinvT.data(), sizeof(float) * pinvT.size(), hipMemcpyHostToDevice));
     AVSE_HIP_CHECK(hipMemcpy(t.twiddle, tw.data(), sizeof(float2) * N, hipMemcpyHostToDevice));
     AVSE_HIP_CHECK(hipMemcpy(t.window, win.data(), sizeof(float) * N, hipMemcpyHostToDevice));
+    // Tridiagonal form for the fused kernel: every bin covered by at most two filters j0, j0 + 1 => M M^T
+    // has no entry beyond the first off-diagonals, and pinv(M) a = M^T y with (M M^T) y = a (Thomas, no
+    // pivoting: the Gram matrix is symmetric positive definite).  Recomputed in double from G (Gi above
+    // overwrote its working copy).
+    {
+        bool ok = true;
+        std::vector<float4> bins(nb);
+        for (int k = 0; k < nb && ok; ++k) {
+            int j0 = -1, cnt = 0;
+            for (int j = 0; j < n_mels; ++j)
+                if (M[(size_t)j * nb + k] != 0.0) {
+                    if (j0 < 0) j0 = j;
+                    else if (j != j0 + 1) ok = false;
+                    ++cnt;
+                }
+            if (cnt > 2) ok = false;
+            const float w0 = j0 >= 0 ? (float)M[(size_t)j0 * nb + k] : 0.f;
+            const float w1 = (j0 >= 0 && j0 + 1 < n_mels) ? (float)M[(size_t)(j0 + 1) * nb + k] : 0.f;
+            int j0b = j0;
+            float j0f;
+            std::memcpy(&j0f, &j0b, 4);
+            bins[k] = make_float4(w0, w1, j0f, 0.f);
+        }
+        if (ok) {
+            auto gram = [&](int i, int j) {
+                double acc = 0;
+                for (int k = 0; k < nb; ++k) acc += M[(size_t)i * nb + k] * M[(size_t)j * nb + k];
+                return acc;
+            };
+            std::vector<float4> tri(n_mels);
+            double cprev = 0;
+            for (int i = 0; i < n_mels && ok; ++i) {
+                const double ai = i > 0 ? gram(i, i - 1) : 0.0, bi = gram(i, i);
+                const double ci = i + 1 < n_mels ? gram(i, i + 1) : 0.0;
+                const double piv = bi - ai * cprev;
+                if (!(std::fabs(piv) > 1e-300)) { ok = false; break; }
+                cprev = ci / piv;
+                tri[i] = make_float4((float)ai, (float)(1.0 / piv), (float)cprev, 0.f);
+            }
+            if (ok) {
+                AVSE_HIP_CHECK(hipMalloc(&t.tri, sizeof(float4) * n_mels));
+                AVSE_HIP_CHECK(hipMalloc(&t.bins, sizeof(float4) * nb));
+                AVSE_HIP_CHECK(hipMemcpy(t.tri, tri.data(), sizeof(float4) * n_mels, hipMemcpyHostToDevice));
+                AVSE_HIP_CHECK(hipMemcpy(t.bins, bins.data(), sizeof(float4) * nb, hipMemcpyHostToDevice));
+            }
+        }
+    }
     t.sr = sr; t.n_fft = n_fft; t.n_mels = n_mels; t.fmin = fmin; t.fmax = fmax;
     return 0;
 }
@@ -761,6 +813,7 @@ void avse_ctx_destroy(avse_ctx* c) {
     (void)hipFree(c->spec.twiddle); (void)hipFree(c->spec.window);
     (void)hipFree(c->spec.mel.start); (void)hipFree(c->spec.mel.width); (void)hipFree(c->spec.mel.weight);
     (void)hipFree(c->istft.pinvT); (void)hipFree(c->istft.twiddle); (void)hipFree(c->istft.window);
+    (void)hipFree(c->istft.tri); (void)hipFree(c->istft.bins);
     (void)hipFree(c->frames);
     (void)hipFree(c->umax);
     (void)hipFree(c->mse_partial);
@@ -887,6 +940,8 @@ int avse_istft(avse_ctx* c, const float* mel_db, const float* stft_ri, int64_t n
     a.window = c->istft.window;
     a.frames = c->frames;
     a.sig = sig;
+    a.tri = c->opt.dense_istft ? nullptr : c->istft.tri;
+    a.bins = c->istft.bins;
     return launch_istft(a, (hipStream_t)stream);
 }
 

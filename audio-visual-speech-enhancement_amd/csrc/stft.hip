@@ -12,15 +12,23 @@
 //   step 2: lane (f, k2 in [0,20)) does a 16-point DFT (4 x 4) over n1 -> Z[k2 + 20 k1]
 //   step 3: lane (f, k) untangles X[k], X[320-k] from Z[k], Z[320-k]  -> |X| in LDS
 //   step 4: lane (f, mel band) sparse Slaney dot (<= max_width bins) -> dB
-// Each 448-lane block handles one chunk of up to 21 frames of one utterance, 3 frames per
+// A persistent 448-lane block walks chunks of up to 21 frames of one utterance, 3 frames per
 // wave (48 / 60 active lanes in steps 1 / 2).  When the chunk covers the whole utterance (the
 // 200-ms segment case: 3200 samples -> 21 frames) the top_db clamp (max over the WHOLE
 // [80, T] array, including the frame the slicing later drops) happens in-kernel; otherwise each
 // chunk publishes its max with an ordered-uint atomicMax and a clamp kernel follows.
 //
 // Other n_fft (e.g. 533 at 29.97 fps) use k_spec_dft: a direct DFT, one block per frame.
+#include <algorithm>
+
 #include "avse_common.h"
 #include "fft_common.h"
+
+#ifdef AVSE_NO_WPE   // A/B: no occupancy cap
+#define AVSE_WPE4
+#else
+#define AVSE_WPE4 __attribute__((amdgpu_waves_per_eu(4)))
+#endif
 
 namespace avse {
 
@@ -41,10 +49,6 @@ __device__ __forceinline__ float sample_at(const float* __restrict__ s, long lon
     return s[i];
 }
 
-__device__ __forceinline__ float2 sample_pair(const float* __restrict__ s, long long L, long long i, int pad_mode) {
-    if (i >= 0 && i + 1 < L) return *reinterpret_cast<const float2*>(s + i);
-    return make_float2(sample_at(s, L, i, pad_mode), sample_at(s, L, i + 1, pad_mode));
-}
 
 __device__ __forceinline__ unsigned int f2ord(float f) {
     unsigned int u = __float_as_uint(f);
@@ -63,165 +67,219 @@ __device__ __forceinline__ long long out_index(int spf, int n_slices, int n_mels
     return (u * n_mels + m) * (long long)T + t;
 }
 
-// One block per (chunk of CHUNK frames, utterance): wave w owns frames [3w, 3w + 3) of the chunk, so a
-// 21-frame chunk is one pass of 7 waves (was one 64-lane wave walking 7 passes: ~110 us of serial
-// latency per utterance).  Twiddles, window and the Slaney table live in LDS — the per-weight global
-// loads of the mel dot were a dependent-latency chain.  |X| of a frame aliases its FFT buffer.
+// One block of 7 waves per work item (utterance, chunk of CHUNK frames); wave w owns frames [3w, 3w + 3).
+// Round-1 version: 0.198 ms for 4096 segments (5 % of the HBM roofline).  Changes (0.173 ms):
+//  - capped at 128 VGPRs (amdgpu_waves_per_eu(4)) so two ~80-KB blocks share a CU (137 VGPRs allowed one);
+//  - interior frames (the whole 640-sample window inside the signal) load 8-B sample pairs without the
+//    reflect / zero-pad index arithmetic, which stays on the edge frames only (branch-free);
+//  - the mel dot runs over a compile-time 24-bin band (host rows zero-padded, 16-B weight reads);
+//  - step 3 maps items bin-major / frame-minor over the whole chunk, so the complex-STFT store (librosa's
+//    [bin][frame] layout) writes 21-frame runs instead of 8-B scatters (configs[4] STFT 0.65 -> 0.50 ms).
+// Tried: a persistent grid with the next item's samples prefetched into registers during steps 2-4 — the
+// loop-invariant address math the compiler hoisted out of the item loop needed 207-256 VGPRs (one block
+// per CU): 0.224 ms.
 constexpr int WAVES = CHUNK / FPG;     // 7
-constexpr int MEL_LDS_CAP = 6144;      // floats of the [n_mels][max_width] table staged in LDS
+constexpr int MW = 24;                 // padded Slaney band width of the LDS table (host-checked)
 
-template <bool MEL_LDS>
-__global__ __launch_bounds__(64 * WAVES) void k_spec640(SpecArgs a, int n_chunks) {
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// index of sample i after centre padding: reflect (librosa's 2017 default) or zero (then `keep` is false)
+__device__ __forceinline__ int padded_index(int i, int L, int pad_mode, bool& keep) {
+    keep = pad_mode == 0 || (i >= 0 && i < L);
+    if (pad_mode == 0) {
+        const int j = abs(i);
+        return min(j, 2 * (L - 1) - j);
+    }
+    return min(max(i, 0), L - 1);
+}
+
+// lane (f1, n1) of step 1 loads z[n1 + 16 n2] = (x[s0 + 2(n1 + 16 n2)], x[s0 + 2(n1 + 16 n2) + 1]), n2 < 20
+__device__ __forceinline__ void load_frame(float2 (&x)[20], const float* __restrict__ s, int L, int s0, int n1,
+                                           int pad_mode) {
+    if (s0 >= 0 && s0 + 640 <= L) {
+        const float2* p = reinterpret_cast<const float2*>(s + s0) + n1;
+#pragma unroll
+        for (int n2 = 0; n2 < 20; ++n2) x[n2] = p[16 * n2];
+    } else {   // edge frame: branch-free per-sample index arithmetic
+#pragma unroll
+        for (int n2 = 0; n2 < 20; ++n2) {
+            const int i = s0 + 2 * (n1 + 16 * n2);
+            bool k0, k1;
+            const int j0 = padded_index(i, L, pad_mode, k0), j1 = padded_index(i + 1, L, pad_mode, k1);
+            const float v0 = s[j0], v1 = s[j1];
+            x[n2] = make_float2(k0 ? v0 : 0.f, k1 ? v1 : 0.f);
+        }
+    }
+}
+
+template <bool FAST_MEL>
+__global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec640(SpecArgs a, int n_chunks) {
     __shared__ float2 zbuf[WAVES * FPG * ZS];
     __shared__ float dbuf[80 * CHUNK];
     __shared__ float2 twl[640];
     __shared__ float2 winl[320];
-    __shared__ float wmax[WAVES];
-    extern __shared__ __attribute__((aligned(16))) float mel_sm[];   // [n_mels * mw] weights, start, width
+    __shared__ float4 melw4[FAST_MEL ? 80 * MW / 4 : 1];
+    __shared__ int mel_st[80], mel_wd[80];
+    __shared__ float wmax[1][WAVES];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int chunk = blockIdx.x;
-    const long long u = blockIdx.y;
     const int T = a.n_frames;
-    const int t0 = chunk * CHUNK;
-    const int nf = min(CHUNK, T - t0);
-    const int g = FPG * wave;                       // this wave's first frame in the chunk
-    const int ng = max(0, min(FPG, nf - g));
-    const long long L = a.n_samples;
-    const float* __restrict__ sig = a.sig + u * L;
+    const int L = (int)a.n_samples;
     const int n_mels = a.n_mels, mw = a.mel_max_width;
-    float* mel_w = mel_sm;
-    int* mel_st = reinterpret_cast<int*>(mel_sm + (MEL_LDS ? n_mels * mw : 0));
-    int* mel_wd = mel_st + n_mels;
+    const int g = FPG * wave;                       // this wave's first frame in the chunk
 
     for (int i = tid; i < 640; i += 64 * WAVES) twl[i] = a.twiddle[i];
     for (int i = tid; i < 320; i += 64 * WAVES) winl[i] = reinterpret_cast<const float2*>(a.window)[i];
-    if (MEL_LDS)
-        for (int i = tid; i < n_mels * mw; i += 64 * WAVES) mel_w[i] = a.mel_weight[i];
+    if (FAST_MEL)   // host rows are zero-padded to MW
+        for (int i = tid; i < n_mels * MW / 4; i += 64 * WAVES) melw4[i] = reinterpret_cast<const float4*>(a.mel_weight)[i];
     for (int i = tid; i < n_mels; i += 64 * WAVES) {
         mel_st[i] = a.mel_start[i];
         mel_wd[i] = a.mel_width[i];
     }
-    // samples of step 1 (issued before the table barrier so their latency overlaps it)
+
     const int f1 = lane >> 4, n1 = lane & 15;
+    const int item = blockIdx.x;
+    const int u = item / n_chunks, chunk = item - u * n_chunks;
     float2 x[20];
-    if (f1 < ng) {
-        const long long s0 = (long long)(t0 + g + f1) * a.hop - 320;
-#pragma unroll
-        for (int n2 = 0; n2 < 20; ++n2) x[n2] = sample_pair(sig, L, s0 + 2 * (n1 + 16 * n2), a.pad_mode);
+    {
+        const int nf = min(CHUNK, T - chunk * CHUNK);
+        if (f1 < min(FPG, nf - g))
+            load_frame(x, a.sig + (long long)u * L, L, (chunk * CHUNK + g + f1) * a.hop - 320, n1, a.pad_mode);
     }
     __syncthreads();
+    {
+        const int parity = 0;   // (wmax slot of the item)
+        const int t0 = chunk * CHUNK;
+        const int nf = min(CHUNK, T - t0);
+        const int ng = max(0, min(FPG, nf - g));
+        float2* zw = zbuf + wave * FPG * ZS;
 
-    float2* zw = zbuf + wave * FPG * ZS;
-    // ---- step 1: 20-point DFTs over n2, lane = (f, n1) ----
-    if (f1 < ng) {
+        // ---- step 1: 20-point DFTs over n2, lane = (f, n1) ----
         float2 v[20];
 #pragma unroll
         for (int n2 = 0; n2 < 20; ++n2) {
             const float2 w = winl[n1 + 16 * n2];
             v[n2] = make_float2(x[n2].x * w.x, x[n2].y * w.y);
         }
-        dft20(v, twl);
-        // v[5c + d] = Y[c + 4d]; twiddle W320^{n1 k2} = W640^{2 n1 k2}
-        float2* zf = zw + f1 * ZS;
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-#pragma unroll
-            for (int d = 0; d < 5; ++d) {
-                const int k2 = c + 4 * d;
-                float2 y = v[5 * c + d];
-                if (k2) y = cmul(y, twl[(2 * n1 * k2) % 640]);
-                zf[k2 * 17 + n1] = y;
-            }
-    }
-    __syncthreads();
-    // ---- step 2: 16-point DFTs over n1, lane = (f, k2) ----
-    {
-        const int f = lane / 20, k2 = lane - 20 * (lane / 20);
-        const bool act = f < ng;
-        float2 v[16];
-        float2* zf = zw + min(f, FPG - 1) * ZS;
-        if (act) {
-#pragma unroll
-            for (int n = 0; n < 16; ++n) v[n] = zf[k2 * 17 + n];
-        }
-        __syncthreads();
-        if (act) {
-            dft16(v, twl);
-            // v[4c + d] = Z[k2 + 20 (c + 4d)]
+        if (f1 < ng) {
+            dft20(v, twl);
+            // v[5c + d] = Y[c + 4d]; twiddle W320^{n1 k2} = W640^{2 n1 k2}
+            float2* zf = zw + f1 * ZS;
 #pragma unroll
             for (int c = 0; c < 4; ++c)
 #pragma unroll
-                for (int d = 0; d < 4; ++d) zf[k2 + 20 * (c + 4 * d)] = v[4 * c + d];
+                for (int d = 0; d < 5; ++d) {
+                    const int k2 = c + 4 * d;
+                    float2 y = v[5 * c + d];
+                    if (k2) y = cmul(y, twl[(2 * n1 * k2) % 640]);
+                    zf[k2 * 17 + n1] = y;
+                }
         }
-    }
-    __syncthreads();
-    // ---- step 3: real-FFT untangling + magnitude, item = (f, k), k in [0,160]; |X| overwrites Z ----
-    constexpr int IT3 = (FPG * 161 + 63) / 64;
-    float mk[IT3], mm[IT3];
+        lds_barrier();
+        // ---- step 2: 16-point DFTs over n1, lane = (f, k2) ----
+        {
+            const int f = lane / 20, k2 = lane - 20 * (lane / 20);
+            const bool act = f < ng;
+            float2 w[16];
+            float2* zf = zw + min(f, FPG - 1) * ZS;
+            if (act) {
 #pragma unroll
-    for (int j = 0; j < IT3; ++j) {
-        const int it = lane + 64 * j;
-        if (it >= ng * 161) break;
-        const int f = it / 161, k = it - 161 * f;
-        const float2* zf = zw + f * ZS;
-        const float2 zk = zf[k];
-        const float2 zm = zf[k == 0 ? 0 : 320 - k];
-        // E = (Zk + conj Zm)/2 ; O = -i/2 (Zk - conj Zm)
-        const float2 E = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y));
-        const float2 O = make_float2(0.5f * (zk.y + zm.y), -0.5f * (zk.x - zm.x));
-        const float2 WO = cmul(twl[k], O);
-        const float2 X = cadd(E, WO);
-        const float2 Xm = make_float2(E.x - WO.x, -(E.y - WO.y));   // X[320 - k] = conj(E - W^k O)
-        mk[j] = sqrtf(X.x * X.x + X.y * X.y);
-        mm[j] = sqrtf(Xm.x * Xm.x + Xm.y * Xm.y);
-        if (a.stft_ri) {
-            const long long t = t0 + g + f;
-            float2* o = reinterpret_cast<float2*>(a.stft_ri);
-            o[(u * 321 + k) * T + t] = X;
-            if (k != 160) o[(u * 321 + (320 - k)) * T + t] = Xm;
+                for (int n = 0; n < 16; ++n) w[n] = zf[k2 * 17 + n];
+            }
+            lds_barrier();
+            if (act) {
+                dft16(w, twl);
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+#pragma unroll
+                    for (int d = 0; d < 4; ++d) zf[k2 + 20 * (c + 4 * d)] = w[4 * c + d];
+            }
         }
-    }
-    __syncthreads();
+        lds_barrier();
+        // ---- step 3: real-FFT untangling + magnitude over the chunk, item = (k, f), f fastest ----
+        constexpr int IT3 = (161 * CHUNK + 64 * WAVES - 1) / (64 * WAVES);   // 8
+        float mk[IT3], mm[IT3];
 #pragma unroll
-    for (int j = 0; j < IT3; ++j) {
-        const int it = lane + 64 * j;
-        if (it >= ng * 161) break;
-        const int f = it / 161, k = it - 161 * f;
-        float* mf = reinterpret_cast<float*>(zw + f * ZS);
-        mf[k] = mk[j];
-        mf[320 - k] = mm[j];
-    }
-    __syncthreads();
-    // ---- step 4: Slaney mel + dB, item = (f, m) ----
-    float vmax = -INFINITY;
-    for (int it = lane; it < ng * n_mels; it += 64) {
-        const int f = it / n_mels, m = it - n_mels * f;
-        const float* mf = reinterpret_cast<const float*>(zw + f * ZS) + mel_st[m];
-        const float* wm = MEL_LDS ? mel_w + m * mw : a.mel_weight + m * mw;
-        const int wdt = mel_wd[m];
-        float acc = 0.f;
-        for (int j = 0; j < wdt; ++j) acc = fmaf(mf[j], wm[j], acc);
-        const float db = acc > a.amin ? 20.0f * log10f(acc) : a.db_floor;
-        vmax = fmaxf(vmax, db);
-        dbuf[m * CHUNK + g + f] = db;
-    }
+        for (int j = 0; j < IT3; ++j) {
+            const int it = tid + 64 * WAVES * j;
+            const int k = it / CHUNK, f = it - CHUNK * k;
+            if (k > 160 || f >= nf) continue;
+            const float2* zf = zbuf + f * ZS;
+            const float2 zk = zf[k];
+            const float2 zm = zf[k == 0 ? 0 : 320 - k];
+            // E = (Zk + conj Zm)/2 ; O = -i/2 (Zk - conj Zm)
+            const float2 E = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y));
+            const float2 O = make_float2(0.5f * (zk.y + zm.y), -0.5f * (zk.x - zm.x));
+            const float2 WO = cmul(twl[k], O);
+            const float2 X = cadd(E, WO);
+            const float2 Xm = make_float2(E.x - WO.x, -(E.y - WO.y));   // X[320 - k] = conj(E - W^k O)
+            mk[j] = sqrtf(X.x * X.x + X.y * X.y);
+            mm[j] = sqrtf(Xm.x * Xm.x + Xm.y * Xm.y);
+            if (a.stft_ri) {
+                float2* o = reinterpret_cast<float2*>(a.stft_ri) + (long long)u * 321 * T + t0 + f;
+                o[(long long)k * T] = X;
+                if (k != 160) o[(long long)(320 - k) * T] = Xm;
+            }
+        }
+        lds_barrier();
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) vmax = fmaxf(vmax, __shfl_xor(vmax, o));
-    if (lane == 0) wmax[wave] = vmax;
-    __syncthreads();
-    vmax = wmax[0];
+        for (int j = 0; j < IT3; ++j) {
+            const int it = tid + 64 * WAVES * j;
+            const int k = it / CHUNK, f = it - CHUNK * k;
+            if (k > 160 || f >= nf) continue;
+            float* mf = reinterpret_cast<float*>(zbuf + f * ZS);
+            mf[k] = mk[j];
+            mf[320 - k] = mm[j];
+        }
+        if (FAST_MEL) {   // bins [321, 321 + MW) are read by the padded band dots: make them zero
+            for (int it = tid; it < CHUNK * MW; it += 64 * WAVES) {
+                const int f = it / MW, j = it - MW * f;
+                reinterpret_cast<float*>(zbuf + f * ZS)[321 + j] = 0.f;
+            }
+        }
+        lds_barrier();
+        // ---- step 4: Slaney mel + dB, item = (f, m) ----
+        float vmax = -INFINITY;
+        for (int it = lane; it < ng * n_mels; it += 64) {
+            const int f = it >= n_mels ? (it >= 2 * n_mels ? 2 : 1) : 0, m = it - n_mels * f;
+            const float* mf = reinterpret_cast<const float*>(zw + f * ZS) + mel_st[m];
+            float acc = 0.f;
+            if (FAST_MEL) {
+                const float4* wm = melw4 + m * (MW / 4);
 #pragma unroll
-    for (int w = 1; w < WAVES; ++w) vmax = fmaxf(vmax, wmax[w]);
-    // ---- clamp / publish ----
-    const bool single = (n_chunks == 1);
-    const float floor_db = (single && a.top_db >= 0.f) ? vmax - a.top_db : -INFINITY;
-    for (int it = tid; it < n_mels * nf; it += 64 * WAVES) {
-        const int m = it / nf, tl = it - nf * m;
-        const long long oi = out_index(a.spf, a.n_slices, n_mels, T, u, m, t0 + tl);
-        if (oi >= 0) a.mel_db[oi] = fmaxf(dbuf[m * CHUNK + tl], floor_db);
+                for (int q = 0; q < MW / 4; ++q) {
+                    const float4 w = wm[q];
+                    acc = fmaf(mf[4 * q], w.x, acc);
+                    acc = fmaf(mf[4 * q + 1], w.y, acc);
+                    acc = fmaf(mf[4 * q + 2], w.z, acc);
+                    acc = fmaf(mf[4 * q + 3], w.w, acc);
+                }
+            } else {
+                const float* wm = a.mel_weight + m * mw;
+                const int wdt = mel_wd[m];
+                for (int j = 0; j < wdt; ++j) acc = fmaf(mf[j], wm[j], acc);
+            }
+            const float db = acc > a.amin ? 20.0f * log10f(acc) : a.db_floor;
+            vmax = fmaxf(vmax, db);
+            dbuf[m * CHUNK + g + f] = db;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) vmax = fmaxf(vmax, __shfl_xor(vmax, o));
+        if (lane == 0) wmax[parity][wave] = vmax;
+        lds_barrier();
+        vmax = wmax[parity][0];
+#pragma unroll
+        for (int w = 1; w < WAVES; ++w) vmax = fmaxf(vmax, wmax[parity][w]);
+        // ---- clamp / publish ----
+        const bool single = (n_chunks == 1);
+        const float floor_db = (single && a.top_db >= 0.f) ? vmax - a.top_db : -INFINITY;
+        for (int it = tid; it < n_mels * nf; it += 64 * WAVES) {
+            const int m = it / nf, tl = it - nf * m;
+            const long long oi = out_index(a.spf, a.n_slices, n_mels, T, u, m, t0 + tl);
+            if (oi >= 0) a.mel_db[oi] = fmaxf(dbuf[m * CHUNK + tl], floor_db);
+        }
+        if (!single && tid == 0) atomicMax(a.umax + u, f2ord(vmax));
     }
-    if (!single && tid == 0) atomicMax(a.umax + u, f2ord(vmax));
 }
 
 // Direct DFT fallback for n_fft != 640: one 256-thread block per (frame, utterance).
@@ -284,13 +342,16 @@ int launch_spectrogram(const SpecArgs& a, hipStream_t s) {
     const bool need_clamp_pass = a.top_db >= 0.f;
     if (a.n_fft == 640) {
         const int n_chunks = (a.n_frames + CHUNK - 1) / CHUNK;
+        const long long items = (long long)n_chunks * a.n_utt;
+        if (items > INT32_MAX || a.n_samples > INT32_MAX) {
+            set_error("spectrogram batch too large (n_utt * chunks and n_samples must fit in int32)");
+            return 3;   // AVSE_ERR_UNSUPPORTED
+        }
         if (n_chunks > 1) AVSE_HIP_CHECK(hipMemsetAsync(a.umax, 0, sizeof(unsigned) * a.n_utt, s));
-        const bool mel_lds = a.n_mels * a.mel_max_width <= MEL_LDS_CAP;
-        const size_t shm = sizeof(float) * ((mel_lds ? a.n_mels * a.mel_max_width : 0) + 2 * a.n_mels);
-        if (mel_lds)
-            hipLaunchKernelGGL(k_spec640<true>, dim3(n_chunks, (unsigned)a.n_utt), dim3(64 * WAVES), shm, s, a, n_chunks);
+        if (a.n_mels <= 80 && a.mel_max_width == MW)
+            hipLaunchKernelGGL(k_spec640<true>, dim3((unsigned)items), dim3(64 * WAVES), 0, s, a, n_chunks);
         else
-            hipLaunchKernelGGL(k_spec640<false>, dim3(n_chunks, (unsigned)a.n_utt), dim3(64 * WAVES), shm, s, a, n_chunks);
+            hipLaunchKernelGGL(k_spec640<false>, dim3((unsigned)items), dim3(64 * WAVES), 0, s, a, n_chunks);
         AVSE_HIP_CHECK(hipGetLastError());
         if (n_chunks > 1 && need_clamp_pass) {
             hipLaunchKernelGGL(k_spec_clamp, dim3(1024), dim3(256), 0, s, a);

@@ -65,6 +65,7 @@ void avse_ctx_destroy(avse_ctx* ctx);
  *   serial / aud_side                one stream / audio encoder on the side stream
  *   graph (AVSE_GRAPH)               avse_forward replays a hipGraph per argument set
  *   gemm_ksplit_cap (AVSE_GEMM_KSPLIT) cap on k_gemm's split-K factor (0 = none)
+ *   dense_istft (AVSE_DENSE_ISTFT)   avse_istft through the dense pinv + frame scratch + overlap-add pass
  * Unknown names return AVSE_ERR_INVALID. */
 int avse_ctx_set_option(avse_ctx* ctx, const char* name, int value);
 int avse_ctx_get_option(avse_ctx* ctx, const char* name, int* value);

@@ -62,3 +62,20 @@ def test_reconstruct_signal_from_spectrogram_api(gpu):
     ref = R.reconstruct_signal_from_spectrogram(mref, pref, 16000, 640, 160)
     assert got.shape == ref.shape == (16000,)
     assert rel_rms(got, ref) < 1e-4, rel_rms(got, ref)
+
+
+@pytest.mark.parametrize("n_samples", [48000, 47000, 3200])
+def test_fused_istft_matches_dense_path(gpu, n_samples):
+    """k_istft_fused (tridiagonal Gram solve + in-LDS overlap-add) against the dense-pinv / scratch-frame /
+    k_ola path on the same inputs, including a chunk that ends mid-block (47000) and a one-chunk signal."""
+    from avse_amd import _lib, ops
+    rng = np.random.default_rng(11)
+    x = torch.from_numpy(synth_audio(rng, 3, n_samples)).to(gpu)
+    mel, D = ops.spectrogram(x, frames_per_slice=20, return_stft=True)
+    pred = mel + torch.from_numpy(rng.normal(0, 1.0, tuple(mel.shape)).astype(np.float32)).to(gpu)
+    fused = ops.istft(pred, D)
+    with _lib.context(gpu).options(dense_istft=1):
+        dense = ops.istft(pred, D)
+    torch.cuda.synchronize()
+    assert fused.shape == dense.shape
+    assert rel_rms(fused.cpu().numpy(), dense.cpu().numpy()) < 1e-5
