@@ -52,7 +52,15 @@ SIGNATURES = {
     "avse_forward_profile": (_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64,
                                     _c_void_p, _c_void_p, ctypes.POINTER(_flt)]),
     "avse_debug_scratch": (_int, [_c_void_p, _i64, _int, ctypes.POINTER(_c_void_p), ctypes.POINTER(_i64)]),
+    "avse_trainer_create": (_int, [_c_void_p, _c_void_p, _i64, _i64, ctypes.POINTER(_c_void_p)]),
+    "avse_trainer_destroy": (None, [_c_void_p]),
+    "avse_trainer_step": (_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _flt, _flt,
+                                 ctypes.c_uint32, _int, _c_void_p, _c_void_p]),
+    "avse_trainer_read": (_int, [_c_void_p, _int, _c_void_p, _i64]),
+    "avse_trainer_iterations": (_int, [_c_void_p, ctypes.POINTER(_i64)]),
 }
+AVSE_TRAIN_PARAMS, AVSE_TRAIN_GRADS, AVSE_TRAIN_ADAM_M, AVSE_TRAIN_ADAM_V = 0, 1, 2, 3
+AVSE_TRAIN_GRADS_ONLY = 1
 
 
 class AvseError(RuntimeError):

@@ -9,9 +9,14 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 
+struct avse_ctx;
+
 namespace avse {
 
 void set_error(const std::string& msg);
+
+// device index of a context (capi.hip; the training step, train.hip, allocates on the same device)
+int ctx_device_index(const struct ::avse_ctx* c);
 
 // hipFuncSetAttribute(MaxDynamicSharedMemorySize) for `fn` on the CURRENT device, once per (kernel, device)
 // (thread-safe; capi.hip).  Every launcher that needs more than 64 KB of dynamic LDS calls it first.

@@ -1,0 +1,1027 @@
+// One Keras training step of the reference network, fp32, gfx950 — SpeechEnhancementNetwork.train
+// (/root/reference/network.py:177-206: Model.fit with batch_size 16 on the model compiled at network.py:35-36 with
+// optimizers.adam(lr=5e-4) and loss='mean_squared_error').
+//
+// Keras 2.0 training-mode semantics restated here (oracle/keras_train_ref.py restates the same in float64 autograd):
+//   * BatchNormalization (eps 1e-3, momentum 0.99): normalises with the BATCH mean and biased variance over every
+//     axis but the channel, and updates moving_mean / moving_variance <- m * 0.99 + batch * 0.01;
+//   * LeakyReLU(0.3); MaxPooling2D(2, 2, 'same') on even grids (the gradient goes to the window's first maximum);
+//   * Dropout(0.25) after each video pooling (network.py:142-174): kept values scaled by 1 / 0.75.  The mask comes
+//     from a counter-based hash of (seed, layer, element) — reproducible, so the oracle can apply the same mask;
+//   * loss = mean((y - t)^2) over every element; Adam (Keras 2.0: beta1 0.9, beta2 0.999, epsilon 1e-8,
+//     lr_t = lr sqrt(1 - beta2^t) / (1 - beta1^t)).
+//
+// Device work per step (N clips):
+//   forward   per layer: k_conv (fp32 MFMA implicit GEMM, conv.hip) with bias only -> z; column mean, then
+//             column sum of squared deviations (two passes, double finish) -> batch stats + moving-average update;
+//             k_act_fwd: BN + LeakyReLU [+ 2x2 max pool + dropout] -> the next layer's input (the concat buffer
+//             for a_conv5 / v_conv6)
+//   loss      k_mse: loss and dL/dy
+//   backward  per layer, reverse: k_act_bwd (dropout, pool routing, LeakyReLU') -> dL/d(BN output);
+//             column sums of g and g * xhat -> dgamma, dbeta; k_bn_bwd -> dz; column sum of dz -> dbias;
+//             k_wgrad (LDS-tiled reduction over the batch's pixels, deterministic split + ordered reduce) -> dW;
+//             k_conv on repacked weights -> dL/dx (strided convs as multi-phase gathers, transposed convs as strided
+//             convs, dense as a GEMM with the Keras (in, out) matrix)
+//   update    k_adam over the whole canonical parameter blob (moving statistics carry zero gradient: unchanged)
+// Parameters, gradients and Adam moments live in the canonical blob layout (include/avse.h avse_weights_load), so
+// export is a copy; forward / dgrad weight packings are gathered from it by index maps built once on the host.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/avse.h"
+#include "avse_common.h"
+#include "netplan.h"
+
+namespace avse {
+namespace {
+
+constexpr float LRELU = 0.3f;
+constexpr float BN_MOMENTUM = 0.99f;
+
+__host__ __device__ inline uint32_t drop_hash(uint32_t seed, uint32_t layer, uint32_t idx) {
+    uint32_t h = idx * 0x9E3779B1u ^ (seed * 0x85EBCA77u + layer * 0xC2B2AE3Du);
+    h ^= h >> 16;
+    h *= 0x7FEB352Du;
+    h ^= h >> 15;
+    h *= 0x846CA68Bu;
+    h ^= h >> 16;
+    return h;
+}
+
+inline unsigned grid_for(long long n, int block = 256, long long cap = 8192) {
+    long long g = (n + block - 1) / block;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return (unsigned)g;
+}
+
+__global__ void k_gather(float* __restrict__ dst, const int* __restrict__ map, const float* __restrict__ src, long long n) {
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+        const int j = map[i];
+        dst[i] = j >= 0 ? src[j] : 0.f;
+    }
+}
+
+// video [N][128][128][5] -> (x - mean) / std (VideoNormalizer, data_processor.py:208-212) -> [N][128][128][8]
+__global__ void k_prep_video(const float* __restrict__ v, const float* __restrict__ mean, const float* __restrict__ stdv,
+                             float* __restrict__ out, long long npix, int hw) {
+    for (long long p = blockIdx.x * (long long)blockDim.x + threadIdx.x; p < npix; p += (long long)gridDim.x * blockDim.x) {
+        const int q = (int)(p % hw);
+        const float m = mean ? mean[q] : 0.f, s = stdv ? stdv[q] : 1.f;
+        float o[8];
+#pragma unroll
+        for (int c = 0; c < 5; ++c) o[c] = mean ? (v[p * 5 + c] - m) / s : v[p * 5 + c];
+        o[5] = o[6] = o[7] = 0.f;
+        float4* d = reinterpret_cast<float4*>(out + p * 8);
+        d[0] = make_float4(o[0], o[1], o[2], o[3]);
+        d[1] = make_float4(o[4], o[5], o[6], o[7]);
+    }
+}
+
+// audio [N][80][20] -> [N][80][20][8] (expand_dims(-1), network.py:181, channel padded to the 8-wide chunk)
+__global__ void k_prep_audio(const float* __restrict__ a, float* __restrict__ out, long long npix) {
+    for (long long p = blockIdx.x * (long long)blockDim.x + threadIdx.x; p < npix; p += (long long)gridDim.x * blockDim.x) {
+        float4* d = reinterpret_cast<float4*>(out + p * 8);
+        d[0] = make_float4(a[p], 0.f, 0.f, 0.f);
+        d[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+}
+
+// Column reductions over the rows of a [M][ld] matrix (first C columns), one partial per row block:
+//   MODE 0: sum x                       (means, bias gradients)
+//   MODE 1: sum (x - mean)^2            (biased batch variance, second pass)
+//   MODE 2: sum g, sum g * xhat         (BN backward; xhat = (z - mean) * inv from z)
+// grid (ceil(C / 64), nblk), 256 threads = 64 columns x 4 row groups.
+template <int MODE>
+__global__ __launch_bounds__(256) void k_colreduce(const float* __restrict__ x, int ld, const float* __restrict__ z,
+                                                   const float* __restrict__ mean, const float* __restrict__ inv,
+                                                   long long M, int C, long long rows_per_blk, float* __restrict__ part) {
+    __shared__ float s0[4][64], s1[4][64];
+    const int tid = threadIdx.x, cl = tid & 63, rg = tid >> 6;
+    const int c = blockIdx.x * 64 + cl;
+    const long long r0 = blockIdx.y * rows_per_blk, r1 = min(M, r0 + rows_per_blk);
+    float a0 = 0.f, a1 = 0.f;
+    if (c < C) {
+        const float mu = (MODE >= 1) ? mean[c] : 0.f;
+        const float iv = (MODE == 2) ? inv[c] : 0.f;
+        for (long long r = r0 + rg; r < r1; r += 4) {
+            const float v = x[r * ld + c];
+            if (MODE == 0) a0 += v;
+            if (MODE == 1) { const float d = v - mu; a0 = fmaf(d, d, a0); }
+            if (MODE == 2) { a0 += v; a1 = fmaf(v, (z[r * C + c] - mu) * iv, a1); }
+        }
+    }
+    s0[rg][cl] = a0;
+    s1[rg][cl] = a1;
+    __syncthreads();
+    if (rg == 0 && c < C) {
+        part[(long long)blockIdx.y * C + c] = s0[0][cl] + s0[1][cl] + s0[2][cl] + s0[3][cl];
+        if (MODE == 2)
+            part[(long long)(gridDim.y + blockIdx.y) * C + c] = s1[0][cl] + s1[1][cl] + s1[2][cl] + s1[3][cl];
+    }
+}
+
+// Finish a column reduction in double, in block order (deterministic):
+//   STAGE 0: mean[c] = S / M
+//   STAGE 1: var = S / M (biased), inv = 1 / sqrt(var + eps), moving stats <- m * 0.99 + batch * 0.01
+//   STAGE 2: dbeta = S0, dgamma = S1 (into the gradient blob)
+//   STAGE 3: out[c] = S (bias gradient)
+template <int STAGE>
+__global__ void k_colfinish(const float* __restrict__ part, int nblk, int C, long long M, float* __restrict__ mean,
+                            float* __restrict__ inv, float* __restrict__ mm, float* __restrict__ mv,
+                            float* __restrict__ out0, float* __restrict__ out1) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    double s = 0, t = 0;
+    for (int b = 0; b < nblk; ++b) {
+        s += part[(long long)b * C + c];
+        if (STAGE == 2) t += part[(long long)(nblk + b) * C + c];
+    }
+    if (STAGE == 0) mean[c] = (float)(s / (double)M);
+    if (STAGE == 1) {
+        const double var = s / (double)M;
+        inv[c] = (float)(1.0 / std::sqrt(var + (double)kBnEps));
+        mm[c] = mm[c] * BN_MOMENTUM + mean[c] * (1.f - BN_MOMENTUM);
+        mv[c] = mv[c] * BN_MOMENTUM + (float)var * (1.f - BN_MOMENTUM);
+    }
+    if (STAGE == 2) {
+        out0[c] = (float)s;   // dbeta
+        out1[c] = (float)t;   // dgamma
+    }
+    if (STAGE == 3) out0[c] = (float)s;
+}
+
+struct ActArgs {
+    const float* z;          // [N][Hq][Wq][C] pre-BN conv output
+    int N, Hq, Wq, C;
+    const float* mean;
+    const float* inv;
+    const float* gamma;
+    const float* beta;
+    int pool;
+    float drop;              // dropout rate (0 = none)
+    uint32_t seed, layer;
+    float* out;              // layer output (pooled grid when pool)
+    long long out_clip;
+    int out_pix, out_c;
+};
+
+__device__ __forceinline__ float bn_lrelu(const ActArgs& a, long long zi, int c, float& yhat) {
+    yhat = fmaf(a.gamma[c], (a.z[zi] - a.mean[c]) * a.inv[c], a.beta[c]);
+    return yhat >= 0.f ? yhat : LRELU * yhat;
+}
+
+__device__ __forceinline__ float drop_scale(const ActArgs& a, long long idx) {
+    if (a.drop <= 0.f) return 1.f;
+    const uint32_t h = drop_hash(a.seed, a.layer, (uint32_t)idx);
+    return ((float)(h >> 8) * (1.f / 16777216.f)) >= a.drop ? 1.f / (1.f - a.drop) : 0.f;
+}
+
+// forward: y = LeakyReLU(BN(z)) [-> 2x2 max pool -> dropout], one thread per output element
+__global__ void k_act_fwd(ActArgs a) {
+    const int Ho = a.pool ? a.Hq / 2 : a.Hq, Wo = a.pool ? a.Wq / 2 : a.Wq;
+    const long long total = (long long)a.N * Ho * Wo * a.C;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+        const int c = (int)(i % a.C);
+        const long long p = i / a.C;
+        const int ox = (int)(p % Wo), oy = (int)((p / Wo) % Ho), n = (int)(p / ((long long)Wo * Ho));
+        float y, yh;
+        if (a.pool) {
+            y = -INFINITY;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const long long zi = (((long long)n * a.Hq + 2 * oy + (e >> 1)) * a.Wq + 2 * ox + (e & 1)) * a.C + c;
+                y = fmaxf(y, bn_lrelu(a, zi, c, yh));
+            }
+        } else {
+            y = bn_lrelu(a, i, c, yh);
+        }
+        y *= drop_scale(a, i);
+        a.out[n * a.out_clip + (long long)(oy * Wo + ox) * a.out_pix + a.out_c + c] = y;
+    }
+}
+
+// backward: g_hat = dL/d(BN output) at full resolution from dL/d(layer output); pool: the window's first maximum
+__global__ void k_act_bwd(ActArgs a, const float* __restrict__ gout, long long g_clip, int g_pix, int g_c,
+                          float* __restrict__ ghat) {
+    const int Ho = a.pool ? a.Hq / 2 : a.Hq, Wo = a.pool ? a.Wq / 2 : a.Wq;
+    const long long total = (long long)a.N * Ho * Wo * a.C;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+        const int c = (int)(i % a.C);
+        const long long p = i / a.C;
+        const int ox = (int)(p % Wo), oy = (int)((p / Wo) % Ho), n = (int)(p / ((long long)Wo * Ho));
+        const float g = gout[n * g_clip + (long long)(oy * Wo + ox) * g_pix + g_c + c] * drop_scale(a, i);
+        if (a.pool) {
+            float best = -INFINITY, bh = 0.f;
+            int be = 0;
+            long long zis[4];
+            float yhs[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                zis[e] = (((long long)n * a.Hq + 2 * oy + (e >> 1)) * a.Wq + 2 * ox + (e & 1)) * a.C + c;
+                const float y = bn_lrelu(a, zis[e], c, yhs[e]);
+                if (y > best) { best = y; be = e; bh = yhs[e]; }
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) ghat[zis[e]] = (e == be) ? g * (bh >= 0.f ? 1.f : LRELU) : 0.f;
+        } else {
+            float yh;
+            (void)bn_lrelu(a, i, c, yh);
+            ghat[i] = g * (yh >= 0.f ? 1.f : LRELU);
+        }
+    }
+}
+
+// dz = gamma * inv * (g - dbeta / M - xhat * dgamma / M), in place over g
+__global__ void k_bn_bwd(const float* __restrict__ z, float* __restrict__ g, long long M, int C, const float* __restrict__ mean,
+                         const float* __restrict__ inv, const float* __restrict__ gamma, const float* __restrict__ dbeta,
+                         const float* __restrict__ dgamma) {
+    const long long total = M * C;
+    const float rM = 1.f / (float)M;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+        const int c = (int)(i % C);
+        const float xh = (z[i] - mean[c]) * inv[c];
+        g[i] = gamma[c] * inv[c] * (g[i] - dbeta[c] * rM - xh * dgamma[c] * rM);
+    }
+}
+
+// mean squared error (network.py:36, Keras mean over every element): per-block partial loss + dL/dy (channel stride gcs)
+__global__ __launch_bounds__(256) void k_mse(const float* __restrict__ y, const float* __restrict__ t, long long n, int gcs,
+                                             float* __restrict__ g, float* __restrict__ part) {
+    __shared__ float red[256];
+    float acc = 0.f;
+    const float s = 2.f / (float)n;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+        const float d = y[i * gcs] - t[i];
+        acc = fmaf(d, d, acc);
+        g[i * gcs] = s * d;
+    }
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+__global__ void k_mse_finish(const float* __restrict__ part, int nblk, long long n, float* __restrict__ loss) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    double s = 0;
+    for (int b = 0; b < nblk; ++b) s += part[b];
+    *loss = (float)(s / (double)n);
+}
+
+// Weight gradient dW[tap][a][b] = sum over (n, y, x) of G[n][y*sy + dy_t][x*sx + dx_t][a] * H[n][y][x][b]
+// (conv: G = input, H = dz; transposed conv: G = dz, H = input; dense: 1 x 1 grids).  Block = 64 a x 64 b of one tap
+// over one split of the rows; 256 threads x 4 x 4 outputs; 16-row chunks of G and H staged in LDS.
+struct WgArgs {
+    const float* G;
+    int Hg, Wg, gcs;
+    long long g_clip;
+    const float* H;
+    int Hh, Wh, hcs;
+    long long h_clip;
+    int N, sy, sx;
+    int A, B;
+    int ntaps;
+    const int2* taps;
+    long long rows_per_split;
+    float* part;             // [splits][ntaps][A][B]
+};
+
+__global__ __launch_bounds__(256) void k_wgrad(WgArgs w) {
+    __shared__ float gs[16][68], hs[16][68];
+    const int tid = threadIdx.x, ta = tid >> 4, tb = tid & 15;
+    const int nbt = (w.B + 63) / 64;
+    const int a0 = (blockIdx.x / nbt) * 64, b0 = (blockIdx.x % nbt) * 64;
+    const int tap = blockIdx.y;
+    const int2 t = w.taps[tap];
+    const long long R = (long long)w.N * w.Hh * w.Wh;
+    const long long r0 = blockIdx.z * w.rows_per_split, r1 = min(R, r0 + w.rows_per_split);
+    float acc[4][4] = {};
+    const int lr = tid >> 4, lc = (tid & 15) * 4;   // loader: row lr of the chunk, 4 columns lc..lc+3
+    for (long long rc = r0; rc < r1; rc += 16) {
+        const long long r = rc + lr;
+        float4 gv = make_float4(0.f, 0.f, 0.f, 0.f), hv = gv;
+        if (r < r1) {
+            const int x = (int)(r % w.Wh), y = (int)((r / w.Wh) % w.Hh), n = (int)(r / ((long long)w.Wh * w.Hh));
+            const float* hp = w.H + n * w.h_clip + (long long)(y * w.Wh + x) * w.hcs + b0 + lc;
+            if (b0 + lc + 3 < w.B) hv = make_float4(hp[0], hp[1], hp[2], hp[3]);
+            else {
+                if (b0 + lc < w.B) hv.x = hp[0];
+                if (b0 + lc + 1 < w.B) hv.y = hp[1];
+                if (b0 + lc + 2 < w.B) hv.z = hp[2];
+            }
+            const int gy = y * w.sy + t.x, gx = x * w.sx + t.y;
+            if (gy >= 0 && gy < w.Hg && gx >= 0 && gx < w.Wg) {
+                const float* gp = w.G + n * w.g_clip + (long long)(gy * w.Wg + gx) * w.gcs + a0 + lc;
+                if (a0 + lc + 3 < w.A) gv = make_float4(gp[0], gp[1], gp[2], gp[3]);
+                else {
+                    if (a0 + lc < w.A) gv.x = gp[0];
+                    if (a0 + lc + 1 < w.A) gv.y = gp[1];
+                    if (a0 + lc + 2 < w.A) gv.z = gp[2];
+                }
+            }
+        }
+        __syncthreads();
+        *reinterpret_cast<float4*>(&gs[lr][lc]) = gv;
+        *reinterpret_cast<float4*>(&hs[lr][lc]) = hv;
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const float4 ga = *reinterpret_cast<const float4*>(&gs[k][ta * 4]);
+            const float4 hb = *reinterpret_cast<const float4*>(&hs[k][tb * 4]);
+            const float av[4] = {ga.x, ga.y, ga.z, ga.w}, bv[4] = {hb.x, hb.y, hb.z, hb.w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(av[i], bv[j], acc[i][j]);
+        }
+    }
+    float* out = w.part + ((long long)blockIdx.z * w.ntaps + tap) * w.A * w.B;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int a = a0 + ta * 4 + i;
+        if (a >= w.A) continue;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int b = b0 + tb * 4 + j;
+            if (b < w.B) out[(long long)a * w.B + b] = acc[i][j];
+        }
+    }
+}
+
+__global__ void k_sum_splits(const float* __restrict__ part, int splits, long long n, float* __restrict__ out) {
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+        float s = part[i];
+        for (int z = 1; z < splits; ++z) s += part[(long long)z * n + i];
+        out[i] = s;
+    }
+}
+
+// Keras 2.0 Adam (optimizers.py): m = b1 m + (1 - b1) g; v = b2 v + (1 - b2) g^2; p -= lr_t m / (sqrt(v) + eps)
+__global__ void k_adam(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m, float* __restrict__ v,
+                       long long n, float lr_t, float b1, float b2, float eps) {
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+        const float gi = g[i];
+        const float mi = b1 * m[i] + (1.f - b1) * gi;
+        const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+        m[i] = mi;
+        v[i] = vi;
+        p[i] -= lr_t * mi / (sqrtf(vi) + eps);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// host plan
+// ------------------------------------------------------------------------------------------------------------
+struct TLayer {
+    LayerDef L;
+    int cin_pad = 0;          // channel stride of this layer's input tensor
+    int hq = 1, wq = 1;       // conv output grid (full resolution)
+    int ho = 1, wo = 1;       // after pool
+    long long o_k = 0, o_b = 0, o_g = -1, o_be = -1, o_mm = -1, o_mv = -1;   // canonical blob offsets
+    // forward conv (k_conv), packed [phase][cout][kpad] gathered from the blob
+    int nphase = 1;
+    ConvPhase ph[MAX_PHASES];
+    std::vector<int2> taps;
+    long long fw_off = 0;     // offset in the forward packed buffer
+    int2* d_taps = nullptr;
+    // dgrad
+    bool dgrad = false;
+    int dg_nphase = 1, dg_hq = 1, dg_wq = 1, dg_sy = 1, dg_sx = 1, dg_oys = 1, dg_oxs = 1, dg_ci = 0;
+    ConvPhase dg_ph[MAX_PHASES];
+    std::vector<int2> dg_taps;
+    long long dg_off = 0;
+    int2* d_dg_taps = nullptr;
+    // wgrad taps (dy, dx) per Keras tap ky * kw + kx
+    std::vector<int2> wg_taps;
+    int2* d_wg_taps = nullptr;
+    // tensors
+    float* in = nullptr;      // this layer's input [N][hin][win][cin_pad] (or a concat view)
+    long long in_clip = 0;
+    float* z = nullptr;       // [N][hq][wq][cout] pre-BN (the output itself for d_deconv6, channel stride zc)
+    int zc = 0;
+    float* mean = nullptr;
+    float* inv = nullptr;
+    float* gin = nullptr;     // dL/d(input), same layout as `in` (only when dgrad)
+};
+
+}  // namespace
+}  // namespace avse
+
+using namespace avse;
+
+struct avse_trainer {
+    int device = 0;
+    int64_t max_n = 0;
+    int64_t nparams = 0;
+    int64_t step = 0;         // Adam iterations done (Keras `iterations`)
+    std::vector<TLayer> layers;
+    float *P = nullptr, *Gr = nullptr, *Mo = nullptr, *Vo = nullptr;
+    float *wfwd = nullptr, *wdg = nullptr;
+    int *map_fwd = nullptr, *map_dg = nullptr;
+    long long n_fwd = 0, n_dg = 0;
+    float *ones = nullptr, *zeros = nullptr;
+    float *in_audio = nullptr, *in_video = nullptr, *concat = nullptr, *g6 = nullptr, *ghat = nullptr;
+    float* red = nullptr;     // column-reduction / loss partials
+    long long red_floats = 0;
+    float* wpart = nullptr;   // wgrad split partials
+    long long wpart_floats = 0;
+    float* loss = nullptr;
+    std::vector<void*> allocs;
+};
+
+namespace {
+
+int tfail(int code, const std::string& msg) {
+    set_error(msg);
+    return code;
+}
+
+template <typename T>
+int talloc(avse_trainer* t, T** p, size_t count) {
+    void* q = nullptr;
+    if (hipMalloc(&q, std::max<size_t>(count, 1) * sizeof(T)) != hipSuccess) return tfail(AVSE_ERR_OOM, "hipMalloc failed (trainer)");
+    if (hipMemset(q, 0, std::max<size_t>(count, 1) * sizeof(T)) != hipSuccess) return tfail(AVSE_ERR_HIP, "hipMemset failed");
+    t->allocs.push_back(q);
+    *p = reinterpret_cast<T*>(q);
+    return 0;
+}
+
+long long kpad_of(int ntaps, int cp) { return ((long long)ntaps * cp + 31) / 32 * 32; }
+
+// Keras kernel element index for (ky, kx, in-channel c_in, out-channel c_out) of layer L
+long long kidx(const LayerDef& L, int ky, int kx, int ci, int co) {
+    if (L.kind == DENSE) return (long long)ci * L.cout + co;
+    if (L.kind == CONV) return (((long long)ky * L.kw + kx) * L.cin + ci) * L.cout + co;
+    return (((long long)ky * L.kw + kx) * L.cout + co) * L.cin + ci;   // transposed conv (kh, kw, cout, cin)
+}
+
+int build_plan(avse_trainer* t, const float* host_blob) {
+    t->layers.resize(kNumLayers);
+    long long off = 0;
+    std::vector<int> mf, md;   // forward / dgrad gather maps
+    for (int i = 0; i < kNumLayers; ++i) {
+        TLayer& T = t->layers[i];
+        const LayerDef& L = kLayers[i];
+        T.L = L;
+        T.cin_pad = (L.kind == DENSE) ? L.cin : ((L.cin + 7) / 8) * 8;
+        T.o_k = off;
+        off += (long long)L.kh * L.kw * L.cin * L.cout;
+        T.o_b = off;
+        off += L.cout;
+        if (L.bn) {
+            T.o_g = off; T.o_be = off + L.bn_channels; T.o_mm = off + 2 * L.bn_channels; T.o_mv = off + 3 * L.bn_channels;
+            off += 4LL * L.bn_channels;
+        }
+        const int pt = (L.kind == CONV) ? same_pad_before(L.hin, L.kh, L.sh) : std::max(L.kh - L.sh, 0) / 2;
+        const int pl = (L.kind == CONV) ? same_pad_before(L.win, L.kw, L.sw) : std::max(L.kw - L.sw, 0) / 2;
+        // ---- forward phases / taps (as capi.hip build_layer) ----
+        std::vector<std::vector<std::pair<int, int>>> ptaps;
+        if (L.kind == DENSE) {
+            T.nphase = 1;
+            ptaps.push_back({{0, 0}});
+            T.taps.push_back(make_int2(0, 0));
+            T.ph[0] = ConvPhase{0, 0, 1, 0, 0, 0};
+        } else if (L.kind == CONV) {
+            T.hq = same_out(L.hin, L.sh);
+            T.wq = same_out(L.win, L.sw);
+            T.nphase = 1;
+            std::vector<std::pair<int, int>> pl_;
+            for (int ky = 0; ky < L.kh; ++ky)
+                for (int kx = 0; kx < L.kw; ++kx) {
+                    pl_.push_back({ky, kx});
+                    T.taps.push_back(make_int2(ky - pt, kx - pl));
+                }
+            ptaps.push_back(pl_);
+            T.ph[0] = ConvPhase{0, 0, (int)pl_.size(), 0, 0, 0};
+        } else {
+            T.hq = L.hin * L.sh;
+            T.wq = L.win * L.sw;
+            T.nphase = L.sh * L.sw;
+            if (T.nphase > MAX_PHASES) return tfail(AVSE_ERR_UNSUPPORTED, "deconv stride too large");
+            for (int py = 0; py < L.sh; ++py)
+                for (int px = 0; px < L.sw; ++px) {
+                    std::vector<std::pair<int, int>> pl_;
+                    const int toff = (int)T.taps.size();
+                    for (int ky = 0; ky < L.kh; ++ky) {
+                        const int ry = py + pt - ky;
+                        if (((ry % L.sh) + L.sh) % L.sh) continue;
+                        for (int kx = 0; kx < L.kw; ++kx) {
+                            const int rx = px + pl - kx;
+                            if (((rx % L.sw) + L.sw) % L.sw) continue;
+                            pl_.push_back({ky, kx});
+                            T.taps.push_back(make_int2(ry / L.sh, rx / L.sw));
+                        }
+                    }
+                    T.ph[py * L.sw + px] = ConvPhase{py, px, (int)pl_.size(), 0, 0, toff};
+                    ptaps.push_back(pl_);
+                }
+        }
+        T.ho = L.pool ? T.hq / 2 : T.hq;
+        T.wo = L.pool ? T.wq / 2 : T.wq;
+        T.fw_off = (long long)mf.size();
+        long long woff = 0;
+        for (int p = 0; p < T.nphase; ++p) {
+            const int cp = T.cin_pad;
+            const long long kp = kpad_of((int)ptaps[p].size(), cp);
+            T.ph[p].kpad = (int)kp;
+            T.ph[p].w_off = woff;
+            const size_t base = mf.size();
+            mf.resize(base + (size_t)(L.cout * kp), -1);
+            for (int n = 0; n < L.cout; ++n)
+                for (size_t j = 0; j < ptaps[p].size(); ++j)
+                    for (int c = 0; c < L.cin; ++c)
+                        mf[base + (size_t)n * kp + j * cp + c] =
+                            (int)(T.o_k + kidx(L, ptaps[p][j].first, ptaps[p][j].second, c, n));
+            woff += (long long)L.cout * kp;
+        }
+        // ---- weight-gradient taps: Keras tap order, offsets (ky - pt, kx - pl) on the strided grid ----
+        for (int ky = 0; ky < L.kh; ++ky)
+            for (int kx = 0; kx < L.kw; ++kx) T.wg_taps.push_back(make_int2(ky - (L.kind == DENSE ? 0 : pt), kx - (L.kind == DENSE ? 0 : pl)));
+        // ---- dgrad: not for the first layer of a branch (its input is data) ----
+        T.dgrad = !(i == 0 || std::strcmp(L.name, "v_conv1") == 0);
+        if (T.dgrad) {
+            const int cpi = (L.cout % 8) ? ((L.cout + 7) / 8) * 8 : L.cout;   // dz channel stride (d_deconv6: 8)
+            T.dg_ci = (L.kind == DENSE) ? L.cout : cpi;
+            std::vector<std::vector<std::pair<int, int>>> dtaps;
+            if (L.kind == DENSE) {
+                T.dg_nphase = 1;
+                dtaps.push_back({{0, 0}});
+                T.dg_taps.push_back(make_int2(0, 0));
+                T.dg_ph[0] = ConvPhase{0, 0, 1, 0, 0, 0};
+            } else if (L.kind == CONV) {
+                // dx[iy], iy = q s + r: taps ky = r + pt (mod s), dz row q + (r + pt - ky) / s
+                if (L.hin % L.sh || L.win % L.sw) return tfail(AVSE_ERR_UNSUPPORTED, "conv dgrad needs input dims divisible by the stride");
+                T.dg_nphase = L.sh * L.sw;
+                T.dg_hq = L.hin / L.sh;
+                T.dg_wq = L.win / L.sw;
+                T.dg_oys = L.sh;
+                T.dg_oxs = L.sw;
+                for (int ry = 0; ry < L.sh; ++ry)
+                    for (int rx = 0; rx < L.sw; ++rx) {
+                        std::vector<std::pair<int, int>> pl_;
+                        const int toff = (int)T.dg_taps.size();
+                        for (int ky = 0; ky < L.kh; ++ky) {
+                            const int dy = ry + pt - ky;
+                            if (((dy % L.sh) + L.sh) % L.sh) continue;
+                            for (int kx = 0; kx < L.kw; ++kx) {
+                                const int dx = rx + pl - kx;
+                                if (((dx % L.sw) + L.sw) % L.sw) continue;
+                                pl_.push_back({ky, kx});
+                                T.dg_taps.push_back(make_int2(dy / L.sh, dx / L.sw));
+                            }
+                        }
+                        if (pl_.empty()) return tfail(AVSE_ERR_UNSUPPORTED, "conv dgrad phase without taps");
+                        T.dg_ph[ry * L.sw + rx] = ConvPhase{ry, rx, (int)pl_.size(), 0, 0, toff};
+                        dtaps.push_back(pl_);
+                    }
+            } else {
+                // transposed conv: din[iy] = sum_ky dout[iy s + ky - pt] W[ky] (a strided conv of dout)
+                T.dg_nphase = 1;
+                T.dg_hq = L.hin;
+                T.dg_wq = L.win;
+                T.dg_sy = L.sh;
+                T.dg_sx = L.sw;
+                std::vector<std::pair<int, int>> pl_;
+                for (int ky = 0; ky < L.kh; ++ky)
+                    for (int kx = 0; kx < L.kw; ++kx) {
+                        pl_.push_back({ky, kx});
+                        T.dg_taps.push_back(make_int2(ky - pt, kx - pl));
+                    }
+                dtaps.push_back(pl_);
+                T.dg_ph[0] = ConvPhase{0, 0, (int)pl_.size(), 0, 0, 0};
+            }
+            T.dg_off = (long long)md.size();
+            long long doff = 0;
+            for (int p = 0; p < T.dg_nphase; ++p) {
+                const int cp = T.dg_ci;
+                const long long kp = kpad_of((int)dtaps[p].size(), cp);
+                T.dg_ph[p].kpad = (int)kp;
+                T.dg_ph[p].w_off = doff;
+                const size_t base = md.size();
+                md.resize(base + (size_t)(L.cin * kp), -1);
+                for (int n = 0; n < L.cin; ++n)          // output channel of dgrad = the layer's input channel
+                    for (size_t j = 0; j < dtaps[p].size(); ++j)
+                        for (int c = 0; c < L.cout; ++c)   // reduction channel = the layer's output channel
+                            md[base + (size_t)n * kp + j * cp + c] =
+                                (int)(T.o_k + kidx(L, dtaps[p][j].first, dtaps[p][j].second, n, c));
+                doff += (long long)L.cin * kp;
+            }
+        }
+    }
+    if (off != blob_floats()) return tfail(AVSE_ERR_INVALID, "trainer plan / blob size mismatch");
+    t->nparams = off;
+    t->n_fwd = (long long)mf.size();
+    t->n_dg = (long long)md.size();
+    if (int rc = talloc(t, &t->map_fwd, mf.size())) return rc;
+    if (int rc = talloc(t, &t->map_dg, md.size())) return rc;
+    if (int rc = talloc(t, &t->wfwd, mf.size())) return rc;
+    if (int rc = talloc(t, &t->wdg, md.size())) return rc;
+    AVSE_HIP_CHECK(hipMemcpy(t->map_fwd, mf.data(), mf.size() * sizeof(int), hipMemcpyHostToDevice));
+    AVSE_HIP_CHECK(hipMemcpy(t->map_dg, md.data(), md.size() * sizeof(int), hipMemcpyHostToDevice));
+    for (auto& T : t->layers) {
+        if (int rc = talloc(t, &T.d_taps, T.taps.size())) return rc;
+        AVSE_HIP_CHECK(hipMemcpy(T.d_taps, T.taps.data(), T.taps.size() * sizeof(int2), hipMemcpyHostToDevice));
+        if (int rc = talloc(t, &T.d_wg_taps, T.wg_taps.size())) return rc;
+        AVSE_HIP_CHECK(hipMemcpy(T.d_wg_taps, T.wg_taps.data(), T.wg_taps.size() * sizeof(int2), hipMemcpyHostToDevice));
+        if (T.dgrad) {
+            if (int rc = talloc(t, &T.d_dg_taps, T.dg_taps.size())) return rc;
+            AVSE_HIP_CHECK(hipMemcpy(T.d_dg_taps, T.dg_taps.data(), T.dg_taps.size() * sizeof(int2), hipMemcpyHostToDevice));
+        }
+    }
+    // parameters, gradients, Adam moments
+    if (int rc = talloc(t, &t->P, off)) return rc;
+    if (int rc = talloc(t, &t->Gr, off)) return rc;
+    if (int rc = talloc(t, &t->Mo, off)) return rc;
+    if (int rc = talloc(t, &t->Vo, off)) return rc;
+    AVSE_HIP_CHECK(hipMemcpy(t->P, host_blob, off * sizeof(float), hipMemcpyHostToDevice));
+    return 0;
+}
+
+// wgrad work split over the reduction rows: ~2048 blocks in total, >= 256 rows per split
+long long wg_splits(const TLayer& T, int64_t N) {
+    const LayerDef& L = T.L;
+    const int A = (L.kind == DECONV) ? L.cout : L.cin, B = (L.kind == DECONV) ? L.cin : L.cout;
+    const long long R = N * (long long)((L.kind == DECONV) ? L.hin * L.win : T.hq * T.wq);
+    const long long tiles = (long long)((A + 63) / 64) * ((B + 63) / 64) * L.kh * L.kw;
+    return std::max(1LL, std::min((2048 + tiles - 1) / tiles, (R + 255) / 256));
+}
+
+int alloc_tensors(avse_trainer* t) {
+    const long long N = t->max_n;
+    // unit scale / zero shift of the bias-only and dgrad convolutions: one entry per output channel (the widest
+    // is enc_dense's input gradient, 5248 channels)
+    int cmax = 0;
+    for (int i = 0; i < kNumLayers; ++i) cmax = std::max({cmax, kLayers[i].cin, kLayers[i].cout});
+    std::vector<float> one(cmax, 1.f);
+    if (int rc = talloc(t, &t->ones, cmax)) return rc;
+    if (int rc = talloc(t, &t->zeros, cmax)) return rc;
+    AVSE_HIP_CHECK(hipMemcpy(t->ones, one.data(), cmax * sizeof(float), hipMemcpyHostToDevice));
+    if (int rc = talloc(t, &t->in_audio, N * 80 * 20 * 8)) return rc;
+    if (int rc = talloc(t, &t->in_video, N * 128 * 128 * 8)) return rc;
+    if (int rc = talloc(t, &t->concat, N * 5248)) return rc;
+    if (int rc = talloc(t, &t->g6, N * 80 * 20 * 8)) return rc;
+    long long zmax = 0, red = 0, wmax = 0;
+    for (int i = 0; i < kNumLayers; ++i) {
+        TLayer& T = t->layers[i];
+        const LayerDef& L = T.L;
+        T.zc = (L.cout % 8 && L.kind != DENSE) ? ((L.cout + 7) / 8) * 8 : L.cout;
+        const long long zel = N * T.hq * T.wq * T.zc;
+        zmax = std::max(zmax, zel);
+        if (int rc = talloc(t, &T.z, zel)) return rc;
+        if (L.bn) {
+            if (int rc = talloc(t, &T.mean, L.bn_channels)) return rc;
+            if (int rc = talloc(t, &T.inv, L.bn_channels)) return rc;
+        }
+        const long long rows = N * T.hq * T.wq * (L.kind == DENSE ? L.cout / std::max(L.bn_channels, 1) : 1);
+        red = std::max(red, 2 * ((rows + 4095) / 4096 + 1) * (long long)std::max(L.cout, 64));
+    }
+    for (int i = 0; i < kNumLayers; ++i) {   // after zc: wg_splits reads the grids
+        const TLayer& T = t->layers[i];
+        long long mx = 0;
+        for (int64_t n = 1; n <= N; n = (n < N && 2 * n > N) ? N : 2 * n) mx = std::max(mx, wg_splits(T, n));
+        wmax = std::max(wmax, (long long)T.L.kh * T.L.kw * T.L.cin * T.L.cout * mx);
+    }
+    if (int rc = talloc(t, &t->ghat, zmax)) return rc;
+    t->red_floats = std::max(red, 1LL << 16);
+    if (int rc = talloc(t, &t->red, t->red_floats)) return rc;
+    t->wpart_floats = wmax;
+    if (int rc = talloc(t, &t->wpart, wmax)) return rc;
+    if (int rc = talloc(t, &t->loss, 1)) return rc;
+    // layer inputs: the previous layer's output tensor; the first layers read the prepared inputs
+    for (int i = 0; i < kNumLayers; ++i) {
+        TLayer& T = t->layers[i];
+        const LayerDef& L = T.L;
+        if (i == 0) { T.in = t->in_audio; T.in_clip = 80 * 20 * 8; }
+        else if (std::strcmp(L.name, "v_conv1") == 0) { T.in = t->in_video; T.in_clip = 128 * 128 * 8; }
+        else if (std::strcmp(L.name, "enc_dense") == 0) { T.in = t->concat; T.in_clip = 5248; }
+        else {
+            const long long el = (long long)L.hin * L.win * T.cin_pad;
+            if (int rc = talloc(t, &T.in, N * el)) return rc;
+            T.in_clip = el;
+        }
+        if (T.dgrad) {
+            if (int rc = talloc(t, &T.gin, N * T.in_clip)) return rc;
+        }
+    }
+    return 0;
+}
+
+// where layer i's output goes (and its gradient comes from): next input, or the concat buffer
+void out_view(avse_trainer* t, int i, float** buf, float** gbuf, long long* clip, int* pix, int* coff) {
+    const TLayer& T = t->layers[i];
+    const char* nm = T.L.name;
+    *pix = std::strcmp(nm, "dec_dense2") == 0 ? 128 : T.L.cout;   // dec_dense2: Reshape(5, 5, 128) (network.py:76)
+    if (std::strcmp(nm, "a_conv5") == 0 || std::strcmp(nm, "v_conv6") == 0) {
+        const TLayer& E = t->layers[11];   // enc_dense
+        *buf = t->concat;
+        *gbuf = E.gin;
+        *clip = 5248;
+        *coff = std::strcmp(nm, "a_conv5") == 0 ? 0 : 3200;
+        return;
+    }
+    const TLayer& Nx = t->layers[i + 1];
+    *buf = Nx.in;
+    *gbuf = Nx.gin;
+    *clip = Nx.in_clip;
+    *coff = 0;
+}
+
+ConvArgs fwd_args(avse_trainer* t, const TLayer& T, int64_t N) {
+    const LayerDef& L = T.L;
+    ConvArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.in = T.in;
+    a.out = T.z;
+    a.w = t->wfwd + T.fw_off;
+    a.scale = t->ones;
+    a.shift = t->P + T.o_b;
+    a.taps = T.d_taps;
+    a.N = (int)N;
+    a.Hi = L.hin;
+    a.Wi = L.win;
+    a.Ci = T.cin_pad;
+    a.in_clip_stride = T.in_clip;
+    a.Hq = (L.kind == DECONV) ? L.hin : T.hq;
+    a.Wq = (L.kind == DECONV) ? L.win : T.wq;
+    a.sy = (L.kind == CONV) ? L.sh : 1;
+    a.sx = (L.kind == CONV) ? L.sw : 1;
+    a.oys = (L.kind == DECONV) ? L.sh : 1;
+    a.oxs = (L.kind == DECONV) ? L.sw : 1;
+    a.Ho = T.hq;
+    a.Wo = T.wq;
+    a.Co = L.cout;
+    a.out_clip_stride = (long long)T.hq * T.wq * T.zc;
+    a.out_pix_stride = T.zc;
+    a.out_c_off = 0;
+    a.pool = 0;
+    a.act = 0;
+    a.nphase = T.nphase;
+    a.ksplit = 1;
+    for (int p = 0; p < T.nphase; ++p) a.ph[p] = T.ph[p];
+    return a;
+}
+
+ConvArgs dgrad_args(avse_trainer* t, const TLayer& T, const float* dz, int64_t N) {
+    const LayerDef& L = T.L;
+    ConvArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.in = dz;
+    a.out = T.gin;
+    a.w = t->wdg + T.dg_off;
+    a.scale = t->ones;
+    a.shift = t->zeros;
+    a.taps = T.d_dg_taps;
+    a.N = (int)N;
+    a.Hi = T.hq;
+    a.Wi = T.wq;
+    a.Ci = T.dg_ci;
+    a.in_clip_stride = (long long)T.hq * T.wq * T.zc;
+    a.Hq = (L.kind == DENSE) ? 1 : T.dg_hq;
+    a.Wq = (L.kind == DENSE) ? 1 : T.dg_wq;
+    a.sy = T.dg_sy;
+    a.sx = T.dg_sx;
+    a.oys = T.dg_oys;
+    a.oxs = T.dg_oxs;
+    a.Ho = L.hin;
+    a.Wo = L.win;
+    a.Co = L.cin;
+    a.out_clip_stride = T.in_clip;
+    a.out_pix_stride = T.cin_pad;
+    a.out_c_off = 0;
+    a.pool = 0;
+    a.act = 0;
+    a.nphase = T.dg_nphase;
+    a.ksplit = 1;
+    for (int p = 0; p < T.dg_nphase; ++p) a.ph[p] = T.dg_ph[p];
+    return a;
+}
+
+// column reduction + finish; returns status
+template <int MODE, int STAGE>
+int colred(avse_trainer* t, const float* x, int ld, const float* z, const float* mean, const float* inv, long long M, int C,
+           float* fmean, float* finv, float* mm, float* mv, float* o0, float* o1, hipStream_t s) {
+    long long rpb = 4096;
+    long long nblk = (M + rpb - 1) / rpb;
+    if (nblk < 1) nblk = 1;
+    if ((MODE == 2 ? 2 : 1) * nblk * (long long)C > t->red_floats) return tfail(AVSE_ERR_INVALID, "reduction workspace too small");
+    hipLaunchKernelGGL(k_colreduce<MODE>, dim3((C + 63) / 64, (unsigned)nblk), dim3(256), 0, s, x, ld, z, mean, inv, M, C, rpb, t->red);
+    AVSE_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(k_colfinish<STAGE>, dim3((C + 255) / 256), dim3(256), 0, s, t->red, (int)nblk, C, M, fmean, finv, mm, mv, o0, o1);
+    AVSE_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int wgrad(avse_trainer* t, const TLayer& T, const float* dz, int64_t N, hipStream_t s) {
+    const LayerDef& L = T.L;
+    WgArgs w;
+    std::memset(&w, 0, sizeof(w));
+    w.N = (int)N;
+    w.ntaps = L.kh * L.kw;
+    w.taps = T.d_wg_taps;
+    if (L.kind == DECONV) {   // G = dz on the output grid (stride s), H = input
+        w.G = dz; w.Hg = T.hq; w.Wg = T.wq; w.gcs = T.zc; w.g_clip = (long long)T.hq * T.wq * T.zc;
+        w.H = T.in; w.Hh = L.hin; w.Wh = L.win; w.hcs = T.cin_pad; w.h_clip = T.in_clip;
+        w.sy = L.sh; w.sx = L.sw;
+        w.A = L.cout; w.B = L.cin;
+    } else {                  // G = input (stride s), H = dz on the conv grid
+        w.G = T.in; w.Hg = L.hin; w.Wg = L.win; w.gcs = T.cin_pad; w.g_clip = T.in_clip;
+        w.H = dz; w.Hh = T.hq; w.Wh = T.wq; w.hcs = T.zc; w.h_clip = (long long)T.hq * T.wq * T.zc;
+        w.sy = (L.kind == CONV) ? L.sh : 1; w.sx = (L.kind == CONV) ? L.sw : 1;
+        w.A = L.cin; w.B = L.cout;
+    }
+    const long long R = N * (long long)w.Hh * w.Wh;
+    const long long tiles = (long long)((w.A + 63) / 64) * ((w.B + 63) / 64) * w.ntaps;
+    long long splits = wg_splits(T, N);
+    const long long per = (long long)w.ntaps * w.A * w.B;
+    if (splits * per > t->wpart_floats) return tfail(AVSE_ERR_INVALID, "wgrad workspace too small");
+    w.rows_per_split = ((R + splits - 1) / splits + 15) / 16 * 16;
+    splits = (R + w.rows_per_split - 1) / w.rows_per_split;
+    w.part = t->wpart;
+    hipLaunchKernelGGL(k_wgrad, dim3((unsigned)(tiles / w.ntaps), (unsigned)w.ntaps, (unsigned)splits), dim3(256), 0, s, w);
+    AVSE_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(k_sum_splits, dim3(grid_for(per)), dim3(256), 0, s, (const float*)t->wpart, (int)splits, per, t->Gr + T.o_k);
+    AVSE_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int step_impl(avse_trainer* t, const float* audio, const float* video, const float* target, const float* vmean,
+              const float* vstd, int64_t N, float lr, float drop, uint32_t seed, int flags, float* loss, hipStream_t s) {
+    // ---- weight packings from the current parameters ----
+    hipLaunchKernelGGL(k_gather, dim3(grid_for(t->n_fwd)), dim3(256), 0, s, t->wfwd, (const int*)t->map_fwd, (const float*)t->P, t->n_fwd);
+    hipLaunchKernelGGL(k_gather, dim3(grid_for(t->n_dg)), dim3(256), 0, s, t->wdg, (const int*)t->map_dg, (const float*)t->P, t->n_dg);
+    AVSE_HIP_CHECK(hipGetLastError());
+    AVSE_HIP_CHECK(hipMemsetAsync(t->Gr, 0, sizeof(float) * t->nparams, s));
+    // ---- inputs ----
+    hipLaunchKernelGGL(k_prep_audio, dim3(grid_for(N * 1600)), dim3(256), 0, s, audio, t->in_audio, (long long)N * 1600);
+    hipLaunchKernelGGL(k_prep_video, dim3(grid_for(N * 16384)), dim3(256), 0, s, video, vmean, vstd, t->in_video,
+                       (long long)N * 16384, 16384);
+    AVSE_HIP_CHECK(hipGetLastError());
+    // ---- forward ----
+    for (int i = 0; i < kNumLayers; ++i) {
+        TLayer& T = t->layers[i];
+        const LayerDef& L = T.L;
+        ConvArgs a = fwd_args(t, T, N);
+        if (int rc = launch_conv(a, AVSE_F32, s)) return rc;
+        if (!L.bn) continue;
+        const int C = L.bn_channels;
+        const long long M = N * (long long)T.hq * T.wq * (L.cout / C);
+        float* P = t->P;
+        if (int rc = colred<0, 0>(t, T.z, C, nullptr, nullptr, nullptr, M, C, T.mean, nullptr, nullptr, nullptr, nullptr, nullptr, s)) return rc;
+        if (int rc = colred<1, 1>(t, T.z, C, nullptr, T.mean, nullptr, M, C, T.mean, T.inv, P + T.o_mm, P + T.o_mv, nullptr, nullptr, s)) return rc;
+        ActArgs aa;
+        std::memset(&aa, 0, sizeof(aa));
+        aa.z = T.z; aa.N = (int)N; aa.C = C;
+        aa.Hq = (L.kind == DENSE) ? ((std::strcmp(L.name, "dec_dense2") == 0) ? 5 : 1) : T.hq;
+        aa.Wq = (L.kind == DENSE) ? ((std::strcmp(L.name, "dec_dense2") == 0) ? 5 : 1) : T.wq;
+        aa.mean = T.mean; aa.inv = T.inv; aa.gamma = P + T.o_g; aa.beta = P + T.o_be;
+        aa.pool = L.pool ? 1 : 0;
+        aa.drop = L.pool ? drop : 0.f;   // Dropout(0.25) follows each video pooling (network.py:142-174)
+        aa.seed = seed; aa.layer = (uint32_t)i;
+        float* gdummy;
+        out_view(t, i, &aa.out, &gdummy, &aa.out_clip, &aa.out_pix, &aa.out_c);
+        const long long total = N * (long long)aa.Hq * aa.Wq * C / (aa.pool ? 4 : 1);
+        hipLaunchKernelGGL(k_act_fwd, dim3(grid_for(total)), dim3(256), 0, s, aa);
+        AVSE_HIP_CHECK(hipGetLastError());
+    }
+    // ---- loss ----
+    TLayer& D6 = t->layers[kNumLayers - 1];
+    const long long nout = N * 80 * 20;
+    const unsigned lb = grid_for(nout, 256, 1024);
+    hipLaunchKernelGGL(k_mse, dim3(lb), dim3(256), 0, s, (const float*)D6.z, target, nout, D6.zc, t->g6, t->red);
+    hipLaunchKernelGGL(k_mse_finish, dim3(1), dim3(64), 0, s, (const float*)t->red, (int)lb, nout, t->loss);
+    AVSE_HIP_CHECK(hipGetLastError());
+    if (loss) AVSE_HIP_CHECK(hipMemcpyAsync(loss, t->loss, sizeof(float), hipMemcpyDeviceToDevice, s));
+    // ---- backward ----
+    for (int i = kNumLayers - 1; i >= 0; --i) {
+        TLayer& T = t->layers[i];
+        const LayerDef& L = T.L;
+        float* dz;
+        const long long Mfull = N * (long long)T.hq * T.wq;
+        if (!L.bn) {
+            dz = t->g6;   // dL/dy with the output's 8-channel stride
+        } else {
+            const int C = L.bn_channels;
+            const long long M = Mfull * (L.cout / C);
+            ActArgs aa;
+            std::memset(&aa, 0, sizeof(aa));
+            aa.z = T.z; aa.N = (int)N; aa.C = C;
+            aa.Hq = (L.kind == DENSE) ? ((std::strcmp(L.name, "dec_dense2") == 0) ? 5 : 1) : T.hq;
+            aa.Wq = (L.kind == DENSE) ? ((std::strcmp(L.name, "dec_dense2") == 0) ? 5 : 1) : T.wq;
+            aa.mean = T.mean; aa.inv = T.inv; aa.gamma = t->P + T.o_g; aa.beta = t->P + T.o_be;
+            aa.pool = L.pool ? 1 : 0;
+            aa.drop = L.pool ? drop : 0.f;
+            aa.seed = seed; aa.layer = (uint32_t)i;
+            float *obuf, *gbuf;
+            long long gclip;
+            int gpix, gc;
+            out_view(t, i, &obuf, &gbuf, &gclip, &gpix, &gc);
+            const long long total = N * (long long)aa.Hq * aa.Wq * C / (aa.pool ? 4 : 1);
+            hipLaunchKernelGGL(k_act_bwd, dim3(grid_for(total)), dim3(256), 0, s, aa, (const float*)gbuf, gclip, gpix, gc, t->ghat);
+            AVSE_HIP_CHECK(hipGetLastError());
+            if (int rc = colred<2, 2>(t, t->ghat, C, T.z, T.mean, T.inv, M, C, nullptr, nullptr, nullptr, nullptr,
+                                      t->Gr + T.o_be, t->Gr + T.o_g, s)) return rc;
+            hipLaunchKernelGGL(k_bn_bwd, dim3(grid_for(M * C)), dim3(256), 0, s, (const float*)T.z, t->ghat, M, C,
+                               (const float*)T.mean, (const float*)T.inv, (const float*)(t->P + T.o_g),
+                               (const float*)(t->Gr + T.o_be), (const float*)(t->Gr + T.o_g));
+            AVSE_HIP_CHECK(hipGetLastError());
+            dz = t->ghat;
+            if ((flags & AVSE_TRAIN_DEBUG_STOP) && (flags >> 8) == i) return 0;   // debug: dz of layer i in ghat
+        }
+        // bias: sum of dz over every pixel (per output channel)
+        if (int rc = colred<0, 3>(t, dz, T.zc, nullptr, nullptr, nullptr, Mfull, L.cout, nullptr, nullptr, nullptr, nullptr,
+                                  t->Gr + T.o_b, nullptr, s)) return rc;
+        if (int rc = wgrad(t, T, dz, N, s)) return rc;
+        if (T.dgrad) {
+            ConvArgs a = dgrad_args(t, T, dz, N);
+            if (int rc = launch_conv(a, AVSE_F32, s)) return rc;
+            if ((flags & AVSE_TRAIN_DEBUG_GIN) && (flags >> 8) == i) {   // debug: dL/d(input) of layer i in the scratch
+                AVSE_HIP_CHECK(hipMemcpyAsync(t->ghat, T.gin, sizeof(float) * N * T.in_clip, hipMemcpyDeviceToDevice, s));
+                return 0;
+            }
+        }
+    }
+    if (flags & 1) return 0;   // gradients only
+    // ---- Adam ----
+    t->step += 1;
+    const double b1 = 0.9, b2 = 0.999;
+    const double lr_t = (double)lr * std::sqrt(1.0 - std::pow(b2, (double)t->step)) / (1.0 - std::pow(b1, (double)t->step));
+    hipLaunchKernelGGL(k_adam, dim3(grid_for(t->nparams)), dim3(256), 0, s, t->P, (const float*)t->Gr, t->Mo, t->Vo,
+                       (long long)t->nparams, (float)lr_t, (float)b1, (float)b2, 1e-8f);
+    AVSE_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int avse_trainer_create(avse_ctx* c, const float* host_blob, int64_t n_floats, int64_t max_batch, avse_trainer** out) {
+    if (!c || !host_blob || !out) return tfail(AVSE_ERR_INVALID, "NULL argument");
+    if (n_floats != blob_floats()) return tfail(AVSE_ERR_INVALID, "weight blob has the wrong size");
+    if (max_batch < 1 || max_batch > 4096) return tfail(AVSE_ERR_INVALID, "max_batch must be in [1, 4096]");
+    auto* t = new avse_trainer();
+    t->device = ctx_device_index(c);
+    t->max_n = max_batch;
+    int rc = hipSetDevice(t->device) == hipSuccess ? 0 : tfail(AVSE_ERR_HIP, "hipSetDevice failed");
+    if (!rc) rc = build_plan(t, host_blob);
+    if (!rc) rc = alloc_tensors(t);
+    if (rc) {
+        avse_trainer_destroy(t);
+        return rc;
+    }
+    *out = t;
+    return 0;
+}
+
+void avse_trainer_destroy(avse_trainer* t) {
+    if (!t) return;
+    (void)hipSetDevice(t->device);
+    for (void* p : t->allocs) (void)hipFree(p);
+    delete t;
+}
+
+int avse_trainer_step(avse_trainer* t, const float* audio, const float* video, const float* target, const float* vnorm_mean,
+                      const float* vnorm_std, int64_t N, float lr, float dropout_rate, uint32_t dropout_seed, int flags,
+                      float* loss, void* stream) {
+    if (!t || !audio || !video || !target) return tfail(AVSE_ERR_INVALID, "NULL argument");
+    if (N < 1 || N > t->max_n) return tfail(AVSE_ERR_INVALID, "batch size outside [1, max_batch]");
+    if ((vnorm_mean == nullptr) != (vnorm_std == nullptr)) return tfail(AVSE_ERR_INVALID, "vnorm_mean / vnorm_std: both or neither");
+    if (!(dropout_rate >= 0.f && dropout_rate < 1.f)) return tfail(AVSE_ERR_INVALID, "dropout_rate must be in [0, 1)");
+    AVSE_HIP_CHECK(hipSetDevice(t->device));
+    return step_impl(t, audio, video, target, vnorm_mean, vnorm_std, N, lr, dropout_rate, dropout_seed, flags, loss,
+                     (hipStream_t)stream);
+}
+
+int avse_trainer_read(avse_trainer* t, int what, float* host_blob, int64_t n_floats) {
+    if (!t || !host_blob) return tfail(AVSE_ERR_INVALID, "NULL argument");
+    if (n_floats != t->nparams && !(what == AVSE_TRAIN_DEBUG_DZ && n_floats <= t->nparams))
+        return tfail(AVSE_ERR_INVALID, "blob size mismatch");
+    const float* src = what == AVSE_TRAIN_PARAMS ? t->P : what == AVSE_TRAIN_GRADS ? t->Gr : what == AVSE_TRAIN_ADAM_M ? t->Mo
+                       : what == AVSE_TRAIN_ADAM_V ? t->Vo : nullptr;
+    if (what == AVSE_TRAIN_DEBUG_DZ) {   // debug: the head of the dz scratch (see AVSE_TRAIN_DEBUG_STOP)
+        AVSE_HIP_CHECK(hipSetDevice(t->device));
+        AVSE_HIP_CHECK(hipDeviceSynchronize());
+        AVSE_HIP_CHECK(hipMemcpy(host_blob, t->ghat, sizeof(float) * n_floats, hipMemcpyDeviceToHost));
+        return 0;
+    }
+    if (!src) return tfail(AVSE_ERR_INVALID, "unknown trainer buffer");
+    AVSE_HIP_CHECK(hipSetDevice(t->device));
+    AVSE_HIP_CHECK(hipDeviceSynchronize());
+    AVSE_HIP_CHECK(hipMemcpy(host_blob, src, sizeof(float) * n_floats, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int avse_trainer_iterations(avse_trainer* t, int64_t* iterations) {
+    if (!t || !iterations) return tfail(AVSE_ERR_INVALID, "NULL argument");
+    *iterations = t->step;
+    return 0;
+}
+
+}  // extern "C"

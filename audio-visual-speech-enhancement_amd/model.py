@@ -127,6 +127,19 @@ class KerasModel:
     def to_blob(self):
         return np.concatenate([self.tensors[n].ravel() for n, _ in tensor_names()]).astype(np.float32)
 
+    @classmethod
+    def from_blob(cls, blob):
+        """Inverse of to_blob (the canonical layout of include/avse.h avse_weights_load)."""
+        blob = np.asarray(blob, dtype=np.float32).ravel()
+        t, off = OrderedDict(), 0
+        for n, shape in tensor_names():
+            k = int(np.prod(shape))
+            t[n] = blob[off:off + k].reshape(shape).copy()
+            off += k
+        if off != blob.size:
+            raise ValueError(f"blob has {blob.size} floats, the network {off}")
+        return cls(t)
+
     def layer_dict(self):
         """{'a_conv1': {'kernel', 'bias'}, 'a_conv1_bn': {'gamma', ...}, ...}"""
         d = {}

@@ -3,7 +3,7 @@
 build / predict / evaluate / load / save keep the reference's signatures and tensor shapes
 (`predict` takes [N, 80, 20] + [N, 128, 128, 5] and returns np.squeeze of [N, 80, 20, 1]).
 The forward pass is libavse's avse_forward (HIP kernels); there is no Keras and no CPU fallback.
-Training (network.py:177-206) is out of scope for this build.
+train (network.py:177-206) runs Keras-semantics fit steps on libavse's training step (fit.py, csrc/train.hip).
 """
 import numpy as np
 import torch
@@ -38,8 +38,22 @@ class SpeechEnhancementNetwork(object):
                 f"(16 kHz / 25 fps, 200-ms slices); got {tuple(audio_spectrogram_shape)}, {tuple(video_shape)}")
         return SpeechEnhancementNetwork(KerasModel.init(seed=seed), compute_dtype)
 
-    def train(self, *args, **kwargs):
-        raise NotImplementedError("training (network.py:177-206) is outside this build's hot path")
+    def train(self, train_mixed_spectrograms, train_video_samples, train_speech_spectrograms,
+              validation_mixed_spectrograms, validation_video_samples, validation_speech_spectrograms,
+              model_cache_path, tensorboard_dir=None, batch_size=16, epochs=1000, lr=5e-4, seed=0, verbose=1):
+        """network.py:177-206: Model.fit(batch_size=16, epochs=1000) with ModelCheckpoint(model_cache_path),
+        ReduceLROnPlateau(val_loss, 0.5, patience 5), EarlyStopping(val_loss, min_delta 0.01, patience 10) on the
+        Adam(5e-4) / MSE compilation of network.py:35-36.  Video samples are expected normalised (as the
+        reference's speech_enhancer.train does in place).  tensorboard_dir is accepted and unused (no
+        TensorFlow).  The trained parameters replace this network's; returns the per-epoch history."""
+        from .fit import fit
+        model, history = fit(self.__model, (train_mixed_spectrograms, train_video_samples, train_speech_spectrograms),
+                             (validation_mixed_spectrograms, validation_video_samples, validation_speech_spectrograms),
+                             model_cache_path=model_cache_path, batch_size=batch_size, epochs=epochs, lr=lr, seed=seed,
+                             device=self.__device, verbose=verbose)
+        self.__model = model
+        self.__dw = None
+        return history
 
     def predict_device(self, mixed_spectrograms, video_samples, video_normalizer=None):
         """Device-tensor forward: [N, 80, 20] x [N, 128, 128, 5] -> [N, 80, 20] (no squeeze)."""

@@ -210,3 +210,72 @@ def to_device(x, device=None):
     if isinstance(x, torch.Tensor):
         return x.to(device=dev, dtype=torch.float32).contiguous()
     return torch.from_numpy(np.ascontiguousarray(x, dtype=np.float32)).to(dev)
+
+
+class Trainer:
+    """libavse training step (avse_trainer_*, train.hip): one Keras fit step of SpeechEnhancementNetwork.train
+    (network.py:177-206) — BatchNormalization on batch statistics, Dropout after each video pooling, MSE, Adam.
+    Parameters / gradients / Adam moments stay on the device in the canonical blob layout."""
+
+    def __init__(self, model, max_batch=16, device=None):
+        if not isinstance(model, KerasModel):
+            raise TypeError("model must be a KerasModel")
+        self.ctx = _lib.context(device)
+        self.max_batch = int(max_batch)
+        blob = model.to_blob()
+        self.handle = ctypes.c_void_p()
+        with torch.cuda.device(self.ctx.device_index):
+            _lib.check(_lib.load().avse_trainer_create(self.ctx.handle, blob.ctypes.data_as(ctypes.c_void_p), blob.size,
+                                                       self.max_batch, ctypes.byref(self.handle)), "avse_trainer_create")
+        self._loss = torch.zeros((), dtype=torch.float32, device=torch.device("cuda", self.ctx.device_index))
+
+    def step(self, audio, video, target, vnorm_mean=None, vnorm_std=None, lr=5e-4, dropout=0.25, seed=0,
+             grads_only=False):
+        """One fit step on a batch: audio / target [N, 80, 20], video [N, 128, 128, 5] (raw crops when vnorm_* are
+        given) float32 device tensors.  Returns the batch MSE before the update as a 0-dim device tensor."""
+        _dev_f32(audio, "audio", (80, 20))
+        _dev_f32(target, "target", (80, 20))
+        _dev_f32(video, "video", (128, 128, 5))
+        N = audio.shape[0]
+        if video.shape[0] != N or target.shape[0] != N:
+            raise ValueError("audio, video and target batch sizes differ")
+        if N > self.max_batch:
+            raise ValueError(f"batch of {N} exceeds the trainer's max_batch {self.max_batch}")
+        if (vnorm_mean is None) != (vnorm_std is None):
+            raise ValueError("vnorm_mean and vnorm_std must both be given")
+        devs = {self.ctx.device_index, audio.device.index, video.device.index, target.device.index}
+        if len(devs) != 1:
+            raise ValueError("trainer and batch tensors must share one device")
+        with torch.cuda.device(audio.device):
+            _lib.check(_lib.load().avse_trainer_step(
+                self.handle, _lib.ptr(audio), _lib.ptr(video), _lib.ptr(target), _lib.ptr(vnorm_mean),
+                _lib.ptr(vnorm_std), N, float(lr), float(dropout), int(seed) & 0xFFFFFFFF,
+                _lib.AVSE_TRAIN_GRADS_ONLY if grads_only else 0, _lib.ptr(self._loss),
+                _lib.stream_handle(audio.device)), "avse_trainer_step")
+        return self._loss.clone()
+
+    def _read(self, what):
+        out = np.empty(blob_floats(), dtype=np.float32)
+        _lib.check(_lib.load().avse_trainer_read(self.handle, what, out.ctypes.data_as(ctypes.c_void_p), out.size),
+                   "avse_trainer_read")
+        return out
+
+    def model(self):
+        """Current parameters (incl. BN moving statistics) as a KerasModel."""
+        return KerasModel.from_blob(self._read(_lib.AVSE_TRAIN_PARAMS))
+
+    def gradients(self):
+        """Gradients of the last step, {tensor name: array} (moving statistics: zero)."""
+        return KerasModel.from_blob(self._read(_lib.AVSE_TRAIN_GRADS)).tensors
+
+    @property
+    def iterations(self):
+        v = ctypes.c_int64()
+        _lib.check(_lib.load().avse_trainer_iterations(self.handle, ctypes.byref(v)), "avse_trainer_iterations")
+        return v.value
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value and _lib._lib is not None:
+            _lib._lib.avse_trainer_destroy(h)
+            self.handle = None

@@ -9,9 +9,8 @@ Differences (host plumbing outside the hot path):
   * video: the reference decodes with ffmpeg and crops the mouth with dlib (data_processor.py:12-32);
     this build reads pre-cropped mouth stacks <name>.npy [frames, 128, 128] (25 fps unless a
     <name>.fps text file says otherwise);
-  * train: fitting (network.py:177-206) is out of scope; `--init-only` writes the files the reference's
-    train produces (model.h5py from a Keras-default initialisation, normalization.pkl fitted on the
-    training video) so that predict runs end to end;
+  * train: Keras-semantics fit on libavse's training step (network.train, fit.py); `--epochs` (default 1000
+    like the reference) bounds it, `--init-only` writes only the initialised model + normaliser;
   * the enhanced/mixture .mp4 muxing (mediaio.ffmpeg.merge) runs only when ffmpeg is installed;
   * caches hold no pickles: preprocessed samples are <name>.npz (arrays + a JSON metadata string, read with
     allow_pickle=False), the normaliser normalization.npz, the model model.safetensors (a Keras model.h5py
@@ -160,15 +159,21 @@ def preprocess(args):
 
 
 def train(args):
-    if not args.init_only:
-        raise NotImplementedError("training (network.py:177-206) is outside this build's hot path; "
-                                  "use --init-only to write an initialised model + normalizer")
+    """speech_enhancer.py:31-58: sample sets, VideoNormalizer fitted on the training video and applied in place to
+    both sets, the normaliser saved, network built, fit with the model checkpointed every epoch, saved."""
     layout = Layout(args.base_dir)
     samples = load_preprocessed_blobs([layout.preprocessed(d) for d in args.train_data_names])
-    video, mixed, _ = make_sample_set(samples)
+    video, mixed, speech = make_sample_set(samples)
     normalizer = data_processor.VideoNormalizer(video)
     normalizer.save(layout.normalizer_file(args.model))
     network = SpeechEnhancementNetwork.build(mixed.shape[1:], video.shape[1:], seed=args.seed)
+    if not args.init_only:
+        vsamples = load_preprocessed_blobs([layout.preprocessed(d) for d in args.validation_data_names])
+        vvideo, vmixed, vspeech = make_sample_set(vsamples)
+        normalizer.normalize(video)
+        normalizer.normalize(vvideo)
+        network.train(mixed, video, speech, vmixed, vvideo, vspeech, layout.model_file(args.model),
+                      epochs=args.epochs, seed=args.seed)
     network.save(layout.model_file(args.model))
 
 
@@ -214,6 +219,7 @@ def main(argv=None):
     t.add_argument("-vdn", "--validation_data_names", nargs="+", type=str, required=True)
     t.add_argument("-g", "--gpus", type=int, default=1)
     t.add_argument("--init-only", action="store_true")
+    t.add_argument("--epochs", type=int, default=1000)
     t.add_argument("--seed", type=int, default=0)
     t.set_defaults(func=train)
 

@@ -170,6 +170,40 @@ int avse_video_normalize(avse_ctx* ctx, float* video, int64_t S, int H, int W, i
 int avse_mse(avse_ctx* ctx, const float* pred, const float* target, int64_t n, float* loss,
              void* stream);
 
+/* ---- training (SpeechEnhancementNetwork.train, network.py:177-206) ---------------------- */
+
+/* One Keras fit step of the model compiled at network.py:35-36 (Adam(lr) on mean_squared_error), in float32:
+ * BatchNormalization on batch statistics (biased variance, eps 1e-3) with moving-average updates (momentum 0.99),
+ * LeakyReLU(0.3), MaxPooling2D(2, 2), Dropout(dropout_rate) after each video pooling (the reference uses 0.25),
+ * MSE over every element, Keras-2.0 Adam (beta1 0.9, beta2 0.999, epsilon 1e-8, bias-corrected step size).
+ * Parameters, gradients and Adam moments are kept in the canonical blob layout of avse_weights_load. */
+typedef struct avse_trainer avse_trainer;
+enum avse_train_buffer { AVSE_TRAIN_PARAMS = 0, AVSE_TRAIN_GRADS = 1, AVSE_TRAIN_ADAM_M = 2, AVSE_TRAIN_ADAM_V = 3,
+                         AVSE_TRAIN_DEBUG_DZ = 4 /* test aid: the first n_floats of the dz scratch */ };
+/* AVSE_TRAIN_DEBUG_STOP | (layer << 8): test aid, end the backward pass right after layer's BN backward (its
+ * dL/dz is then readable with AVSE_TRAIN_DEBUG_DZ; gradients of earlier layers are not computed) */
+/* AVSE_TRAIN_DEBUG_GIN | (layer << 8): test aid, end the backward pass after layer's input gradient, copied to the
+ * dz scratch */
+enum avse_train_flags { AVSE_TRAIN_GRADS_ONLY = 1, AVSE_TRAIN_DEBUG_STOP = 2, AVSE_TRAIN_DEBUG_GIN = 4 };
+
+/* host_blob: initial parameters (avse_weights_load layout); max_batch: largest N passed to avse_trainer_step. */
+int avse_trainer_create(avse_ctx* ctx, const float* host_blob, int64_t n_floats, int64_t max_batch,
+                        avse_trainer** out);
+void avse_trainer_destroy(avse_trainer* t);
+
+/* audio [N][80][20] mixed mel-dB, video [N][128][128][5] raw mouth crops (normalised in-kernel when vnorm_* are
+ * given), target [N][80][20] speech mel-dB.  loss: nullable device float (the batch MSE before the update).
+ * flags AVSE_TRAIN_GRADS_ONLY: forward (moving statistics updated) + backward, no Adam update.
+ * The dropout mask of element e of video layer l is hash(dropout_seed, l, e) >= dropout_rate (train.hip). */
+int avse_trainer_step(avse_trainer* t, const float* audio, const float* video, const float* target,
+                      const float* vnorm_mean, const float* vnorm_std, int64_t N, float lr, float dropout_rate,
+                      uint32_t dropout_seed, int flags, float* loss, void* stream);
+
+/* Copy one of the trainer's blobs (avse_train_buffer) to the host; synchronises the device. */
+int avse_trainer_read(avse_trainer* t, int what, float* host_blob, int64_t n_floats);
+/* Adam iterations applied so far (Keras `optimizer.iterations`). */
+int avse_trainer_iterations(avse_trainer* t, int64_t* iterations);
+
 /* ---- diagnostics ----------------------------------------------------------------------- */
 
 /* Number of forward scratch buffers reported by avse_debug_scratch. */

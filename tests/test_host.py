@@ -154,3 +154,15 @@ def test_preprocessed_blob_and_normalizer_round_trip(tmp_path):
     norm.save(q)
     back = data_processor.VideoNormalizer.load(q)
     assert np.array_equal(back.mean_image, norm.mean_image) and np.array_equal(back.std_image, norm.std_image)
+
+
+def test_non_25_fps_network_shape_is_refused():
+    """At 29.97 fps the reference slices [80, 24] spectrograms (data_processor.py:44-49) and Keras would build a
+    different network (Dense widths follow the audio embedding: 5888 -> 1472, network.py:53-54).  The kernels and
+    the weight blob are specialised for the 25-fps graph, so build() refuses other shapes up front (the STFT /
+    ISTFT themselves do run at 29.97 fps: tests/test_gpu_stft.py, tests/test_gpu_istft.py)."""
+    from avse_amd.network import SpeechEnhancementNetwork
+    with pytest.raises(NotImplementedError, match=r"\(80, 20\)"):
+        SpeechEnhancementNetwork.build((80, 24), (128, 128, 5))
+    with pytest.raises(NotImplementedError):
+        SpeechEnhancementNetwork.build((80, 20), (64, 64, 5))

@@ -85,3 +85,31 @@ def test_keras_h5_shape_mismatch_is_an_error(tmp_path):
     r = _run("keras_h5_to_avse.py", str(h5), str(st))
     assert r.returncode != 0 and "v_conv3" in r.stderr
     assert not st.exists()
+
+
+@needs_h5py
+@pytest.mark.gpu
+def test_converted_keras_h5_runs_forward_against_oracle(tmp_path, gpu):
+    """SpeechEnhancementNetwork.load of a Keras model file (network.py:222-226), end to end: a Keras-2-layout
+    HDF5 file -> tools/keras_h5_to_avse.py -> KerasModel.load -> libavse fp32 forward, against the float64
+    oracle run on the ORIGINAL tensors (so a mis-mapped layer shows up as a forward error, not only as a
+    tensor mismatch)."""
+    import torch
+    from avse_amd import ops
+    from avse_amd.model import KerasModel
+    from oracle import keras_ref as K
+    m = KerasModel.init(seed=5, randomize=True)
+    npz, h5, st = tmp_path / "w.npz", tmp_path / "model.h5py", tmp_path / "model.safetensors"
+    _write_npz(m, npz)
+    assert _run("make_keras_h5.py", str(npz), str(h5), "--offset", "4").returncode == 0
+    r = _run("keras_h5_to_avse.py", str(h5), str(st))
+    assert r.returncode == 0, r.stderr
+    loaded = KerasModel.load(str(st))
+    rng = np.random.default_rng(50)
+    mel = rng.normal(-40, 12, (3, 80, 20)).astype(np.float32)
+    video = rng.integers(0, 256, (3, 128, 128, 5)).astype(np.float32)
+    ref = K.forward(m.layer_dict(), mel, video)
+    dw = ops.DeviceWeights(loaded, "float32")
+    got = ops.forward(dw, torch.from_numpy(mel).to(gpu), torch.from_numpy(video).to(gpu)).cpu().numpy()
+    err = float(np.sqrt(np.mean((got.astype(np.float64) - ref) ** 2)))
+    assert err <= 1e-4 * max(1.0, float(np.sqrt(np.mean(ref ** 2)))), err
