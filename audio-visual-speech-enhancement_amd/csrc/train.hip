@@ -124,22 +124,36 @@ __global__ __launch_bounds__(256) void k_colreduce(const float* __restrict__ x, 
     }
 }
 
-// Finish a column reduction in double, in block order (deterministic):
+// Finish a column reduction in double: one 256-thread block per column, each thread summing a strided subset of the
+// row-block partials, then a fixed LDS tree (deterministic):
 //   STAGE 0: mean[c] = S / M
 //   STAGE 1: var = S / M (biased), inv = 1 / sqrt(var + eps), moving stats <- m * 0.99 + batch * 0.01
 //   STAGE 2: dbeta = S0, dgamma = S1 (into the gradient blob)
 //   STAGE 3: out[c] = S (bias gradient)
 template <int STAGE>
-__global__ void k_colfinish(const float* __restrict__ part, int nblk, int C, long long M, float* __restrict__ mean,
-                            float* __restrict__ inv, float* __restrict__ mm, float* __restrict__ mv,
-                            float* __restrict__ out0, float* __restrict__ out1) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
+__global__ __launch_bounds__(256) void k_colfinish(const float* __restrict__ part, int nblk, int C, long long M,
+                                                   float* __restrict__ mean, float* __restrict__ inv, float* __restrict__ mm,
+                                                   float* __restrict__ mv, float* __restrict__ out0, float* __restrict__ out1) {
+    __shared__ double rs[256], rt[256];
+    const int c = blockIdx.x, tid = threadIdx.x;
     double s = 0, t = 0;
-    for (int b = 0; b < nblk; ++b) {
+    for (int b = tid; b < nblk; b += 256) {
         s += part[(long long)b * C + c];
         if (STAGE == 2) t += part[(long long)(nblk + b) * C + c];
     }
+    rs[tid] = s;
+    rt[tid] = t;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (tid < o) {
+            rs[tid] += rs[tid + o];
+            if (STAGE == 2) rt[tid] += rt[tid + o];
+        }
+        __syncthreads();
+    }
+    if (tid != 0) return;
+    s = rs[0];
+    t = rt[0];
     if (STAGE == 0) mean[c] = (float)(s / (double)M);
     if (STAGE == 1) {
         const double var = s / (double)M;
@@ -353,6 +367,66 @@ __global__ __launch_bounds__(256) void k_wgrad(WgArgs w) {
             if (b < w.B) out[(long long)a * w.B + b] = acc[i][j];
         }
     }
+}
+
+// Narrow-A variant (A <= 8: v_conv1's 5 input frames, d_deconv6's single output channel): block tile 8 a x 128 b,
+// thread = 4 a x 1 b, 32-row chunks (the 64 x 64 tile computed 92 % padding for v_conv1: 1.9 ms of a 19.7-ms step).
+__global__ __launch_bounds__(256) void k_wgrad_na(WgArgs w) {
+    __shared__ float gs[32][8], hs[32][132];
+    const int tid = threadIdx.x, ta = tid >> 7, tb = tid & 127;
+    const int b0 = blockIdx.x * 128;
+    const int tap = blockIdx.y;
+    const int2 t = w.taps[tap];
+    const long long R = (long long)w.N * w.Hh * w.Wh;
+    const long long r0 = blockIdx.z * w.rows_per_split, r1 = min(R, r0 + w.rows_per_split);
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (long long rc = r0; rc < r1; rc += 32) {
+        float gv = 0.f;
+        {   // G: row tid / 8, channel tid % 8
+            const long long r = rc + (tid >> 3);
+            const int a = tid & 7;
+            if (r < r1 && a < w.A) {
+                const int x = (int)(r % w.Wh), y = (int)((r / w.Wh) % w.Hh), n = (int)(r / ((long long)w.Wh * w.Hh));
+                const int gy = y * w.sy + t.x, gx = x * w.sx + t.y;
+                if (gy >= 0 && gy < w.Hg && gx >= 0 && gx < w.Wg) gv = w.G[n * w.g_clip + (long long)(gy * w.Wg + gx) * w.gcs + a];
+            }
+        }
+        float hv[16];
+        {   // H: row (tid / 128) + 2 q, channel b0 + tid % 128; (n, y, x) advanced by 2 rows per q (no divisions)
+            const long long r = rc + (tid >> 7);
+            int x = (int)(r % w.Wh), y = (int)((r / w.Wh) % w.Hh), n = (int)(r / ((long long)w.Wh * w.Hh));
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                hv[q] = 0.f;
+                if (rc + (tid >> 7) + 2 * q < r1 && b0 + tb < w.B)
+                    hv[q] = w.H[n * w.h_clip + (long long)(y * w.Wh + x) * w.hcs + b0 + tb];
+                x += 2;
+                while (x >= w.Wh) {
+                    x -= w.Wh;
+                    if (++y == w.Hh) { y = 0; ++n; }
+                }
+            }
+        }
+        __syncthreads();
+        gs[tid >> 3][tid & 7] = gv;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) hs[(tid >> 7) + 2 * q][tb] = hv[q];
+        __syncthreads();
+#pragma unroll 8
+        for (int k = 0; k < 32; ++k) {
+            const float hb = hs[k][tb];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc[i] = fmaf(gs[k][ta * 4 + i], hb, acc[i]);
+        }
+    }
+    float* out = w.part + ((long long)blockIdx.z * w.ntaps + tap) * w.A * w.B;
+    const int b = b0 + tb;
+    if (b < w.B)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int a = ta * 4 + i;
+            if (a < w.A) out[(long long)a * w.B + b] = acc[i];
+        }
 }
 
 __global__ void k_sum_splits(const float* __restrict__ part, int splits, long long n, float* __restrict__ out) {
@@ -649,7 +723,7 @@ long long wg_splits(const TLayer& T, int64_t N) {
     const LayerDef& L = T.L;
     const int A = (L.kind == DECONV) ? L.cout : L.cin, B = (L.kind == DECONV) ? L.cin : L.cout;
     const long long R = N * (long long)((L.kind == DECONV) ? L.hin * L.win : T.hq * T.wq);
-    const long long tiles = (long long)((A + 63) / 64) * ((B + 63) / 64) * L.kh * L.kw;
+    const long long tiles = (A <= 8 ? (long long)((B + 127) / 128) : (long long)((A + 63) / 64) * ((B + 63) / 64)) * L.kh * L.kw;
     return std::max(1LL, std::min((2048 + tiles - 1) / tiles, (R + 255) / 256));
 }
 
@@ -689,7 +763,7 @@ int alloc_tensors(avse_trainer* t) {
         wmax = std::max(wmax, (long long)T.L.kh * T.L.kw * T.L.cin * T.L.cout * mx);
     }
     if (int rc = talloc(t, &t->ghat, zmax)) return rc;
-    t->red_floats = std::max(red, 1LL << 16);
+    t->red_floats = std::max(red, 2LL * (2048 + 64) * 64 + 4096);   // colred's nblk * C <= (2048 + 64) * 64 (x2 MODE 2)
     if (int rc = talloc(t, &t->red, t->red_floats)) return rc;
     t->wpart_floats = wmax;
     if (int rc = talloc(t, &t->wpart, wmax)) return rc;
@@ -807,13 +881,15 @@ ConvArgs dgrad_args(avse_trainer* t, const TLayer& T, const float* dz, int64_t N
 template <int MODE, int STAGE>
 int colred(avse_trainer* t, const float* x, int ld, const float* z, const float* mean, const float* inv, long long M, int C,
            float* fmean, float* finv, float* mm, float* mv, float* o0, float* o1, hipStream_t s) {
-    long long rpb = 4096;
-    long long nblk = (M + rpb - 1) / rpb;
-    if (nblk < 1) nblk = 1;
+    // ~2048 blocks of 64 columns x >= 64 rows: v_conv1's 262k-row reductions ran on 128 blocks (10 of 19.7 ms/step)
+    const long long cblk = (C + 63) / 64;
+    long long nblk = std::min(std::max(1LL, 2048 / cblk), std::max(1LL, (M + 63) / 64));
+    const long long rpb = (M + nblk - 1) / nblk;
+    nblk = (M + rpb - 1) / rpb;
     if ((MODE == 2 ? 2 : 1) * nblk * (long long)C > t->red_floats) return tfail(AVSE_ERR_INVALID, "reduction workspace too small");
     hipLaunchKernelGGL(k_colreduce<MODE>, dim3((C + 63) / 64, (unsigned)nblk), dim3(256), 0, s, x, ld, z, mean, inv, M, C, rpb, t->red);
     AVSE_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(k_colfinish<STAGE>, dim3((C + 255) / 256), dim3(256), 0, s, t->red, (int)nblk, C, M, fmean, finv, mm, mv, o0, o1);
+    hipLaunchKernelGGL(k_colfinish<STAGE>, dim3(C), dim3(256), 0, s, t->red, (int)nblk, C, M, fmean, finv, mm, mv, o0, o1);
     AVSE_HIP_CHECK(hipGetLastError());
     return 0;
 }
@@ -841,10 +917,13 @@ int wgrad(avse_trainer* t, const TLayer& T, const float* dz, int64_t N, hipStrea
     long long splits = wg_splits(T, N);
     const long long per = (long long)w.ntaps * w.A * w.B;
     if (splits * per > t->wpart_floats) return tfail(AVSE_ERR_INVALID, "wgrad workspace too small");
-    w.rows_per_split = ((R + splits - 1) / splits + 15) / 16 * 16;
+    w.rows_per_split = ((R + splits - 1) / splits + 31) / 32 * 32;
     splits = (R + w.rows_per_split - 1) / w.rows_per_split;
     w.part = t->wpart;
-    hipLaunchKernelGGL(k_wgrad, dim3((unsigned)(tiles / w.ntaps), (unsigned)w.ntaps, (unsigned)splits), dim3(256), 0, s, w);
+    if (w.A <= 8)
+        hipLaunchKernelGGL(k_wgrad_na, dim3((unsigned)((w.B + 127) / 128), (unsigned)w.ntaps, (unsigned)splits), dim3(256), 0, s, w);
+    else
+        hipLaunchKernelGGL(k_wgrad, dim3((unsigned)(tiles / w.ntaps), (unsigned)w.ntaps, (unsigned)splits), dim3(256), 0, s, w);
     AVSE_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(k_sum_splits, dim3(grid_for(per)), dim3(256), 0, s, (const float*)t->wpart, (int)splits, per, t->Gr + T.o_k);
     AVSE_HIP_CHECK(hipGetLastError());

@@ -149,6 +149,33 @@ def leg_audio_fp32(dev, model, reps=50, B=256):
             "stage_ms": {k: round(v, 4) for k, v in st.items() if v > 0.0005}, "reps": reps}
 
 
+def leg_train(dev, model, reps=20, B=16):
+    """one Keras fit step (network.py:177-206, batch 16 like the reference) on libavse's fp32 training
+    path: training-mode forward (batch-stat BN, dropout), backward (dgrad + wgrad), Adam.  Algorithmic work per clip
+    ~3 x the forward's 5.377 GFLOP (forward, input gradient, weight gradient), priced against the fp32 MFMA peak."""
+    rng = np.random.default_rng(16)
+    audio = torch.from_numpy(rng.normal(-40, 12, (B, 80, 20)).astype(np.float32)).to(dev)
+    video = torch.from_numpy(rng.normal(0, 1, (B, 128, 128, 5)).astype(np.float32)).to(dev)
+    target = audio + 1.0
+    tr = ops.Trainer(model, max_batch=B, device=dev)
+    for i in range(3):
+        tr.step(audio, video, target, seed=i)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for i in range(reps):
+        tr.step(audio, video, target, seed=100 + i)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    tf = 3 * FLOP_PER_CLIP * B / (ms * 1e-3) / 1e12
+    return {"config": "SURVEY §8(f)4: Keras fit step (Adam 5e-4, MSE, BN batch statistics, dropout 0.25), fp32, batch 16",
+            "ms_per_step": round(ms, 3), "clips_per_s": round(B / (ms * 1e-3), 1),
+            "roofline": {"bound": "mfma", "achieved": round(tf, 2), "peak": round(PEAK_TFLOPS["fp32"], 1),
+                         "unit": "TFLOP/s", "frac": round(tf / PEAK_TFLOPS["fp32"], 4),
+                         "flop_per_clip": 3 * FLOP_PER_CLIP}, "reps": reps}
+
+
 def cpu_baseline(audio, video, mean, std, model, gpu_out, budget_s=12.0, max_s=30.0):
     """The CPU oracle (numpy librosa restatement + torch-CPU fp32 Keras graph) on a bounded sample of the same
     inputs; also the parity of the timed GPU output against the float64 oracle pipeline on those clips."""
@@ -412,7 +439,8 @@ def main():
         },
     }
     if rank == 0 and world == 1 and not args.no_legs:
-        result["legs"] = {"stft_b4096": leg_stft(dev), "audio_fp32_b256": leg_audio_fp32(dev, model)}
+        result["legs"] = {"stft_b4096": leg_stft(dev), "audio_fp32_b256": leg_audio_fp32(dev, model),
+                          "train_fp32_b16": leg_train(dev, model)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         base, parity = cpu_baseline(audio_np, video_np, mean_np, std_np, model, timed_out)
         result["cpu_baseline"] = base
