@@ -12,7 +12,7 @@
 //   step 2: lane (f, k2 in [0,20)) does a 16-point DFT (4 x 4) over n1 -> Z[k2 + 20 k1]
 //   step 3: lane (f, k) untangles X[k], X[320-k] from Z[k], Z[320-k]  -> |X| in LDS
 //   step 4: lane (f, mel band) sparse Slaney dot (<= max_width bins) -> dB
-// A persistent 448-lane block walks chunks of up to 21 frames of one utterance, 3 frames per
+// A 448-lane block handles a chunk of up to 21 frames of one utterance, 3 frames per
 // wave (48 / 60 active lanes in steps 1 / 2).  When the chunk covers the whole utterance (the
 // 200-ms segment case: 3200 samples -> 21 frames) the top_db clamp (max over the WHOLE
 // [80, T] array, including the frame the slicing later drops) happens in-kernel; otherwise each
@@ -75,13 +75,19 @@ __device__ __forceinline__ long long out_index(int spf, int n_slices, int n_mels
 //  - the mel dot runs over a compile-time 24-bin band (host rows zero-padded, 16-B weight reads);
 //  - step 3 maps items bin-major / frame-minor over the whole chunk, so the complex-STFT store (librosa's
 //    [bin][frame] layout) writes 21-frame runs instead of 8-B scatters (configs[4] STFT 0.65 -> 0.50 ms).
+//  - without the complex-STFT output (the segment / configs[1] case) steps 1-4 touch only the wave's own frames:
+//    wave-synchronous LDS hand-offs, one block barrier per item (0.172 -> 0.154 ms), dB via v_log_f32 (0.151 ms).
 // Tried: a persistent grid with the next item's samples prefetched into registers during steps 2-4 — the
 // loop-invariant address math the compiler hoisted out of the item loop needed 207-256 VGPRs (one block
-// per CU): 0.224 ms.
+// per CU): 0.224 ms.  PMC (r02, B = 4096): 1,907 VALU instructions per wave (636 per frame), 48 % of wave
+// cycles parked on waitcnt / barrier, 21 % issue-stalled.
 constexpr int WAVES = CHUNK / FPG;     // 7
 constexpr int MW = 24;                 // padded Slaney band width of the LDS table (host-checked)
 
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+// wave-synchronous LDS hand-off: a wave's LDS operations complete in issue order, so draining lgkmcnt (and keeping the
+// compiler from moving memory operations across) is enough when every lane that wrote belongs to the reading wave
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 // index of sample i after centre padding: reflect (librosa's 2017 default) or zero (then `keep` is false)
 __device__ __forceinline__ int padded_index(int i, int L, int pad_mode, bool& keep) {
@@ -91,6 +97,19 @@ __device__ __forceinline__ int padded_index(int i, int L, int pad_mode, bool& ke
         return min(j, 2 * (L - 1) - j);
     }
     return min(max(i, 0), L - 1);
+}
+
+// real-FFT untangling of the packed 320-point transform Z of one frame: X[k] and X[320 - k]
+__device__ __forceinline__ void untangle(const float2* __restrict__ zf, int k, const float2* __restrict__ twl, float2& X,
+                                         float2& Xm) {
+    const float2 zk = zf[k];
+    const float2 zm = zf[k == 0 ? 0 : 320 - k];
+    // E = (Zk + conj Zm)/2 ; O = -i/2 (Zk - conj Zm)
+    const float2 E = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y));
+    const float2 O = make_float2(0.5f * (zk.y + zm.y), -0.5f * (zk.x - zm.x));
+    const float2 WO = cmul(twl[k], O);
+    X = cadd(E, WO);
+    Xm = make_float2(E.x - WO.x, -(E.y - WO.y));   // X[320 - k] = conj(E - W^k O)
 }
 
 // lane (f1, n1) of step 1 loads z[n1 + 16 n2] = (x[s0 + 2(n1 + 16 n2)], x[s0 + 2(n1 + 16 n2) + 1]), n2 < 20
@@ -112,7 +131,10 @@ __device__ __forceinline__ void load_frame(float2 (&x)[20], const float* __restr
     }
 }
 
-template <bool FAST_MEL>
+// RI: the complex STFT is stored too (bin-major over the whole chunk: block barriers between the steps).  Without it
+// every step until the top_db maximum touches only the wave's own three frames, so the waves hand off through LDS
+// wave-synchronously and one block barrier remains per item.
+template <bool FAST_MEL, bool RI>
 __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec640(SpecArgs a, int n_chunks) {
     __shared__ float2 zbuf[WAVES * FPG * ZS];
     __shared__ float dbuf[80 * CHUNK];
@@ -175,7 +197,7 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec640(SpecArgs a, in
                     zf[k2 * 17 + n1] = y;
                 }
         }
-        lds_barrier();
+        if constexpr (RI) lds_barrier(); else wave_lds_sync();
         // ---- step 2: 16-point DFTs over n1, lane = (f, k2) ----
         {
             const int f = lane / 20, k2 = lane - 20 * (lane / 20);
@@ -186,7 +208,7 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec640(SpecArgs a, in
 #pragma unroll
                 for (int n = 0; n < 16; ++n) w[n] = zf[k2 * 17 + n];
             }
-            lds_barrier();
+            if constexpr (RI) lds_barrier(); else wave_lds_sync();
             if (act) {
                 dft16(w, twl);
 #pragma unroll
@@ -195,49 +217,74 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec640(SpecArgs a, in
                     for (int d = 0; d < 4; ++d) zf[k2 + 20 * (c + 4 * d)] = w[4 * c + d];
             }
         }
-        lds_barrier();
-        // ---- step 3: real-FFT untangling + magnitude over the chunk, item = (k, f), f fastest ----
-        constexpr int IT3 = (161 * CHUNK + 64 * WAVES - 1) / (64 * WAVES);   // 8
-        float mk[IT3], mm[IT3];
+        if constexpr (RI) {
+            lds_barrier();
+            // ---- step 3: real-FFT untangling + magnitude over the chunk, item = (k, f), f fastest ----
+            constexpr int IT3 = (161 * CHUNK + 64 * WAVES - 1) / (64 * WAVES);   // 8
+            float mk[IT3], mm[IT3];
 #pragma unroll
-        for (int j = 0; j < IT3; ++j) {
-            const int it = tid + 64 * WAVES * j;
-            const int k = it / CHUNK, f = it - CHUNK * k;
-            if (k > 160 || f >= nf) continue;
-            const float2* zf = zbuf + f * ZS;
-            const float2 zk = zf[k];
-            const float2 zm = zf[k == 0 ? 0 : 320 - k];
-            // E = (Zk + conj Zm)/2 ; O = -i/2 (Zk - conj Zm)
-            const float2 E = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y));
-            const float2 O = make_float2(0.5f * (zk.y + zm.y), -0.5f * (zk.x - zm.x));
-            const float2 WO = cmul(twl[k], O);
-            const float2 X = cadd(E, WO);
-            const float2 Xm = make_float2(E.x - WO.x, -(E.y - WO.y));   // X[320 - k] = conj(E - W^k O)
-            mk[j] = sqrtf(X.x * X.x + X.y * X.y);
-            mm[j] = sqrtf(Xm.x * Xm.x + Xm.y * Xm.y);
-            if (a.stft_ri) {
+            for (int j = 0; j < IT3; ++j) {
+                const int it = tid + 64 * WAVES * j;
+                const int k = it / CHUNK, f = it - CHUNK * k;
+                if (k > 160 || f >= nf) continue;
+                const float2* zf = zbuf + f * ZS;
+                float2 X, Xm;
+                untangle(zf, k, twl, X, Xm);
+                mk[j] = sqrtf(X.x * X.x + X.y * X.y);
+                mm[j] = sqrtf(Xm.x * Xm.x + Xm.y * Xm.y);
                 float2* o = reinterpret_cast<float2*>(a.stft_ri) + (long long)u * 321 * T + t0 + f;
                 o[(long long)k * T] = X;
                 if (k != 160) o[(long long)(320 - k) * T] = Xm;
             }
-        }
-        lds_barrier();
+            lds_barrier();
 #pragma unroll
-        for (int j = 0; j < IT3; ++j) {
-            const int it = tid + 64 * WAVES * j;
-            const int k = it / CHUNK, f = it - CHUNK * k;
-            if (k > 160 || f >= nf) continue;
-            float* mf = reinterpret_cast<float*>(zbuf + f * ZS);
-            mf[k] = mk[j];
-            mf[320 - k] = mm[j];
-        }
-        if (FAST_MEL) {   // bins [321, 321 + MW) are read by the padded band dots: make them zero
-            for (int it = tid; it < CHUNK * MW; it += 64 * WAVES) {
-                const int f = it / MW, j = it - MW * f;
-                reinterpret_cast<float*>(zbuf + f * ZS)[321 + j] = 0.f;
+            for (int j = 0; j < IT3; ++j) {
+                const int it = tid + 64 * WAVES * j;
+                const int k = it / CHUNK, f = it - CHUNK * k;
+                if (k > 160 || f >= nf) continue;
+                float* mf = reinterpret_cast<float*>(zbuf + f * ZS);
+                mf[k] = mk[j];
+                mf[320 - k] = mm[j];
             }
+            if (FAST_MEL) {   // bins [321, 321 + MW) are read by the padded band dots: make them zero
+                for (int it = tid; it < CHUNK * MW; it += 64 * WAVES) {
+                    const int f = it / MW, j = it - MW * f;
+                    reinterpret_cast<float*>(zbuf + f * ZS)[321 + j] = 0.f;
+                }
+            }
+            lds_barrier();
+        } else {
+            wave_lds_sync();
+            // ---- step 3: untangling + magnitude of the wave's own frames, item = (f, k) ----
+            constexpr int IT3 = (FPG * 161 + 63) / 64;   // 8
+            float mk[IT3], mm[IT3];
+#pragma unroll
+            for (int j = 0; j < IT3; ++j) {
+                const int it = lane + 64 * j;
+                if (it >= ng * 161) break;
+                const int f = it / 161, k = it - 161 * f;
+                float2 X, Xm;
+                untangle(zw + f * ZS, k, twl, X, Xm);
+                mk[j] = sqrtf(X.x * X.x + X.y * X.y);
+                mm[j] = sqrtf(Xm.x * Xm.x + Xm.y * Xm.y);
+            }
+            wave_lds_sync();
+#pragma unroll
+            for (int j = 0; j < IT3; ++j) {
+                const int it = lane + 64 * j;
+                if (it >= ng * 161) break;
+                const int f = it / 161, k = it - 161 * f;
+                float* mf = reinterpret_cast<float*>(zw + f * ZS);
+                mf[k] = mk[j];
+                mf[320 - k] = mm[j];
+            }
+            if (FAST_MEL)
+                for (int it = lane; it < FPG * MW; it += 64) {
+                    const int f = it / MW, j = it - MW * f;
+                    reinterpret_cast<float*>(zw + f * ZS)[321 + j] = 0.f;
+                }
+            wave_lds_sync();
         }
-        lds_barrier();
         // ---- step 4: Slaney mel + dB, item = (f, m) ----
         float vmax = -INFINITY;
         for (int it = lane; it < ng * n_mels; it += 64) {
@@ -259,7 +306,7 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec640(SpecArgs a, in
                 const int wdt = mel_wd[m];
                 for (int j = 0; j < wdt; ++j) acc = fmaf(mf[j], wm[j], acc);
             }
-            const float db = acc > a.amin ? 20.0f * log10f(acc) : a.db_floor;
+            const float db = acc > a.amin ? 6.0205999132796239f * __log2f(acc) : a.db_floor;
             vmax = fmaxf(vmax, db);
             dbuf[m * CHUNK + g + f] = db;
         }
@@ -348,10 +395,12 @@ int launch_spectrogram(const SpecArgs& a, hipStream_t s) {
             return 3;   // AVSE_ERR_UNSUPPORTED
         }
         if (n_chunks > 1) AVSE_HIP_CHECK(hipMemsetAsync(a.umax, 0, sizeof(unsigned) * a.n_utt, s));
-        if (a.n_mels <= 80 && a.mel_max_width == MW)
-            hipLaunchKernelGGL(k_spec640<true>, dim3((unsigned)items), dim3(64 * WAVES), 0, s, a, n_chunks);
-        else
-            hipLaunchKernelGGL(k_spec640<false>, dim3((unsigned)items), dim3(64 * WAVES), 0, s, a, n_chunks);
+        const bool fast = a.n_mels <= 80 && a.mel_max_width == MW, ri = a.stft_ri != nullptr;
+        const dim3 grid((unsigned)items), block(64 * WAVES);
+        if (fast && ri) hipLaunchKernelGGL((k_spec640<true, true>), grid, block, 0, s, a, n_chunks);
+        else if (fast) hipLaunchKernelGGL((k_spec640<true, false>), grid, block, 0, s, a, n_chunks);
+        else if (ri) hipLaunchKernelGGL((k_spec640<false, true>), grid, block, 0, s, a, n_chunks);
+        else hipLaunchKernelGGL((k_spec640<false, false>), grid, block, 0, s, a, n_chunks);
         AVSE_HIP_CHECK(hipGetLastError());
         if (n_chunks > 1 && need_clamp_pass) {
             hipLaunchKernelGGL(k_spec_clamp, dim3(1024), dim3(256), 0, s, a);
