@@ -237,7 +237,7 @@ struct HaloArgs {
     const float* vmean;      // nullable [Hc][Wc]               (V1)
     const float* vstd;
     void* out;               // bf16, pooled [N][Hc/2][Wc/2][Co] at (clip stride, pixel stride, channel offset)
-    const void* w;           // bf16 [step][Co][32] (V1: [4 K-slices][Co][32], V1_GMAP, conv_v1r.hip)
+    const void* w;           // bf16 [step][Co][32] (V1: [5 kernel rows][Co][32], conv_v1r.hip)
     const float* scale;
     const float* shift;
     int N, Hc, Wc, Ci, Co;
@@ -245,21 +245,11 @@ struct HaloArgs {
     int out_pix_stride;
     int out_c_off;
     int mfma32;              // conv_stream.hip: 1 = v_mfma_f32_32x32x16_bf16 compute waves (A/B variant)
-    const float* vrn;        // V1: nullable [Hc][Wc][2] = (1 / std, -mean / std), from launch_vnorm_prep
     unsigned long long* prof;   // ablation harness only (ABL & 128): per-wave cycle counters, else unused
 };
 
-// v_conv1 dense K (conv_v1r.hip): K = 125 (5 x 5 taps x 5 frames) in 16 groups of 8 over 4 MFMA K-slices.
-// Group g < 15: kernel row ky = g / 3, elements j = 8 (g % 3) + e of the row's kx-major / frame-minor run
-// (kx = j / 5, frame = j % 5, j < 24); group 15: element e < 5 = (ky = e, kx = 4, frame 4), e >= 5 zero.
-// K-slice s, 16-lane k-group kg holds group V1_GMAP[s][kg]: the pairing with the fewest LDS bank conflicts
-// on the A-fragment reads (exhaustive search, DESIGN.md: only group 15's half-wave is 2-way), group 15 last.
-constexpr int V1_GMAP[4][4] = {{0, 3, 1, 4}, {2, 5, 6, 9}, {7, 10, 8, 14}, {11, 13, 12, 15}};
-
 int launch_conv_stream(const HaloArgs& a, hipStream_t s);   // conv_stream.hip (non-V1 variants)
-int launch_conv_v1r(const HaloArgs& a, hipStream_t s);      // conv_v1r.hip (v_conv1, dense K)
-// VideoNormalizer table for conv_v1r.hip: rn[p] = (1 / std[p], -mean[p] / std[p]), p < npix
-int launch_vnorm_prep(const float* mean, const float* stdv, float* rn, int npix, hipStream_t s);
+int launch_conv_v1r(const HaloArgs& a, hipStream_t s);      // conv_v1r.hip (v_conv1, kernel-row runs)
 int launch_video_prep(const float* video, const float* mean, const float* stdv, void* out, int64_t N,
                       int dtype, hipStream_t s);
 int launch_audio_prep(const float* audio, void* out, int64_t N, int dtype, hipStream_t s);

@@ -571,25 +571,14 @@ int build_layer(avse_weights* W, const LayerDef& L, const float* kernel, const f
         if ((rc = upload(W, scale_h, &G.scale_h))) return rc;
         std::vector<uint16_t> hp;
         if (G.halo == HALO_V1) {
-            // conv_v1r.hip: 4 K-slices [slice][Cout][32], k-group kg of slice s = group V1_GMAP[s][kg]
-            hp.assign((size_t)4 * L.cout * 32, 0);
-            for (int s = 0; s < 4; ++s)
-                for (int kg = 0; kg < 4; ++kg) {
-                    const int g = V1_GMAP[s][kg];
-                    for (int e = 0; e < 8; ++e) {
-                        int ky, kx, f;
-                        if (g < 15) {
-                            const int j = 8 * (g % 3) + e;
-                            ky = g / 3, kx = j / 5, f = j % 5;
-                        } else {
-                            if (e >= 5) continue;
-                            ky = e, kx = 4, f = 4;
-                        }
-                        for (int n = 0; n < L.cout; ++n)
-                            hp[((size_t)s * L.cout + n) * 32 + kg * 8 + e] =
+            // conv_v1r.hip: slice ky, k = kx * 6 + frame (frame 5 and k = 30, 31 zero)
+            hp.assign((size_t)L.kh * L.cout * 32, 0);
+            for (int ky = 0; ky < L.kh; ++ky)
+                for (int n = 0; n < L.cout; ++n)
+                    for (int kx = 0; kx < L.kw; ++kx)
+                        for (int f = 0; f < L.cin; ++f)
+                            hp[((size_t)ky * L.cout + n) * 32 + kx * 6 + f] =
                                 f2bf(sgn[n] * kernel[((size_t)(ky * L.kw + kx) * L.cin + f) * L.cout + n]);
-                    }
-                }
         } else {
             const int nsteps = (L.cin / 128) * 4 * ntap;   // (4 chunks of 32 channels per 128) x taps
             hp.assign((size_t)nsteps * L.cout * 32, 0);
@@ -1079,11 +1068,6 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
                 HaloArgs h = (i < 5) ? halo_args(G, vb(v_in[i]), vid, vm, vs, vb(v_in[i + 1]),
                                                  (long long)G.ho * G.wo * G.def.cout, G.def.cout, 0, n, opt)
                                      : halo_args(G, vb(v_in[i]), vid, vm, vs, cat, 5248, G.def.cout, 3200, n, opt);
-                if (G.halo == HALO_V1 && vm) {   // (1 / std, -mean / std) per pixel into the unused B_VIN buffer
-                    float* rn = reinterpret_cast<float*>(vb(B_VIN));
-                    if ((rc = launch_vnorm_prep(vm, vs, rn, G.def.hin * G.def.win, s))) return rc;
-                    h.vrn = rn;
-                }
                 rc = G.halo == HALO_V1 ? launch_conv_v1r(h, s) : launch_conv_stream(h, s);
                 if (rc || (rc = mark())) return rc;
                 continue;

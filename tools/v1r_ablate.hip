@@ -32,8 +32,7 @@ float run(const HaloArgs& a, int reps) {
     return ms / reps;
 }
 
-int main(int argc, char** argv) {
-    const std::string mode = argc > 1 ? argv[1] : "all";
+int main() {
     const int N = 512, H = 128, C = 128;
     HaloArgs a{};
     a.variant = HALO_V1;
@@ -65,23 +64,11 @@ int main(int argc, char** argv) {
     std::vector<float> ones((size_t)H * H, 1.f);
     (void)hipMemcpy(stdv, ones.data(), ones.size() * 4, hipMemcpyHostToDevice);
     a.video = video; a.vmean = mean; a.vstd = stdv; a.out = out; a.w = w; a.scale = sc; a.shift = sh;
-    float* rn;
-    (void)hipMalloc(&rn, (size_t)H * H * 8);
-    (void)launch_vnorm_prep(mean, stdv, rn, H * H, 0);
-    a.vrn = rn;
     const double flop = 2.0 * N * H * H * C * 125;
     const int reps = 10;
     auto rep = [&](const char* name, float ms) {
         std::printf("%-34s %8.4f ms  %7.1f TF/s (125-K)\n", name, ms, flop / (ms * 1e-3) / 1e12);
     };
-    if (mode == "full") {   // for rocprofv3 --pmc: the production variant only, then the compute-only one
-        rep("full", run<0>(a, reps));
-        return 0;
-    }
-    if (mode == "compute") {
-        rep("compute only", run<11>(a, reps));
-        return 0;
-    }
     rep("full", run<0>(a, reps));
     rep("no output pass (1)", run<1>(a, reps));
     rep("no loader window work (2)", run<2>(a, reps));
@@ -90,38 +77,5 @@ int main(int argc, char** argv) {
     rep("no output pass, no window (3)", run<3>(a, reps));
     rep("only MFMA+frags: (1|2|8)", run<11>(a, reps));
     rep("full (again)", run<0>(a, reps));
-    rep("no compute priority (512)", run<512>(a, reps));
-    rep("loader priority 3 (1024)", run<1024>(a, reps));
-    rep("full (again)", run<0>(a, reps));
-    rep("compute only, no maxima (11|256)", run<11 | 256>(a, reps));
-    rep("compute only, no A reads (11|64)", run<11 | 64>(a, reps));
-    rep("compute only, no B reads (11|128)", run<11 | 128>(a, reps));
-    rep("compute only, MFMA alone (11|64|128|256)", run<11 | 64 | 128 | 256>(a, reps));
-    rep("compute only (again)", run<11>(a, reps));
-    {   // phase stamps (ABL 16): loader phases 7 = top of iteration .. vmcnt, 0 = after the wait, 1 win_store,
-        // 2 left_build, 3 out_pass, 4 win_load, 5 lgkmcnt, 6 barrier; compute 3 slices 1-3, 0 slice 0, 1 lgkm, 2 barrier
-        unsigned long long* prof;
-        const int nb = 256;
-        (void)hipMalloc(&prof, (size_t)nb * 8 * 8 * 8);
-        (void)hipMemset(prof, 0, (size_t)nb * 8 * 8 * 8);
-        a.prof = prof;
-        rep("stamped (16)", run<16>(a, 1));
-        std::vector<unsigned long long> h((size_t)nb * 64);
-        (void)hipMemcpy(h.data(), prof, h.size() * 8, hipMemcpyDeviceToHost);
-        const int tiles = N * 64 / nb;
-        const char* ln[8] = {"vm wait", "win_store", "left_build", "out_pass", "win_load", "lgkm wait", "barrier", "iter top"};
-        const char* cn[8] = {"slice0+epi", "lgkm wait", "barrier", "slices1-3", "-", "-", "-", "-"};
-        for (int role = 0; role < 2; ++role) {
-            std::printf("%s cycles per tile:", role ? "loader " : "compute");
-            for (int i = 0; i < 8; ++i) {
-                double s = 0;
-                for (int b = 0; b < nb; ++b)
-                    for (int w = 0; w < 4; ++w) s += (double)h[((size_t)b * 8 + role * 4 + w) * 8 + i];
-                s /= (double)nb * 4 * tiles;
-                if (s > 0) std::printf("  %s %.0f", role ? ln[i] : cn[i], s);
-            }
-            std::printf("\n");
-        }
-    }
     return 0;
 }
