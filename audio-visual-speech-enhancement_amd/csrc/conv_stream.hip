@@ -413,12 +413,17 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
                     for (int j = 0; j < 8; ++j)
                         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
                             __builtin_bit_cast(bf16x8, ca[i]), __builtin_bit_cast(bf16x8, cb[j]), acc[i][j], 0, 0, 0);
+            // the next slice's 12 fragment reads one per MFMA from the start of the step (measured against two
+            // MFMAs per read over 24 MFMAs, 3:2, 1:2 and all reads first: -1 to -2 % on v_conv2 / v_conv4, the
+            // bunched forms +2 to +17 %).  A 3-slot weight ring that lets the compute waves skip the lgkmcnt(0)
+            // drain before each barrier was slower (+2-4 %): the drain overlaps the barrier wait, the deferred
+            // wait stalls the next step's first MFMAs
 #pragma unroll
             for (int r = 0; r < 12; ++r) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);   // MFMA
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
                 __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
             }
-            __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, 20, 0);
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (!(ABL & 4)) {
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
