@@ -6,6 +6,7 @@
 #include <cstdlib>
 #include <string>
 #include <vector>
+#include <algorithm>
 
 #include "../audio-visual-speech-enhancement_amd/csrc/conv_stream.hip"
 
@@ -107,5 +108,19 @@ int main() {
                     s[r][0] / steps[r], s[r][1] / steps[r], s[r][2] / steps[r]);
     };
     split("LAT10");
+    {   // per-workgroup busy span (compute wave 0: work + wait + barrier): the persistent grid's tail imbalance
+        std::vector<unsigned long long> hp(256 * 8 * 4);
+        (void)hipMemcpy(hp.data(), prof, hp.size() * 8, hipMemcpyDeviceToHost);
+        std::vector<double> tot;
+        for (int b = 0; b < 256; ++b) tot.push_back((double)(hp[(b * 8) * 4] + hp[(b * 8) * 4 + 1] + hp[(b * 8) * 4 + 2]));
+        std::sort(tot.begin(), tot.end());
+        std::printf("per-WG cycles: min %.0f  p10 %.0f  median %.0f  p90 %.0f  max %.0f  (max/median %.3f)\n", tot[0], tot[25],
+                    tot[128], tot[230], tot[255], tot[255] / tot[128]);
+        for (int x = 0; x < 8; ++x) {   // by XCD (block % 8)
+            double s = 0;
+            for (int b = x; b < 256; b += 8) s += (double)(hp[(b * 8) * 4] + hp[(b * 8) * 4 + 1] + hp[(b * 8) * 4 + 2]);
+            std::printf("  XCD %d mean %.0f\n", x, s / 32);
+        }
+    }
     return 0;
 }
