@@ -79,7 +79,7 @@ __device__ __forceinline__ void barrier_raw() { asm volatile("s_barrier" ::: "me
 // LAT (load -> LDS store distance, steps): 10 for 5x5, 6 for 3x3; it divides the unrolled chunk pair
 // (2 KS^2 steps).  Measured on v_conv2 (runtime-tap loader): LAT 4 / 5 / 10 / 20 = 1.14 / 1.04-1.13 / 1.00 /
 // 1.27 ms (20 spills).
-template <int KS, int TH, int TW, int NCLIP, int LAT_ = (KS == 5 ? 10 : 6)>
+template <int KS, int TH, int TW, int NCLIP, int LAT_ = (KS == 5 ? 10 : 6), int BP_ = 1>
 struct StreamGeom {
     static constexpr int HH = TH + KS - 1, HW = TW + KS - 1;
     static constexpr int HPIX = NCLIP * HH * HW;              // halo pixels per chunk
@@ -88,16 +88,20 @@ struct StreamGeom {
     static constexpr int NTAP = KS * KS;
     static constexpr int CSLOT = HPIECES * 1024;               // bytes per halo chunk slot
     static constexpr int WSLOT = 8192;                         // one K-slice of 128 co x 32 ci
-    // LAT: steps between a load and its LDS write; weights are loaded WD = LAT + 2 steps ahead of their
-    // slice and land in a 2-slot LDS ring; 3 halo chunk slots
-    static constexpr int LAT = LAT_, WD = LAT + 2, NHS = 3, PAIR = 2 * NTAP;
-    static constexpr int LDS = NHS * CSLOT + 2 * WSLOT;
+    // LAT: steps between a load and its LDS write; BP: steps per barrier.  The loader stores slice j + BP + 1
+    // during step j (loaded WD = LAT + BP + 1 steps ahead) into a ring of NWS = 2 BP weight slots: the slot
+    // it overwrites held slice j + 1 - BP, whose fragments the compute waves read during step j - BP, before
+    // the previous barrier; 3 halo chunk slots
+    static constexpr int LAT = LAT_, BP = BP_, NWS = 2 * BP, WD = LAT + BP + 1, NHS = 3, PAIR = 2 * NTAP;
+    static_assert(BP == 1 || BP == 2, "barrier period");
+    static constexpr int LDS = NHS * CSLOT + NWS * WSLOT;
     static_assert(LDS + 1024 <= 160 * 1024, "LDS");   // one workgroup per CU: ~250 VGPRs x 8 waves fill the register file
     static_assert(NCLIP * TH * TW == 256, "tile = 256 conv pixels (4 waves x 4 fragments)");
     static_assert(PAIR % LAT == 0 && LAT < NTAP, "the ring set of a step is compile-time");
     // chunk g+2's pieces are loaded at taps 0..HPW-1 of chunk g and written LAT steps later, before
     // the first fragment read of chunk g+2 at step NTAP-1 of chunk g+1
-    static_assert(HPW <= NTAP && HPW - 1 + LAT <= 2 * NTAP - 2, "halo pieces must land in time");
+    // (a store is visible after the barrier closing its BP-step group: at most BP - 1 steps later)
+    static_assert(HPW <= NTAP && HPW - 1 + LAT + BP - 1 <= 2 * NTAP - 2, "halo pieces must land in time");
     // loads issued by step j (tap j % NTAP): two weight chunks + one piece on the first HPW taps
     static constexpr int loads(int j, int abl) {
         const int tap = ((j % NTAP) + NTAP) % NTAP;
@@ -116,18 +120,20 @@ struct StreamGeom {
 // loop, 2 = no weight streaming in the loop, 4 = no barrier/wait, 8 = no fragment reads, 16 = no MFMAs,
 // 64 = every tile reads clip 0's window (L2-resident input), 128 = s_memtime per step: cycles working /
 // waiting (vmcnt, lgkmcnt) / in the barrier, per wave, into a.prof[(block * 8 + wave) * 4 + {0,1,2, 3=steps}]
-template <int KS, int TH, int TW, int NCLIP, bool M16 = true, int LAT_ = StreamGeom<KS, TH, TW, NCLIP>::LAT, int ABL = 0>
+template <int KS, int TH, int TW, int NCLIP, bool M16 = true, int LAT_ = StreamGeom<KS, TH, TW, NCLIP>::LAT, int ABL = 0,
+          int BP_ = 1>
 __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
-    using G = StreamGeom<KS, TH, TW, NCLIP, LAT_>;
+    using G = StreamGeom<KS, TH, TW, NCLIP, LAT_, BP_>;
     constexpr int HH = G::HH, HW = G::HW, HPIX = G::HPIX, HPW = G::HPW, NTAP = G::NTAP;
     constexpr int CSLOT = G::CSLOT, WSLOT = G::WSLOT, LAT = G::LAT, WD = G::WD, PAIR = G::PAIR;
+    constexpr int BP = G::BP, NWS = G::NWS;
     constexpr int BPR = TW / 8, BPC = (TH / 4) * BPR;     // 4x8-pixel blocks (32 MFMA rows) per row / clip
     static_assert(TW % 8 == 0 && TH % 4 == 0 && BPC % 2 == 0, "a wave's two blocks share their y origin mod 4");
     constexpr int PAD = (KS - 1) / 2;
 
     extern __shared__ __attribute__((aligned(1024))) char lds[];
     char* const halo = lds;                    // [NHS][CSLOT]
-    char* const wring = lds + G::NHS * CSLOT;  // [2][WSLOT]
+    char* const wring = lds + G::NHS * CSLOT;  // [NWS][WSLOT]
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -218,14 +224,14 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
                               : (void)0), ...);
         }(std::make_integer_sequence<int, HPW>{});
 #pragma unroll
-        for (int s = 0; s < 2; ++s)
+        for (int s = 0; s <= BP; ++s)
 #pragma unroll
             for (int u = 0; u < 2; ++u) st16(wdst + s * WSLOT + 1024 * u, ld16(wrs, wvoff[u], (s % spt) * wslice));
         i32x4 rw[LAT][2], rp[LAT];
         [&]<int... S>(std::integer_sequence<int, S...>) {
             ([&] {
-                 rw[S][0] = ld16(wrs, wvoff[0], ((S + 2) % spt) * wslice);
-                 rw[S][1] = ld16(wrs, wvoff[1], ((S + 2) % spt) * wslice);
+                 rw[S][0] = ld16(wrs, wvoff[0], ((S + BP + 1) % spt) * wslice);
+                 rw[S][1] = ld16(wrs, wvoff[1], ((S + BP + 1) % spt) * wslice);
                  constexpr int vt = NTAP - LAT + S;   // tap of virtual step S - LAT
                  if constexpr (vt < HPW && !(ABL & 1)) rp[S] = ld16(cur_rs, vo_cur[vt < HPW ? vt : 0], 64);
              }(), ...);
@@ -238,6 +244,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
         // land at pd_cur; pd_prev = where the pieces loaded during chunk g-1 land
         int k = 0, c = 0, g = 0, hs2 = 2;           // hs2 = halo slot of chunk g+2
         int woff = (WD % spt) * wslice;             // weights loaded by the next step: slice step + WD
+        int wrot = 0;                               // (first step of this chunk pair) % NWS
         int vsel[HPW];
         __amdgpu_buffer_rsrc_t prs = cur_rs;
         int psoff = 0;
@@ -279,11 +286,12 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
             constexpr int tl = ((jl % NTAP) + NTAP) % NTAP;
             constexpr bool lprev = (jl < 0) || (jl / NTAP != j / NTAP);  // ... during the previous chunk
             if constexpr (tap == 0) chunk_begin();
-            // 1. LDS stores of set S: weights of slice j+2 (slot j & 1: slice j's, read during step j-1) and
-            //    the piece loaded with them
+            // 1. LDS stores of set S: weights of slice j+BP+1 (slot (j+BP+1) % NWS) and the piece loaded
+            //    with them
             if constexpr (!(ABL & 2)) {
-                st16(wdst + (j & 1) * WSLOT, rw[S][0]);
-                st16(wdst + (j & 1) * WSLOT + 1024, rw[S][1]);
+                char* const wd = wdst + (((j + BP + 1) + wrot) & (NWS - 1)) * WSLOT;
+                st16(wd, rw[S][0]);
+                st16(wd + 1024, rw[S][1]);
             }
             if constexpr (tl < HPW && !(ABL & 1))
                 piece_store(std::integral_constant<int, (tl < HPW ? tl : 0)>{}, lprev ? pd_prev : pd_cur, rp[S]);
@@ -295,9 +303,9 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
             if constexpr (tap < HPW && !(ABL & 1)) rp[S] = ld16(prs, vsel[tap < HPW ? tap : 0], psoff);
             woff += wslice;
             if (woff == wend) woff = 0;
-            // 3. the set of step j-LAT+1 has landed (stored by step j+1); this step's stores are visible
-            //    after the barrier
-            if constexpr (!(ABL & 4)) {
+            // 3. at the end of a BP-step group: the set of step j-LAT+1 has landed (stored by step j+1);
+            //    the group's stores are visible after the barrier
+            if constexpr (!(ABL & 4) && j % BP == BP - 1) {
                 if constexpr ((ABL & 128) != 0) pt0 = __builtin_amdgcn_s_memtime();
                 wait_vm_lgkm0<G::vm_wait(j, ABL)>();
                 if constexpr ((ABL & 128) != 0) pt1 = __builtin_amdgcn_s_memtime();
@@ -312,10 +320,12 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
             }
             if constexpr (tap == NTAP - 1) chunk_end();
         };
-        for (int pr = 0; pr < nchunks; pr += 2)
+        for (int pr = 0; pr < nchunks; pr += 2) {
             [&]<int... J>(std::integer_sequence<int, J...>) {
                 (lstep(std::integral_constant<int, J>{}), ...);
             }(std::make_integer_sequence<int, PAIR>{});
+            wrot = (wrot + PAIR) & (NWS - 1);
+        }
         wait_vm_lgkm0<0>();   // loads still in flight target registers and rows nobody reads
         if constexpr ((ABL & 128) != 0)
             if (lane == 0) {
@@ -397,6 +407,8 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
             }
         };
 
+        unsigned long long ptp = (ABL & 128) ? __builtin_amdgcn_s_memtime() : 0, pt0 = 0, pt1 = 0, p_work = 0,
+                           p_wait = 0, p_bar = 0;
         int tap1 = 1, hs1 = 0;
         i32x4 fa[4], fb[8], na[4], nb[8];
         frags(0, 0, 0, fa, fb);
@@ -404,8 +416,9 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         barrier_raw();   // slice 0 read: the loaders may now overwrite weight slot 0
 
-        auto cstep = [&](auto first, int t, i32x4 (&ca)[4], i32x4 (&cb)[8], i32x4 (&xa)[4], i32x4 (&xb)[8]) {
-            if constexpr (!(ABL & 8)) frags(hs1, tap1, (t + 1) & 1, xa, xb);
+        // bar: the step closes a BP-step group (t % BP == BP - 1; t is even on the first call of each pair)
+        auto cstep = [&](auto bar, int t, i32x4 (&ca)[4], i32x4 (&cb)[8], i32x4 (&xa)[4], i32x4 (&xb)[8]) {
+            if constexpr (!(ABL & 8)) frags(hs1, tap1, (t + 1) & (NWS - 1), xa, xb);
             if constexpr (!(ABL & 16))
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
@@ -425,9 +438,18 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
             }
             __builtin_amdgcn_sched_group_barrier(0x008, 20, 0);
             __builtin_amdgcn_sched_barrier(0);
-            if constexpr (!(ABL & 4)) {
+            if constexpr (!(ABL & 4) && decltype(bar)::value) {
+                if constexpr ((ABL & 128) != 0) pt0 = __builtin_amdgcn_s_memtime();
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                if constexpr ((ABL & 128) != 0) pt1 = __builtin_amdgcn_s_memtime();
                 barrier_raw();
+                if constexpr ((ABL & 128) != 0) {
+                    const unsigned long long pt2 = __builtin_amdgcn_s_memtime();
+                    p_work += pt0 - ptp;
+                    p_wait += pt1 - pt0;
+                    p_bar += pt2 - pt1;
+                    ptp = pt2;
+                }
             }
             if (++tap1 == NTAP) {
                 tap1 = 0;
@@ -437,16 +459,18 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
         int t = 0;
         int cur_clip0, cur_oy0, cur_ox0;
         for (int kt = 0; kt < nmine; ++kt) {
-            cstep(std::true_type{}, t, fa, fb, na, nb);
-            cstep(std::false_type{}, t + 1, na, nb, fa, fb);
-            t += 2;
-            for (int s = 2; s < spt; s += 2, t += 2) {
-                cstep(std::false_type{}, t, fa, fb, na, nb);
-                cstep(std::false_type{}, t + 1, na, nb, fa, fb);
+            for (int s = 0; s < spt; s += 2, t += 2) {
+                cstep(std::bool_constant<BP == 1>{}, t, fa, fb, na, nb);
+                cstep(std::true_type{}, t + 1, na, nb, fa, fb);
             }
             tile_origin(kt, cur_clip0, cur_oy0, cur_ox0);
             epilogue(cur_clip0, cur_oy0, cur_ox0);
         }
+        if constexpr ((ABL & 128) != 0)
+            if (lane == 0) {
+                unsigned long long* pr = a.prof + ((size_t)blockIdx.x * 8 + wave) * 4;
+                pr[0] = p_work; pr[1] = p_wait; pr[2] = p_bar; pr[3] = (unsigned long long)t;
+            }
         return;
     }
     // fragment geometry (v_mfma_f32_32x32x16_bf16: lane l holds row/column l & 31 and k-half hi = l >> 5).
@@ -537,9 +561,10 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     barrier_raw();   // slice 0 read: the loaders may now overwrite weight slot 0
 
-    auto cstep = [&](auto first, int t, i32x4 (&ca)[4], i32x4 (&cb)[8], i32x4 (&xa)[4], i32x4 (&xb)[8]) {
-        // fragments of the next slice (weights in ring slot (t+1)&1), interleaved with the 16 MFMAs
-        if constexpr (!(ABL & 8)) frags(hs1, tap1, (t + 1) & 1, xa, xb);
+    // first: the tile's first step (accumulate onto zero); bar: the step closes a BP-step group
+    auto cstep = [&](auto first, auto bar, int t, i32x4 (&ca)[4], i32x4 (&cb)[8], i32x4 (&xa)[4], i32x4 (&xb)[8]) {
+        // fragments of the next slice (weights in ring slot (t+1) % NWS), interleaved with the 16 MFMAs
+        if constexpr (!(ABL & 8)) frags(hs1, tap1, (t + 1) & (NWS - 1), xa, xb);
         if constexpr (!(ABL & 16))
 #pragma unroll
             for (int m = 0; m < 2; ++m)
@@ -557,7 +582,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
         }
         __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (!(ABL & 4)) {
+        if constexpr (!(ABL & 4) && decltype(bar)::value) {
             if constexpr ((ABL & 128) != 0) pt0 = __builtin_amdgcn_s_memtime();
             // LDS reads only: the epilogue's global stores (vmcnt on gfx9) are never waited for
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -578,13 +603,14 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
     };
     int t = 0;
     int cur_clip0, cur_oy0, cur_ox0;
+    using BAR0 = std::bool_constant<BP == 1>;
     for (int kt = 0; kt < nmine; ++kt) {
-        cstep(std::true_type{}, t, fa, fb, na, nb);
-        cstep(std::false_type{}, t + 1, na, nb, fa, fb);
+        cstep(std::true_type{}, BAR0{}, t, fa, fb, na, nb);
+        cstep(std::false_type{}, std::true_type{}, t + 1, na, nb, fa, fb);
         t += 2;
         for (int s = 2; s < spt; s += 2, t += 2) {
-            cstep(std::false_type{}, t, fa, fb, na, nb);
-            cstep(std::false_type{}, t + 1, na, nb, fa, fb);
+            cstep(std::false_type{}, BAR0{}, t, fa, fb, na, nb);
+            cstep(std::false_type{}, std::true_type{}, t + 1, na, nb, fa, fb);
         }
         tile_origin(kt, cur_clip0, cur_oy0, cur_ox0);
         epilogue(cur_clip0, cur_oy0, cur_ox0);

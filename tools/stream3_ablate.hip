@@ -3,7 +3,9 @@
 //   hipcc --offload-arch=gfx950 -O3 -std=c++20 -o _stream3_ablate stream3_ablate.hip
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <string>
+#include <vector>
 
 #include "../audio-visual-speech-enhancement_amd/csrc/conv_stream.hip"
 
@@ -16,10 +18,10 @@ int ensure_lds_attr(const void* fn, int bytes) {
 
 using namespace avse;
 
-template <int ABL>
+template <int ABL, int BP = 1>
 float run(const HaloArgs& a, int reps) {
-    using G = StreamGeom<3, 16, 16, 1>;
-    auto k = k_conv_stream<3, 16, 16, 1, true, G::LAT, ABL>;
+    using G = StreamGeom<3, 16, 16, 1, 6, BP>;
+    auto k = k_conv_stream<3, 16, 16, 1, true, G::LAT, ABL, BP>;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS + 1024);
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
@@ -51,8 +53,19 @@ int main() {
         (void)hipMalloc(&w, (size_t)9 * Ci * Co * 2);
         (void)hipMalloc(&sc, Co * 4);
         (void)hipMalloc(&sh, Co * 4);
-        (void)hipMemset(in, 0, (size_t)N * H * H * Ci * 2);
-        (void)hipMemset(w, 0, (size_t)9 * Ci * Co * 2);
+        // AVSE_ABL_RANDOM=1: random bf16 activations / weights (MFMA power, hence clock, depends on data)
+        const char* rnd = std::getenv("AVSE_ABL_RANDOM");
+        if (rnd && rnd[0] == '1') {
+            std::vector<uint16_t> h((size_t)N * H * H * Ci);
+            uint32_t st = 12345;
+            auto next = [&] { st = st * 1664525u + 1013904223u; return st; };
+            for (auto& v : h) v = (uint16_t)(0x3c00 + (next() >> 22)) ^ (uint16_t)((next() >> 31) << 15);
+            (void)hipMemcpy(in, h.data(), h.size() * 2, hipMemcpyHostToDevice);
+            (void)hipMemcpy(w, h.data(), (size_t)9 * Ci * Co * 2, hipMemcpyHostToDevice);
+        } else {
+            (void)hipMemset(in, 0, (size_t)N * H * H * Ci * 2);
+            (void)hipMemset(w, 0, (size_t)9 * Ci * Co * 2);
+        }
         (void)hipMemset(sc, 0, Co * 4);
         (void)hipMemset(sh, 0, Co * 4);
         a.in = in; a.out = out; a.w = w; a.scale = sc; a.shift = sh;
@@ -63,6 +76,9 @@ int main() {
             std::printf("  %-30s %8.4f ms  %7.1f TF/s\n", name, ms, flop / (ms * 1e-3) / 1e12);
         };
         rep("full", run<0>(a, reps));
+        rep("full, barrier every step (BP 1)", run<0, 1>(a, reps));
+        rep("full", run<0>(a, reps));
+        rep("full, barrier every step (BP 1)", run<0, 1>(a, reps));
         rep("no halo pieces (1)", run<1>(a, reps));
         rep("no weight streaming (2)", run<2>(a, reps));
         rep("no loads at all (3)", run<3>(a, reps));

@@ -19,19 +19,19 @@ int ensure_lds_attr(const void* fn, int bytes) {
 
 using namespace avse;
 
-template <int ABL, int LAT = 10, bool M16 = true>
+template <int ABL, int LAT = 10, bool M16 = true, int BP = 1>
 float run(const HaloArgs& a, int reps) {
-    using G = StreamGeom<5, 16, 16, 1, LAT>;
-    (void)hipFuncSetAttribute((const void*)k_conv_stream<5, 16, 16, 1, M16, LAT, ABL>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              G::LDS);
+    using G = StreamGeom<5, 16, 16, 1, LAT, BP>;
+    (void)hipFuncSetAttribute((const void*)k_conv_stream<5, 16, 16, 1, M16, LAT, ABL, BP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              G::LDS + 1024);
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
     for (int r = 0; r < 10; ++r)   // warm-up long enough for the clock to settle under MFMA load
-        hipLaunchKernelGGL((k_conv_stream<5, 16, 16, 1, M16, LAT, ABL>), dim3(256, 1), dim3(512), G::LDS, 0, a);
+        hipLaunchKernelGGL((k_conv_stream<5, 16, 16, 1, M16, LAT, ABL, BP>), dim3(256, 1), dim3(512), G::LDS + 1024, 0, a);
     (void)hipEventRecord(e0, 0);
     for (int r = 0; r < reps; ++r)
-        hipLaunchKernelGGL((k_conv_stream<5, 16, 16, 1, M16, LAT, ABL>), dim3(256, 1), dim3(512), G::LDS, 0, a);
+        hipLaunchKernelGGL((k_conv_stream<5, 16, 16, 1, M16, LAT, ABL, BP>), dim3(256, 1), dim3(512), G::LDS + 1024, 0, a);
     (void)hipEventRecord(e1, 0);
     (void)hipEventSynchronize(e1);
     float ms = 0.f;
@@ -77,6 +77,9 @@ int main() {
     rep("full, 32x32x16 compute waves", run<0, 10, false>(a, reps));
     rep("MFMA only, 32x32x16 (15)", run<15, 10, false>(a, reps));
     rep("full", run<0, 10>(a, reps));
+    rep("full, barrier every step (BP 1)", run<0, 10, true, 1>(a, reps));
+    rep("full", run<0, 10>(a, reps));
+    rep("full, barrier every step (BP 1)", run<0, 10, true, 1>(a, reps));
     rep("no halo pieces (1)", run<1, 10>(a, reps));
     rep("no weight streaming (2)", run<2, 10>(a, reps));
     rep("no loads at all (3)", run<3, 10>(a, reps));
@@ -107,6 +110,18 @@ int main() {
         std::printf("%s %-8s cycles/step: work %7.1f  wait(vm/lgkm) %7.1f  barrier %7.1f\n", title, names[r],
                     s[r][0] / steps[r], s[r][1] / steps[r], s[r][2] / steps[r]);
     };
+    split("LAT10");
+    rep("instrumented, no pieces (129)", run<129, 10, false>(a, reps));
+    split("nopc ");
+    rep("instrumented, L2 input (192)", run<192, 10, false>(a, reps));
+    split("L2in ");
+    rep("instrumented, M16 (128)", run<128, 10>(a, reps));
+    split("M16  ");
+    rep("instrumented, M16 no pieces (129)", run<129, 10>(a, reps));
+    split("M16np");
+    rep("instrumented, M16 BP1 (128)", run<128, 10, true, 1>(a, reps));
+    split("M16b1");
+    rep("instrumented (128, 32x32x16) again", run<128, 10, false>(a, reps));
     split("LAT10");
     {   // per-workgroup busy span (compute wave 0: work + wait + barrier): the persistent grid's tail imbalance
         std::vector<unsigned long long> hp(256 * 8 * 4);
