@@ -37,7 +37,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, lo
 __device__ __forceinline__ int wsw(int row) { return 2 * ((row >> 2) & 1); }
 __device__ __forceinline__ i32x4 lds16(const char* p) { return *reinterpret_cast<const i32x4*>(p); }
 
-template <int MODE>
+// ABL: timing ablations for tools/gemm_ablate.hip only (0 in the library): 1 = the tile's last workgroup skips
+// reading the other partials (outputs meaningless)
+template <int MODE, int ABL = 0>
 __global__ __launch_bounds__(NT, 1) void k_gemm(GemmArgs g) {
     extern __shared__ __attribute__((aligned(1024))) char lds[];
     __shared__ int last_flag;
@@ -172,7 +174,7 @@ __global__ __launch_bounds__(NT, 1) void k_gemm(GemmArgs g) {
         for (int i = 0; i < 4; ++i)
 #pragma unroll
             for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-        for (int zz = 0; zz < g.ksplit; ++zz)
+        for (int zz = 0; zz < ((ABL & 1) ? 0 : g.ksplit); ++zz)
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
