@@ -38,9 +38,12 @@ __device__ __forceinline__ float mel_at(const IstftArgs& a, long long u, int m, 
     return a.mel_db[(u * a.n_mels + m) * (long long)a.T + t];
 }
 
+// D / |D| (librosa.magphase; 1 where D == 0) as D * rsq(|D|^2): one v_rsq_f32 and two multiplies instead of a
+// square root and two IEEE divisions (~10 instructions each; 16 per lane per chunk in k_istft_fused)
 __device__ __forceinline__ float2 unit_phase(float2 d) {
-    const float r = sqrtf(d.x * d.x + d.y * d.y);
-    return r > 0.f ? make_float2(d.x / r, d.y / r) : make_float2(1.f, 0.f);
+    const float r2 = d.x * d.x + d.y * d.y;
+    const float s = __builtin_amdgcn_rsqf(r2);
+    return r2 > 0.f ? make_float2(d.x * s, d.y * s) : make_float2(1.f, 0.f);
 }
 
 // X[k] = (pinv(mel) @ 10^(dB/20))[k] * D[k]/|D[k]| for one frame, k in [0, nb)
@@ -160,12 +163,19 @@ __global__ __launch_bounds__(64 * IWAVES) void k_istft_fused(IstftArgs a, int n_
     __shared__ float amp[FW][80];               // amplitudes, then y in place
     __shared__ float4 tri_l[80];
     __shared__ float win_l[640];
-    const float2* __restrict__ tw = a.twiddle;  // W640^k
+    __shared__ float2 tw[640];                  // W640^k
+    __shared__ float4 bins_l[321];              // per bin: the two pinv weights and the first mel band
     const int T = a.T, n_mels = a.n_mels;
     const long long Lout = (long long)a.hop * (T - 1);
 
+    // tables -> LDS once per (persistent) block: the DFT twiddles and bin weights were global-memory reads in
+    // every item's dependency chain
     for (int i = threadIdx.x; i < n_mels; i += 64 * IWAVES) tri_l[i] = a.tri[i];
-    for (int i = threadIdx.x; i < 640; i += 64 * IWAVES) win_l[i] = a.window[i];
+    for (int i = threadIdx.x; i < 640; i += 64 * IWAVES) {
+        win_l[i] = a.window[i];
+        tw[i] = a.twiddle[i];
+    }
+    for (int i = threadIdx.x; i < 321; i += 64 * IWAVES) bins_l[i] = a.bins[i];
     __syncthreads();
 
     for (int item = blockIdx.x; item < n_items; item += gridDim.x) {
@@ -177,10 +187,23 @@ __global__ __launch_bounds__(64 * IWAVES) void k_istft_fused(IstftArgs a, int n_
         const int t_hi = min(T - 1, b * OF + OF + 1);
         const int nfr = t_hi - t_lo + 1;
 
-        // ---- 1. amplitudes (frame fastest: runs of consecutive frames of one band) ----
-        for (int it = tid; it < FW * n_mels; it += 64 * IWAVES) {
-            const int m = it / FW, f = it - FW * m;
-            if (f < nfr) amp[f][m] = sqrtf(exp10f(0.1f * mel_at(a, u, m, t_lo + f)));
+        // ---- 1. amplitudes (frame fastest: runs of consecutive frames of one band); all of a lane's loads
+        //         (clamped in range) are issued before the first is used ----
+        {
+            constexpr int IT1 = (FW * 80 + 64 * IWAVES - 1) / (64 * IWAVES);   // 4 (n_mels <= 80, host-checked)
+            float mv[IT1];
+#pragma unroll
+            for (int j = 0; j < IT1; ++j) {
+                const int it = min(tid + 64 * IWAVES * j, FW * n_mels - 1);
+                const int m = it / FW, f = it - FW * m;
+                mv[j] = mel_at(a, u, m, t_lo + min(f, nfr - 1));
+            }
+#pragma unroll
+            for (int j = 0; j < IT1; ++j) {
+                const int it = tid + 64 * IWAVES * j;
+                const int m = it / FW, f = it - FW * m;
+                if (it < FW * n_mels && f < nfr) amp[f][m] = sqrtf(exp10f(0.1f * mv[j]));
+            }
         }
         ibarrier();
         // ---- 2. Thomas solve, lanes 0..2 of every wave = frames wave + 8 lane; 8 bands per batch of loads ----
@@ -245,7 +268,7 @@ __global__ __launch_bounds__(64 * IWAVES) void k_istft_fused(IstftArgs a, int n_
                 asm volatile("" ::: "memory");           // one iteration's table loads at a time (register pressure)
                 if (k > 160 || f >= nfr) continue;
                 const int km = k == 0 ? 320 : 320 - k;
-                const float4 bk = a.bins[k], bm = a.bins[km];
+                const float4 bk = bins_l[k], bm = bins_l[km];
                 const int jk = __float_as_int(bk.z), jm = __float_as_int(bm.z);
                 const float* y = amp[f];
                 const float ak = (jk >= 0 ? bk.x * y[jk] : 0.f) + (jk + 1 < n_mels && jk >= 0 ? bk.y * y[jk + 1] : 0.f);
