@@ -99,6 +99,10 @@ __device__ __forceinline__ int padded_index(int i, int L, int pad_mode, bool& ke
     return min(max(i, 0), L - 1);
 }
 
+// |X| by the hardware v_sqrt_f32 (1 ulp): sqrtf's correctly rounded sequence is ~12 instructions, 16 per lane
+// per chunk, and the magnitudes only feed the mel sums (dB tolerance 1e-3)
+__device__ __forceinline__ float cabs_fast(float2 x) { return __builtin_amdgcn_sqrtf(x.x * x.x + x.y * x.y); }
+
 // real-FFT untangling of the packed 320-point transform Z of one frame: X[k] and X[320 - k]
 __device__ __forceinline__ void untangle(const float2* __restrict__ zf, int k, const float2* __restrict__ twl, float2& X,
                                          float2& Xm) {
@@ -230,8 +234,8 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec640(SpecArgs a, in
                 const float2* zf = zbuf + f * ZS;
                 float2 X, Xm;
                 untangle(zf, k, twl, X, Xm);
-                mk[j] = sqrtf(X.x * X.x + X.y * X.y);
-                mm[j] = sqrtf(Xm.x * Xm.x + Xm.y * Xm.y);
+                mk[j] = cabs_fast(X);
+                mm[j] = cabs_fast(Xm);
                 float2* o = reinterpret_cast<float2*>(a.stft_ri) + (long long)u * 321 * T + t0 + f;
                 o[(long long)k * T] = X;
                 if (k != 160) o[(long long)(320 - k) * T] = Xm;
@@ -265,8 +269,8 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec640(SpecArgs a, in
                 const int f = it / 161, k = it - 161 * f;
                 float2 X, Xm;
                 untangle(zw + f * ZS, k, twl, X, Xm);
-                mk[j] = sqrtf(X.x * X.x + X.y * X.y);
-                mm[j] = sqrtf(Xm.x * Xm.x + Xm.y * Xm.y);
+                mk[j] = cabs_fast(X);
+                mm[j] = cabs_fast(Xm);
             }
             wave_lds_sync();
 #pragma unroll
