@@ -144,20 +144,19 @@ __global__ __launch_bounds__(512, 1) void k_conv_v1r(HaloArgs a) {
             for (int e = 0; e < PPL; ++e) {
                 const int P = L + 256 * e;
                 if (P >= HPIX) continue;
-                const float rs = 1.f / ps[Q][e];
+                // v_rcp_f32 (1 ulp) and packed conversions: the loader shares its SIMD's issue with the MFMA wave
+                const float rs = __builtin_amdgcn_rcpf(ps[Q][e]);
                 float f[NF] = {v4[Q][e][0], v4[Q][e][1], v4[Q][e][2], v4[Q][e][3], v1[Q][e]};
-                unsigned short h[6];
 #pragma unroll
                 for (int i = 0; i < NF; ++i) {
                     const float n = norm ? (f[i] - pm[Q][e]) * rs : f[i];
-                    h[i] = __builtin_bit_cast(unsigned short, (bf16_t)(pok[Q][e] ? n : 0.f));
+                    f[i] = pok[Q][e] ? n : 0.f;
                 }
-                h[5] = 0;
                 const int wy = P / HW, wx = P - wy * HW;
                 unsigned* d = reinterpret_cast<unsigned*>(halo + hs * HSLOT + (wy * HWP + wx) * PB);
-                d[0] = h[0] | ((unsigned)h[1] << 16);
-                d[1] = h[2] | ((unsigned)h[3] << 16);
-                d[2] = h[4];
+                d[0] = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){f[0], f[1]}, bf16x2));
+                d[1] = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){f[2], f[3]}, bf16x2));
+                d[2] = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){f[4], 0.f}, bf16x2));
             }
         };
         // output pass of tile k: BN (|scale|, shift) + LeakyReLU(0.3) on the pooled raw maxima the compute
