@@ -18,16 +18,17 @@ int ensure_lds_attr(const void* fn, int bytes) {
 
 using namespace avse;
 
-template <int ABL, int BP = 1>
+// warm-up: 200 launches (~40 ms) — with 10 the clock was still settling through the whole list of variants
+template <int ABL, int BP = 1, int LAT = 6>
 float run(const HaloArgs& a, int reps) {
-    using G = StreamGeom<3, 16, 16, 1, 6, BP>;
+    using G = StreamGeom<3, 16, 16, 1, LAT, BP>;
     auto k = k_conv_stream<3, 16, 16, 1, true, G::LAT, ABL, BP>;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS + 1024);
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
     const int cob = a.Co / 128, gx = 256 / cob;
-    for (int r = 0; r < 10; ++r) hipLaunchKernelGGL(k, dim3(gx, cob), dim3(512), G::LDS + 1024, 0, a);
+    for (int r = 0; r < 200; ++r) hipLaunchKernelGGL(k, dim3(gx, cob), dim3(512), G::LDS + 1024, 0, a);
     (void)hipEventRecord(e0, 0);
     for (int r = 0; r < reps; ++r) hipLaunchKernelGGL(k, dim3(gx, cob), dim3(512), G::LDS + 1024, 0, a);
     (void)hipEventRecord(e1, 0);
@@ -76,9 +77,11 @@ int main() {
             std::printf("  %-30s %8.4f ms  %7.1f TF/s\n", name, ms, flop / (ms * 1e-3) / 1e12);
         };
         rep("full", run<0>(a, reps));
-        rep("full, barrier every step (BP 1)", run<0, 1>(a, reps));
+        rep("full, LAT 3 (again)", run<0, 1, 3>(a, reps));
+        rep("full, LAT 3", run<0, 1, 3>(a, reps));
         rep("full", run<0>(a, reps));
-        rep("full, barrier every step (BP 1)", run<0, 1>(a, reps));
+        rep("full, LAT 3 (again)", run<0, 1, 3>(a, reps));
+        rep("full, barrier period 2", run<0, 2>(a, reps));
         rep("no halo pieces (1)", run<1>(a, reps));
         rep("no weight streaming (2)", run<2>(a, reps));
         rep("no loads at all (3)", run<3>(a, reps));
