@@ -90,7 +90,8 @@ class Windows:
         if not ms:
             return None
         return {"steps_per_window": self.per, "n": len(ms), "min": round(min(ms), 4),
-                "median": round(statistics.median(ms), 4), "max": round(max(ms), 4)}
+                "median": round(statistics.median(ms), 4), "max": round(max(ms), 4),
+                "in_order": [round(x, 4) for x in ms]}
 
 
 def leg_stft(dev, reps=50, B=4096, sets=5):
