@@ -244,7 +244,9 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
         // land at pd_cur; pd_prev = where the pieces loaded during chunk g-1 land
         int k = 0, c = 0, g = 0, hs2 = 2;           // hs2 = halo slot of chunk g+2
         int woff = (WD % spt) * wslice;             // weights loaded by the next step: slice step + WD
-        int wrot = 0;                               // (first step of this chunk pair) % NWS
+        // (first step of this chunk pair) % NWS: constant 0 unless the pair length is not a multiple of the ring
+        constexpr bool kRot = PAIR % NWS != 0;
+        int wrot = 0;
         int vsel[HPW];
         __amdgpu_buffer_rsrc_t prs = cur_rs;
         int psoff = 0;
@@ -289,7 +291,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
             // 1. LDS stores of set S: weights of slice j+BP+1 (slot (j+BP+1) % NWS) and the piece loaded
             //    with them
             if constexpr (!(ABL & 2)) {
-                char* const wd = wdst + (((j + BP + 1) + wrot) & (NWS - 1)) * WSLOT;
+                char* const wd = wdst + (((j + BP + 1) + (kRot ? wrot : 0)) & (NWS - 1)) * WSLOT;
                 st16(wd, rw[S][0]);
                 st16(wd + 1024, rw[S][1]);
             }
@@ -324,7 +326,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
             [&]<int... J>(std::integer_sequence<int, J...>) {
                 (lstep(std::integral_constant<int, J>{}), ...);
             }(std::make_integer_sequence<int, PAIR>{});
-            wrot = (wrot + PAIR) & (NWS - 1);
+            if constexpr (kRot) wrot = (wrot + PAIR) & (NWS - 1);
         }
         wait_vm_lgkm0<0>();   // loads still in flight target registers and rows nobody reads
         if constexpr ((ABL & 128) != 0)
