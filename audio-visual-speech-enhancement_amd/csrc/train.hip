@@ -429,11 +429,112 @@ __global__ __launch_bounds__(256) void k_wgrad_na(WgArgs w) {
         }
 }
 
-__global__ void k_sum_splits(const float* __restrict__ part, int splits, long long n, float* __restrict__ out) {
-    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
-        float s = part[i];
-        for (int z = 1; z < splits; ++z) s += part[(long long)z * n + i];
-        out[i] = s;
+// All-taps narrow-A variant (A <= 8, 25 taps, H dense NHWC with B and its channel stride multiples of 4): one
+// block walks a row range ONCE for every tap, so the wide operand H (v_conv1's 128-channel dz, 134 MB at batch
+// 16) is read once instead of once per tap (k_wgrad_na reads it 25 times: ~1 ms per step).  The chunk's 8-channel
+// G rows are gathered per tap into LDS.  Thread = 7 taps (tap group tid / 64) x 4 a x 4 b: per row 8
+// ds_read_b128 for 112 FMAs (a 4 a x 1 b x 25 tap thread needed one broadcast read per 4 FMAs: LDS-bound).
+constexpr int NAT_TAPS = 25, NAT_TG = 7;   // taps, taps per group (4 groups, the last one 4 taps)
+__global__ __launch_bounds__(256) void k_wgrad_nat(WgArgs w) {
+    __shared__ float4 hs[32][33];                 // [row][b / 4] (+1 float4 pad)
+    __shared__ float4 gs[4 * NAT_TG][32][2];      // [tap][row][a / 4]
+    __shared__ int2 tl[NAT_TAPS];
+    const int tid = threadIdx.x, tg = tid >> 6, ag = (tid >> 5) & 1, bq = tid & 31;
+    const int b0 = blockIdx.x * 128;
+    const long long R = (long long)w.N * w.Hh * w.Wh;
+    const long long r0 = blockIdx.z * w.rows_per_split, r1 = min(R, r0 + w.rows_per_split);
+    if (tid < NAT_TAPS) tl[tid] = w.taps[tid];
+    float4 acc[NAT_TG][4];                        // [tap j][a] x 4 b
+#pragma unroll
+    for (int j = 0; j < NAT_TG; ++j)
+#pragma unroll
+        for (int a = 0; a < 4; ++a) acc[j][a] = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int hr = tid >> 5, hc = (tid & 31) * 4;   // H loader: rows hr + 8 q, columns b0 + hc .. +3
+    const int gr = tid >> 3, ga = tid & 7;          // G loader: row gr, channel ga, every tap
+    const bool hcol = b0 + hc < w.B;
+    __syncthreads();
+    for (long long rc = r0; rc < r1; rc += 32) {
+        float4 hv[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const long long r = rc + hr + 8 * q;
+            hv[q] = (r < r1 && hcol) ? *reinterpret_cast<const float4*>(w.H + r * w.hcs + b0 + hc)
+                                     : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        float gv[NAT_TAPS];
+        {
+            const long long r = rc + gr;
+            const bool ok = r < r1 && ga < w.A;
+            const long long rr = ok ? r : 0;
+            const int x = (int)(rr % w.Wh), y = (int)((rr / w.Wh) % w.Hh), n = (int)(rr / ((long long)w.Wh * w.Hh));
+            const float* gb = w.G + n * w.g_clip + ga;
+#pragma unroll
+            for (int t = 0; t < NAT_TAPS; ++t) {
+                const int2 tp = tl[t];
+                const int gy = y * w.sy + tp.x, gx = x * w.sx + tp.y;
+                gv[t] = (ok && gy >= 0 && gy < w.Hg && gx >= 0 && gx < w.Wg) ? gb[(long long)(gy * w.Wg + gx) * w.gcs] : 0.f;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 4; ++q) hs[hr + 8 * q][hc >> 2] = hv[q];
+#pragma unroll
+        for (int t = 0; t < NAT_TAPS; ++t) reinterpret_cast<float*>(&gs[t][gr][0])[ga] = gv[t];
+        __syncthreads();
+#pragma unroll 2
+        for (int k = 0; k < 32; ++k) {
+            const float4 h4 = hs[k][bq];
+#pragma unroll
+            for (int j = 0; j < NAT_TG; ++j) {
+                if (tg * NAT_TG + j >= NAT_TAPS) break;   // the last group's 3 missing taps (wave-uniform)
+                const float4 g4 = gs[tg * NAT_TG + j][k][ag];
+                const float gg[4] = {g4.x, g4.y, g4.z, g4.w};
+#pragma unroll
+                for (int a = 0; a < 4; ++a) {
+                    acc[j][a].x = fmaf(gg[a], h4.x, acc[j][a].x);
+                    acc[j][a].y = fmaf(gg[a], h4.y, acc[j][a].y);
+                    acc[j][a].z = fmaf(gg[a], h4.z, acc[j][a].z);
+                    acc[j][a].w = fmaf(gg[a], h4.w, acc[j][a].w);
+                }
+            }
+        }
+    }
+    const int b = b0 + 4 * bq;
+    if (b < w.B)
+#pragma unroll
+        for (int j = 0; j < NAT_TG; ++j) {
+            const int t = tg * NAT_TG + j;
+            if (t >= NAT_TAPS) break;
+            float* out = w.part + ((long long)blockIdx.z * NAT_TAPS + t) * w.A * w.B;
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+                if (4 * ag + a < w.A) *reinterpret_cast<float4*>(out + (long long)(4 * ag + a) * w.B + b) = acc[j][a];
+        }
+}
+
+// out[i] = sum over z of part[z][i], z in increasing order within each of the 4 waves' strided subsets (z = w mod 4),
+// then wave 0 + 1 + 2 + 3: deterministic.  One wave per z subset keeps 4x the loads in flight of a thread that
+// walks all splits (the all-taps wgrad writes ~500 splits of 16,000 floats)
+__global__ __launch_bounds__(256) void k_sum_splits(const float* __restrict__ part, int splits, long long n,
+                                                    float* __restrict__ out) {
+    __shared__ float red[3][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (long long i0 = blockIdx.x * 64LL; i0 < n; i0 += gridDim.x * 64LL) {
+        const long long i = i0 + lane;
+        float s = 0.f;
+        if (i < n) {
+            int z = w;
+            for (; z + 12 < splits; z += 16) {   // four independent loads in flight
+                const float a = part[(long long)z * n + i], b = part[(long long)(z + 4) * n + i];
+                const float c = part[(long long)(z + 8) * n + i], d = part[(long long)(z + 12) * n + i];
+                s += a; s += b; s += c; s += d;
+            }
+            for (; z < splits; z += 4) s += part[(long long)z * n + i];
+        }
+        if (w) red[w - 1][lane] = s;
+        __syncthreads();
+        if (w == 0 && i < n) out[i] = ((s + red[0][lane]) + red[1][lane]) + red[2][lane];
+        __syncthreads();
     }
 }
 
@@ -718,11 +819,22 @@ int build_plan(avse_trainer* t, const float* host_blob) {
     return 0;
 }
 
-// wgrad work split over the reduction rows: ~2048 blocks in total, >= 256 rows per split
+// k_wgrad_nat applies: A <= 8, 5 x 5 taps, a conv whose H (dz on the conv grid) is dense with 4-aligned rows
+bool wg_all_taps(const TLayer& T) {
+    const LayerDef& L = T.L;
+    return L.kind == CONV && L.cin <= 8 && L.kh * L.kw == 25 && L.cout % 4 == 0 && T.zc % 4 == 0;
+}
+
+// wgrad work split over the reduction rows: ~2048 blocks in total, >= 256 rows per split (k_wgrad_nat: ~512
+// blocks of >= 256 rows, each covering every tap: its partials are 25 taps deep)
 long long wg_splits(const TLayer& T, int64_t N) {
     const LayerDef& L = T.L;
     const int A = (L.kind == DECONV) ? L.cout : L.cin, B = (L.kind == DECONV) ? L.cin : L.cout;
     const long long R = N * (long long)((L.kind == DECONV) ? L.hin * L.win : T.hq * T.wq);
+    if (wg_all_taps(T)) {
+        const long long bt = (B + 127) / 128;
+        return std::max(1LL, std::min((512 + bt - 1) / bt, (R + 255) / 256));
+    }
     const long long tiles = (A <= 8 ? (long long)((B + 127) / 128) : (long long)((A + 63) / 64) * ((B + 63) / 64)) * L.kh * L.kw;
     return std::max(1LL, std::min((2048 + tiles - 1) / tiles, (R + 255) / 256));
 }
@@ -920,12 +1032,15 @@ int wgrad(avse_trainer* t, const TLayer& T, const float* dz, int64_t N, hipStrea
     w.rows_per_split = ((R + splits - 1) / splits + 31) / 32 * 32;
     splits = (R + w.rows_per_split - 1) / w.rows_per_split;
     w.part = t->wpart;
-    if (w.A <= 8)
+    if (wg_all_taps(T))
+        hipLaunchKernelGGL(k_wgrad_nat, dim3((unsigned)((w.B + 127) / 128), 1, (unsigned)splits), dim3(256), 0, s, w);
+    else if (w.A <= 8)
         hipLaunchKernelGGL(k_wgrad_na, dim3((unsigned)((w.B + 127) / 128), (unsigned)w.ntaps, (unsigned)splits), dim3(256), 0, s, w);
     else
         hipLaunchKernelGGL(k_wgrad, dim3((unsigned)(tiles / w.ntaps), (unsigned)w.ntaps, (unsigned)splits), dim3(256), 0, s, w);
     AVSE_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(k_sum_splits, dim3(grid_for(per)), dim3(256), 0, s, (const float*)t->wpart, (int)splits, per, t->Gr + T.o_k);
+    hipLaunchKernelGGL(k_sum_splits, dim3((unsigned)std::min<long long>((per + 63) / 64, 8192)), dim3(256), 0, s,
+                       (const float*)t->wpart, (int)splits, per, t->Gr + T.o_k);
     AVSE_HIP_CHECK(hipGetLastError());
     return 0;
 }
