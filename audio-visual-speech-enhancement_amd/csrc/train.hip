@@ -307,6 +307,16 @@ struct WgArgs {
     float* part;             // [splits][ntaps][A][B]
 };
 
+// row r of the reduction -> (n, y, x) on an Hh x Wh grid in 32-bit arithmetic (R < 2^31: host-checked); the
+// 64-bit div / mod sequences it replaces were ~a third of k_wgrad's instructions
+__device__ __forceinline__ void row_nyx(long long r, int Hh, int Wh, int& n, int& y, int& x) {
+    const int ri = (int)r, hw = Hh * Wh;
+    n = ri / hw;
+    const int rem = ri - n * hw;
+    y = rem / Wh;
+    x = rem - y * Wh;
+}
+
 __global__ __launch_bounds__(256) void k_wgrad(WgArgs w) {
     __shared__ float gs[16][68], hs[16][68];
     const int tid = threadIdx.x, ta = tid >> 4, tb = tid & 15;
@@ -322,7 +332,8 @@ __global__ __launch_bounds__(256) void k_wgrad(WgArgs w) {
         const long long r = rc + lr;
         float4 gv = make_float4(0.f, 0.f, 0.f, 0.f), hv = gv;
         if (r < r1) {
-            const int x = (int)(r % w.Wh), y = (int)((r / w.Wh) % w.Hh), n = (int)(r / ((long long)w.Wh * w.Hh));
+            int n, y, x;
+            row_nyx(r, w.Hh, w.Wh, n, y, x);
             const float* hp = w.H + n * w.h_clip + (long long)(y * w.Wh + x) * w.hcs + b0 + lc;
             if (b0 + lc + 3 < w.B) hv = make_float4(hp[0], hp[1], hp[2], hp[3]);
             else {
@@ -386,7 +397,8 @@ __global__ __launch_bounds__(256) void k_wgrad_na(WgArgs w) {
             const long long r = rc + (tid >> 3);
             const int a = tid & 7;
             if (r < r1 && a < w.A) {
-                const int x = (int)(r % w.Wh), y = (int)((r / w.Wh) % w.Hh), n = (int)(r / ((long long)w.Wh * w.Hh));
+                int n, y, x;
+                row_nyx(r, w.Hh, w.Wh, n, y, x);
                 const int gy = y * w.sy + t.x, gx = x * w.sx + t.y;
                 if (gy >= 0 && gy < w.Hg && gx >= 0 && gx < w.Wg) gv = w.G[n * w.g_clip + (long long)(gy * w.Wg + gx) * w.gcs + a];
             }
@@ -394,7 +406,8 @@ __global__ __launch_bounds__(256) void k_wgrad_na(WgArgs w) {
         float hv[16];
         {   // H: row (tid / 128) + 2 q, channel b0 + tid % 128; (n, y, x) advanced by 2 rows per q (no divisions)
             const long long r = rc + (tid >> 7);
-            int x = (int)(r % w.Wh), y = (int)((r / w.Wh) % w.Hh), n = (int)(r / ((long long)w.Wh * w.Hh));
+            int n, y, x;
+            row_nyx(r, w.Hh, w.Wh, n, y, x);
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
                 hv[q] = 0.f;
@@ -466,7 +479,8 @@ __global__ __launch_bounds__(256) void k_wgrad_nat(WgArgs w) {
             const long long r = rc + gr;
             const bool ok = r < r1 && ga < w.A;
             const long long rr = ok ? r : 0;
-            const int x = (int)(rr % w.Wh), y = (int)((rr / w.Wh) % w.Hh), n = (int)(rr / ((long long)w.Wh * w.Hh));
+            int n, y, x;
+            row_nyx(rr, w.Hh, w.Wh, n, y, x);
             const float* gb = w.G + n * w.g_clip + ga;
 #pragma unroll
             for (int t = 0; t < NAT_TAPS; ++t) {
@@ -1025,6 +1039,7 @@ int wgrad(avse_trainer* t, const TLayer& T, const float* dz, int64_t N, hipStrea
         w.A = L.cin; w.B = L.cout;
     }
     const long long R = N * (long long)w.Hh * w.Wh;
+    if (R >= (1LL << 31)) return tfail(AVSE_ERR_UNSUPPORTED, "wgrad: batch x grid exceeds 2^31 rows");
     const long long tiles = (long long)((w.A + 63) / 64) * ((w.B + 63) / 64) * w.ntaps;
     long long splits = wg_splits(T, N);
     const long long per = (long long)w.ntaps * w.A * w.B;
