@@ -81,7 +81,7 @@ __device__ __forceinline__ f32x4 mfma(i32x4 a, i32x4 b, f32x4 c) {
 // STAMP (tools/aud_stamp.hip only; 0 in the library): thread 0 records s_memtime at the phase boundaries into
 // g_stamps[block][k] (k = 0 start, 1 im2col, 2 a_conv1, 3 a_conv2 prologue, 4 a_conv2 loop, 5 its epilogue, 6 a_conv3
 // loop, 7 its epilogue, 8 a_conv4, 9 a_conv5; 10 / 11 the end of the a_conv4 / a_conv5 slab loops)
-__device__ unsigned long long* g_stamps;
+[[maybe_unused]] __device__ unsigned long long* g_stamps;
 template <int STAMP = 0>
 __global__ __launch_bounds__(NT, 1) void k_aud_enc(AudEncArgs a) {
 #define STAMP_AT(k) \
@@ -99,7 +99,6 @@ __global__ __launch_bounds__(NT, 1) void k_aud_enc(AudEncArgs a) {
 
     // every layer's folded bias / BN -> LDS (read as f32x4 quads in the epilogues: lanes of a row group kg share
     // an address, so the reads broadcast)
-    const int mh = w >> 2, nq = w & 3;   // a_conv3: fragments 4 mh .. 4 mh + 3, channels 32 nq .. 32 nq + 31
     {
         constexpr int co[5] = {64, 64, 128, 128, 128};
 #pragma unroll

@@ -51,7 +51,7 @@ constexpr int NW = 8, NT = 64 * NW;                  // waves (two per SIMD), th
 // fragment slots per wave: slots 0..2 = fragments w, w + 8, w + 16 x all 64 channels; slot 3 = fragment 24 x channels
 // 16 w .. 16 w + 15 on waves 0..3 only (25 fragments x 4 channel blocks = 100 pairs: 13 / 12 per wave, 25 per SIMD,
 // where 8 waves x 4 full slots computed 128 pairs and dropped 28)
-constexpr int NF = 4, NFRAG = HW / 16, FX = 24;
+constexpr int NF = 4, FX = 24;
 constexpr int PXB = 1280;                            // d_deconv6 partials of fragment 24 (4 waves x 16 pixels, f32)
 // d_deconv4: taps t -> (dy, dx) = (1 - t / 4, 1 - t % 4); window pixel (y + dy + 2, x + dx + 2)
 constexpr int P4 = 14, ROWS4 = 43, S4 = 96, NPIX4 = ROWS4 * P4;   // 602 pixels, 96-B rows

@@ -199,9 +199,8 @@ __global__ void k_act_fwd(ActArgs a) {
     const int Ho = a.pool ? a.Hq / 2 : a.Hq, Wo = a.pool ? a.Wq / 2 : a.Wq;
     const long long total = (long long)a.N * Ho * Wo * a.C;
     for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
-        const int c = (int)(i % a.C);
-        const long long p = i / a.C;
-        const int ox = (int)(p % Wo), oy = (int)((p / Wo) % Ho), n = (int)(p / ((long long)Wo * Ho));
+        // 32-bit decomposition (every activation tensor < 2^31 elements: avse_trainer_create caps the batch)
+        const int ii = (int)i, c = ii % a.C, p = ii / a.C, ox = p % Wo, t2 = p / Wo, oy = t2 % Ho, n = t2 / Ho;
         float y, yh;
         if (a.pool) {
             y = -INFINITY;
@@ -224,9 +223,8 @@ __global__ void k_act_bwd(ActArgs a, const float* __restrict__ gout, long long g
     const int Ho = a.pool ? a.Hq / 2 : a.Hq, Wo = a.pool ? a.Wq / 2 : a.Wq;
     const long long total = (long long)a.N * Ho * Wo * a.C;
     for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
-        const int c = (int)(i % a.C);
-        const long long p = i / a.C;
-        const int ox = (int)(p % Wo), oy = (int)((p / Wo) % Ho), n = (int)(p / ((long long)Wo * Ho));
+        // 32-bit decomposition (every activation tensor < 2^31 elements: avse_trainer_create caps the batch)
+        const int ii = (int)i, c = ii % a.C, p = ii / a.C, ox = p % Wo, t2 = p / Wo, oy = t2 % Ho, n = t2 / Ho;
         const float g = gout[n * g_clip + (long long)(oy * Wo + ox) * g_pix + g_c + c] * drop_scale(a, i);
         if (a.pool) {
             float best = -INFINITY, bh = 0.f;
@@ -256,7 +254,7 @@ __global__ void k_bn_bwd(const float* __restrict__ z, float* __restrict__ g, lon
     const long long total = M * C;
     const float rM = 1.f / (float)M;
     for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
-        const int c = (int)(i % C);
+        const int c = (int)i % C;   // < 2^31 elements (trainer batch cap)
         const float xh = (z[i] - mean[c]) * inv[c];
         g[i] = gamma[c] * inv[c] * (g[i] - dbeta[c] * rM - xh * dgamma[c] * rM);
     }
@@ -1174,7 +1172,9 @@ extern "C" {
 int avse_trainer_create(avse_ctx* c, const float* host_blob, int64_t n_floats, int64_t max_batch, avse_trainer** out) {
     if (!c || !host_blob || !out) return tfail(AVSE_ERR_INVALID, "NULL argument");
     if (n_floats != blob_floats()) return tfail(AVSE_ERR_INVALID, "weight blob has the wrong size");
-    if (max_batch < 1 || max_batch > 4096) return tfail(AVSE_ERR_INVALID, "max_batch must be in [1, 4096]");
+    // <= 1023 keeps every activation tensor (v_conv1's pre-pool z: 128 x 128 x 128 per clip) below 2^31 elements,
+    // so the element-wise kernels index in 32 bits
+    if (max_batch < 1 || max_batch > 1023) return tfail(AVSE_ERR_INVALID, "max_batch must be in [1, 1023]");
     auto* t = new avse_trainer();
     t->device = ctx_device_index(c);
     t->max_n = max_batch;

@@ -186,7 +186,8 @@ enum avse_train_buffer { AVSE_TRAIN_PARAMS = 0, AVSE_TRAIN_GRADS = 1, AVSE_TRAIN
  * dz scratch */
 enum avse_train_flags { AVSE_TRAIN_GRADS_ONLY = 1, AVSE_TRAIN_DEBUG_STOP = 2, AVSE_TRAIN_DEBUG_GIN = 4 };
 
-/* host_blob: initial parameters (avse_weights_load layout); max_batch: largest N passed to avse_trainer_step. */
+/* host_blob: initial parameters (avse_weights_load layout); max_batch: largest N passed to avse_trainer_step,
+ * 1..1023 (activation tensors stay below 2^31 elements). */
 int avse_trainer_create(avse_ctx* ctx, const float* host_blob, int64_t n_floats, int64_t max_batch,
                         avse_trainer** out);
 void avse_trainer_destroy(avse_trainer* t);
