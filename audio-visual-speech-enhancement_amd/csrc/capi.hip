@@ -175,6 +175,7 @@ const OptionName kOptionNames[] = {
     {"unfused_tail", "AVSE_UNFUSED_TAIL", &Options::unfused_tail},
     {"no_halo", "AVSE_NO_HALO", &Options::no_halo},
     {"mfma32", "AVSE_MFMA32", &Options::mfma32},
+    {"tile_alt", "AVSE_TILE_ALT", &Options::tile_alt},
     {"serial", "AVSE_SERIAL", &Options::serial},
     {"aud_side", "AVSE_AUD_SIDE", &Options::aud_side},
     {"graph", "AVSE_GRAPH", &Options::graph},
@@ -1068,6 +1069,7 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
                 HaloArgs h = (i < 5) ? halo_args(G, vb(v_in[i]), vid, vm, vs, vb(v_in[i + 1]),
                                                  (long long)G.ho * G.wo * G.def.cout, G.def.cout, 0, n, opt)
                                      : halo_args(G, vb(v_in[i]), vid, vm, vs, cat, 5248, G.def.cout, 3200, n, opt);
+                h.rev = opt.tile_alt && (i == 1 || i == 3);   // v_conv1 / v_conv3 write their last tiles last
                 rc = G.halo == HALO_V1 ? launch_conv_v1r(h, s) : launch_conv_stream(h, s);
                 if (rc || (rc = mark())) return rc;
                 continue;
