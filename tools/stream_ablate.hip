@@ -20,7 +20,7 @@ int ensure_lds_attr(const void* fn, int bytes) {
 using namespace avse;
 
 template <int ABL, int LAT = 10, bool M16 = true, int BP = 1>
-float run(const HaloArgs& a, int reps) {
+float run(const HaloArgs& a, int reps, int gx = 256) {
     using G = StreamGeom<5, 16, 16, 1, LAT, BP>;
     (void)hipFuncSetAttribute((const void*)k_conv_stream<5, 16, 16, 1, M16, LAT, ABL, BP>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               G::LDS + 1024);
@@ -28,10 +28,10 @@ float run(const HaloArgs& a, int reps) {
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
     for (int r = 0; r < 10; ++r)   // warm-up long enough for the clock to settle under MFMA load
-        hipLaunchKernelGGL((k_conv_stream<5, 16, 16, 1, M16, LAT, ABL, BP>), dim3(256, 1), dim3(512), G::LDS + 1024, 0, a);
+        hipLaunchKernelGGL((k_conv_stream<5, 16, 16, 1, M16, LAT, ABL, BP>), dim3(gx, 1), dim3(512), G::LDS + 1024, 0, a);
     (void)hipEventRecord(e0, 0);
     for (int r = 0; r < reps; ++r)
-        hipLaunchKernelGGL((k_conv_stream<5, 16, 16, 1, M16, LAT, ABL, BP>), dim3(256, 1), dim3(512), G::LDS + 1024, 0, a);
+        hipLaunchKernelGGL((k_conv_stream<5, 16, 16, 1, M16, LAT, ABL, BP>), dim3(gx, 1), dim3(512), G::LDS + 1024, 0, a);
     (void)hipEventRecord(e1, 0);
     (void)hipEventSynchronize(e1);
     float ms = 0.f;
@@ -77,6 +77,10 @@ int main() {
     rep("full, 32x32x16 compute waves", run<0, 10, false>(a, reps));
     rep("MFMA only, 32x32x16 (15)", run<15, 10, false>(a, reps));
     rep("full", run<0, 10>(a, reps));
+    rep("full, 240 workgroups", run<0, 10>(a, reps, 240));
+    rep("full, 224 workgroups", run<0, 10>(a, reps, 224));
+    rep("full", run<0, 10>(a, reps));
+    rep("full, 240 workgroups", run<0, 10>(a, reps, 240));
     rep("full, barrier every step (BP 1)", run<0, 10, true, 1>(a, reps));
     rep("full", run<0, 10>(a, reps));
     rep("full, barrier every step (BP 1)", run<0, 10, true, 1>(a, reps));
