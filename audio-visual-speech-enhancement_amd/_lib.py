@@ -63,6 +63,23 @@ AVSE_TRAIN_PARAMS, AVSE_TRAIN_GRADS, AVSE_TRAIN_ADAM_M, AVSE_TRAIN_ADAM_V = 0, 1
 AVSE_TRAIN_GRADS_ONLY = 1
 
 
+def source_digest():
+    """sha256 (first 16 hex digits) of the sources libavse.so is built from: csrc/*.hip, csrc/*.h, csrc/Makefile and
+    include/avse.h.  Profiles record it (tools/pmc_summary.py) so that bench.py attaches rocprof counters only to the
+    tree they were measured on — the GPU box has no .git to name a commit."""
+    import glob
+    import hashlib
+    pkg = os.path.dirname(os.path.abspath(__file__))
+    files = sorted(glob.glob(os.path.join(pkg, "csrc", "*.hip")) + glob.glob(os.path.join(pkg, "csrc", "*.h")) +
+                   [os.path.join(pkg, "csrc", "Makefile"), HEADER_PATH])
+    h = hashlib.sha256()
+    for f in files:
+        h.update(os.path.basename(f).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 class AvseError(RuntimeError):
     """A libavse call returned a non-zero status."""
 

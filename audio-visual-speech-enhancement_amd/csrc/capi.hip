@@ -191,11 +191,13 @@ struct avse_weights {
     float* d6_w = nullptr;
     float d6_bias = 0.f;
     // avse_forward with video == NULL (all-zero video input, BASELINE configs[2]): the video encoder's output is
-    // then the same 2048-vector for every clip — computed once on first use and broadcast into the concat rows
-    mutable void* vzero_emb = nullptr;
+    // then the same 2048-vector for every clip — computed once on first use and broadcast into the concat rows.
+    // Published only after its stream has finished (another stream / thread may read it right away), under a lock.
+    mutable std::atomic<void*> vzero_emb{nullptr};
+    mutable std::mutex vzero_mu;
     std::vector<void*> allocs;
     ~avse_weights() {
-        (void)hipFree(vzero_emb);
+        (void)hipFree(vzero_emb.load());
         for (void* p : allocs) (void)hipFree(p);
     }
 };
@@ -1093,26 +1095,35 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
         // all-zero video: the embedding is one constant 2048-vector, computed once per weights object (clip 0 of an
         // N = 1 run whose activations use the N = 1 arena layout, stream-ordered before this forward's buffers)
         const size_t es = dt == AVSE_BF16 ? 2 : 4;
-        if (!W->vzero_emb) {
-            if (!c->zero_video) {
-                AVSE_HIP_CHECK(hipMalloc((void**)&c->zero_video, sizeof(float) * 128 * 128 * 5));
-                AVSE_HIP_CHECK(hipMemsetAsync(c->zero_video, 0, sizeof(float) * 128 * 128 * 5, s));
+        if (!W->vzero_emb.load(std::memory_order_acquire)) {
+            std::lock_guard<std::mutex> lk(W->vzero_mu);
+            if (!W->vzero_emb.load(std::memory_order_relaxed)) {
+                hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+                AVSE_HIP_CHECK(hipStreamIsCapturing(s, &cs));
+                if (cs != hipStreamCaptureStatusNone)
+                    return fail(AVSE_ERR_INVALID, "the all-zero-video embedding must be computed before graph capture");
+                if (!c->zero_video) {
+                    AVSE_HIP_CHECK(hipMalloc((void**)&c->zero_video, sizeof(float) * 128 * 128 * 5));
+                    AVSE_HIP_CHECK(hipMemsetAsync(c->zero_video, 0, sizeof(float) * 128 * 128 * 5, s));
+                }
+                void* emb = nullptr;
+                AVSE_HIP_CHECK(hipMalloc(&emb, 2048 * es));
+                size_t o1[B_COUNT + 1];
+                arena_bytes(1, dt, opt, o1);
+                hipEvent_t* keep = ev;
+                const int keep_stage = stage;
+                ev = nullptr;   // the one-off N = 1 encoder is not a profiled stage
+                rc = video_encoder(c->zero_video, nullptr, nullptr, 1, o1, c->arena + o1[B_CAT]);
+                ev = keep;
+                stage = keep_stage;
+                if (rc) { (void)hipFree(emb); return rc; }
+                AVSE_HIP_CHECK(hipMemcpyAsync(emb, c->arena + o1[B_CAT] + 3200 * es, 2048 * es, hipMemcpyDeviceToDevice, s));
+                // one-time: the embedding is complete before any stream can see the pointer
+                AVSE_HIP_CHECK(hipStreamSynchronize(s));
+                W->vzero_emb.store(emb, std::memory_order_release);
             }
-            void* emb = nullptr;
-            AVSE_HIP_CHECK(hipMalloc(&emb, 2048 * es));
-            size_t o1[B_COUNT + 1];
-            arena_bytes(1, dt, opt, o1);
-            hipEvent_t* keep = ev;
-            const int keep_stage = stage;
-            ev = nullptr;   // the one-off N = 1 encoder is not a profiled stage
-            rc = video_encoder(c->zero_video, nullptr, nullptr, 1, o1, c->arena + o1[B_CAT]);
-            ev = keep;
-            stage = keep_stage;
-            if (rc) { (void)hipFree(emb); return rc; }
-            AVSE_HIP_CHECK(hipMemcpyAsync(emb, c->arena + o1[B_CAT] + 3200 * es, 2048 * es, hipMemcpyDeviceToDevice, s));
-            W->vzero_emb = emb;
         }
-        if ((rc = launch_broadcast_row(W->vzero_emb, (char*)buf(B_CAT) + 3200 * es, N, 2048 * es, 5248 * es, s))) return rc;
+        if ((rc = launch_broadcast_row(W->vzero_emb.load(std::memory_order_acquire), (char*)buf(B_CAT) + 3200 * es, N, 2048 * es, 5248 * es, s))) return rc;
         for (int k = 0; k < 6; ++k)
             if ((rc = mark())) return rc;   // v_conv1..v_conv6 stages (the broadcast shows as v_conv1)
     }

@@ -32,9 +32,10 @@ class ReduceLROnPlateau:
             self.best, self.wait = current, 0
         else:
             if self.wait >= self.patience:
+                # keras/callbacks.py 2.0.x: the wait restarts only when the rate was actually reduced
                 if lr > self.min_lr + 1e-4 * self.min_lr:
                     lr = max(lr * self.factor, self.min_lr)
-                self.wait = 0
+                    self.wait = 0
             self.wait += 1
         return lr
 

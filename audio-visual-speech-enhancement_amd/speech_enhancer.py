@@ -55,20 +55,25 @@ def preprocess_video_sample(video_file_path, slice_duration_ms, mouth_height=128
     return np.stack(slices), fps
 
 
+def noise_at_snr(noise_signal, n_samples, speech_signal, snr_db=0):
+    """The noise of data_processor.py:124-130 as one array: the reference doubles the noise signal until it is at
+    least as long as the speech and truncates it, which is the noise repeated cyclically to n_samples (np.resize);
+    then the 0-dB SNR gain against the speech."""
+    looped = AudioSignal(np.resize(noise_signal.get_data(), (n_samples, noise_signal.get_number_of_channels())),
+                         noise_signal.get_sample_rate())
+    looped.amplify_by_factor(AudioMixer.snr_factor(speech_signal, looped, snr_db=snr_db))
+    return looped
+
+
 def preprocess_audio_pair(speech_file_path, noise_file_path, slice_duration_ms, n_video_slices, video_frame_rate):
-    """data_processor.py:119-139: tile + truncate the noise, 0 dB SNR, mix [1, 1], three spectrograms."""
-    speech_signal = AudioSignal.from_wav_file(speech_file_path)
-    noise_signal = AudioSignal.from_wav_file(noise_file_path)
-    while noise_signal.get_number_of_samples() < speech_signal.get_number_of_samples():
-        noise_signal = AudioSignal.concat([noise_signal, noise_signal])
-    noise_signal.truncate(speech_signal.get_number_of_samples())
-    factor = AudioMixer.snr_factor(speech_signal, noise_signal, snr_db=0)
-    noise_signal.amplify_by_factor(factor)
-    mixed_signal = AudioMixer.mix([speech_signal, noise_signal], mixing_weights=[1, 1])
-    mixed = data_processor.preprocess_audio_signal(mixed_signal, slice_duration_ms, n_video_slices, video_frame_rate)
-    speech = data_processor.preprocess_audio_signal(speech_signal, slice_duration_ms, n_video_slices, video_frame_rate)
-    noise = data_processor.preprocess_audio_signal(noise_signal, slice_duration_ms, n_video_slices, video_frame_rate)
-    return mixed, speech, noise, mixed_signal
+    """data_processor.py:119-139: (mixed, speech, noise) slice stacks and the mixed signal.  Each stack comes from
+    preprocess_audio_signal, which also pads / truncates its signal in place (the returned mixture is that one)."""
+    speech = AudioSignal.from_wav_file(speech_file_path)
+    noise = noise_at_snr(AudioSignal.from_wav_file(noise_file_path), speech.get_number_of_samples(), speech)
+    mixture = AudioMixer.mix([speech, noise], mixing_weights=[1, 1])
+    stacks = [data_processor.preprocess_audio_signal(sig, slice_duration_ms, n_video_slices, video_frame_rate)
+              for sig in (mixture, speech, noise)]
+    return stacks[0], stacks[1], stacks[2], mixture
 
 
 def preprocess_sample(speech_entry, noise_file_path, slice_duration_ms=200):
@@ -126,20 +131,17 @@ def load_preprocessed_blob(path):
 
 
 def load_preprocessed_blobs(paths, max_samples_per_blob=None):
-    out = []
-    for p in paths:
-        out += load_preprocessed_blob(p)[:max_samples_per_blob]
-    return out
+    return [smp for p in paths for smp in load_preprocessed_blob(p)[:max_samples_per_blob]]
 
 
 def make_sample_set(samples, max_samples=None):
-    n = len(samples) if max_samples is None else min(len(samples), max_samples)
-    samples = random.sample(samples, n)
-    video = np.concatenate([s.video_samples for s in samples], axis=0)
-    mixed = np.concatenate([s.mixed_spectrograms for s in samples], axis=0)
-    speech = np.concatenate([s.speech_spectrograms for s in samples], axis=0)
-    perm = np.random.permutation(video.shape[0])
-    return video[perm], mixed[perm], speech[perm]
+    """speech_enhancer.py:241-262: a random subset of the samples, their slices pooled and shuffled together ->
+    (video [S, H, W, F], mixed [S, 80, T], speech [S, 80, T])."""
+    chosen = random.sample(samples, len(samples) if max_samples is None else min(len(samples), max_samples))
+    fields = ("video_samples", "mixed_spectrograms", "speech_spectrograms")
+    pooled = [np.concatenate([getattr(smp, f) for smp in chosen], axis=0) for f in fields]
+    order = np.random.permutation(pooled[0].shape[0])
+    return tuple(a[order] for a in pooled)
 
 
 # ------------------------------------------------------------------------ subcommands

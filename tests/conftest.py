@@ -27,8 +27,10 @@ def has_gpu():
 
 @pytest.fixture(scope="session")
 def gpu():
+    # Only -m gpu tests request this fixture.  A GPU run on a box where torch sees no device must FAIL, not skip:
+    # an all-skipped `pytest -m gpu` would exit 0 without having run a single kernel.
     if not has_gpu():
-        pytest.skip("no ROCm GPU visible")
+        pytest.fail("no ROCm GPU visible to torch: the -m gpu tests cannot run here", pytrace=False)
     import torch
     return torch.device("cuda", 0)
 

@@ -22,6 +22,15 @@ def test_reduce_lr_on_plateau_keras_2_0_rule():
     cb = ReduceLROnPlateau(patience=0)
     assert cb.on_epoch_end(1.0, 1.0) == 1.0
     assert cb.on_epoch_end(1.0 - 5e-5, 1.0) == 0.5
+    # at min_lr the rate is not reduced and the wait is NOT restarted (keras/callbacks.py 2.0.x: `self.wait = 0` sits
+    # inside the `old_lr > min_lr + lr_epsilon` branch)
+    cb = ReduceLROnPlateau(factor=0.5, patience=2, min_lr=0.25)
+    lr, waits = 0.5, []
+    for v in [1.0] + [1.0] * 8:
+        lr = cb.on_epoch_end(v, lr)
+        waits.append(cb.wait)
+    assert lr == 0.25
+    assert waits == [0, 1, 2, 1, 2, 3, 4, 5, 6]
 
 
 def test_early_stopping_keras_2_0_rule():

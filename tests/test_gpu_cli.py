@@ -56,3 +56,25 @@ def test_cli_preprocess_train_predict(gpu, tmp_path):
     assert sr == 16000 and y.shape == (160 * (300 - 1),)
     for f in ("mixture.wav", "source.wav", "noise.wav"):
         assert os.path.exists(os.path.join(os.path.dirname(enhanced[0]), f))
+
+
+def test_cli_train_fits_checkpoints_and_predicts(gpu, tmp_path):
+    """speech_enhancer.py:31-58 without --init-only: sample sets from the preprocessed blobs, the normaliser fitted
+    and applied in place to the training AND validation video, the fit (checkpointed every epoch to the model file),
+    the final save — then predict runs on the trained model."""
+    from avse_amd.model import KerasModel
+    tmp = str(tmp_path)
+    ds, noise = make_dataset(tmp)
+    base = os.path.join(tmp, "base")
+    os.makedirs(base)
+    run(["-bd", base, "preprocess", "-dn", "d", "-ds", ds, "-n", noise], tmp)
+    out = run(["-bd", base, "train", "-mn", "m", "-tdn", "d", "-vdn", "d", "--epochs", "2", "--seed", "1"], tmp)
+    assert "epoch 2:" in out and "val_loss" in out
+    model_dir = os.path.join(base, "cache", "models", "m")
+    assert os.path.exists(os.path.join(model_dir, "normalization.npz"))
+    trained = KerasModel.load(os.path.join(model_dir, "model.safetensors"))
+    init = KerasModel.init(seed=1)
+    assert not np.array_equal(trained.to_blob(), init.to_blob())       # the fit moved the parameters
+    out = run(["-bd", base, "predict", "-mn", "m", "-dn", "d"], tmp)
+    assert "loss:" in out
+    assert len(glob.glob(os.path.join(base, "out", "m", "d", "*", "*", "*", "enhanced.wav"))) == 1

@@ -21,7 +21,8 @@ pytestmark = pytest.mark.gpu
 
 FP32_ABS = 1e-4     # north star: enhanced magnitude within 1e-4 RMS of the CPU reference
 FP32_REL = 1e-5
-BF16_REL = 3e-2
+BF16_REL = 5e-3     # ~2x the measured 2.3e-3 (N = 301 / 512, profiles/r02i_bench.json parity)
+BF16_LAYER_REL = 1.5e-2
 
 BUF_NAMES = ["video_in", "audio_in", "a_conv1", "a_conv2", "a_conv3", "a_conv4", "v_conv1", "v_conv2", "v_conv3",
              "v_conv4", "v_conv5", "concat", "enc_dense", "dec_dense1", "dec_dense2", "d_deconv1", "d_deconv2",
@@ -157,12 +158,13 @@ CHECKED = ["v_conv1", "v_conv2", "v_conv3", "v_conv4", "v_conv5", "concat", "enc
            "d_deconv3"]
 
 
-@pytest.mark.parametrize("N", [301, 512])
+@pytest.mark.parametrize("N", [301, 512, 1024])
 def test_bf16_bench_batch_matches_oracle(gpu, N):
-    """The launch bench.py times (BASELINE configs[3]: bf16, 512 clips, its inputs and normaliser), and N=301
-    (k_gemm's v_conv6 at ksplit == 1 with a ragged 64-row last tile; v_conv5's 4-clip tiles ragged): the output
-    and every materialised layer of 24 spread clips against the float64 oracle, the mel input against the
-    librosa restatement."""
+    """The launch bench.py times (BASELINE configs[3]: bf16, 512 clips, its inputs and normaliser), N=1024 (the
+    forward launch of configs[4]'s end-to-end run, pipeline.Enhancer chunk 1024: 4 v_conv1 / stream-conv tiles per
+    persistent workgroup more than at 512) and N=301 (k_gemm's v_conv6 at ksplit == 1 with a ragged 64-row last
+    tile; v_conv5's 4-clip tiles ragged): the output and every materialised layer of 24 spread clips against the
+    float64 oracle, the mel input against the librosa restatement."""
     import bench
     from avse_amd import ops
     from avse_amd.model import KerasModel
@@ -189,7 +191,7 @@ def test_bf16_bench_batch_matches_oracle(gpu, N):
     assert np.isfinite(out).all()
     assert err <= BF16_REL, (err, layers)
     for k, e in layers.items():
-        assert e <= 1.5e-2, (k, e)
+        assert e <= BF16_LAYER_REL, (k, e)
 
 
 @pytest.mark.parametrize("N", [1, 5])
@@ -213,8 +215,8 @@ def test_bf16_halo_video_convs_match_generic_kernel(gpu, N):
     out_g = ops.forward(dw_g, *args).cpu().numpy()
     sc_g = scratch(dw_g, N)
     for k in ["v_conv1", "v_conv2", "v_conv3", "v_conv4", "v_conv5"]:
-        assert rel_rms(sc_h[k], inter[k]) <= 1.5e-2, (k, rel_rms(sc_h[k], inter[k]))
-        assert rel_rms(sc_h[k], sc_g[k]) <= 1.5e-2, (k, rel_rms(sc_h[k], sc_g[k]))
+        assert rel_rms(sc_h[k], inter[k]) <= BF16_LAYER_REL, (k, rel_rms(sc_h[k], inter[k]))
+        assert rel_rms(sc_h[k], sc_g[k]) <= BF16_LAYER_REL, (k, rel_rms(sc_h[k], sc_g[k]))
     assert rel_rms(out_h, ref) <= BF16_REL
     assert rel_rms(out_h, out_g) <= BF16_REL
 
@@ -311,7 +313,7 @@ def test_bf16_mfma32_variant_agrees(gpu):
         out_b = ops.forward(dw, *args).cpu().numpy()
         sc_b = scratch(dw, N)
     for k in ["v_conv1", "v_conv2", "v_conv3", "v_conv4", "v_conv5"]:
-        assert rel_rms(sc_a[k], inter[k]) <= 1.5e-2, (k, rel_rms(sc_a[k], inter[k]))
+        assert rel_rms(sc_a[k], inter[k]) <= BF16_LAYER_REL, (k, rel_rms(sc_a[k], inter[k]))
         assert rel_rms(sc_a[k], sc_b[k]) <= 1e-2, (k, rel_rms(sc_a[k], sc_b[k]))
     assert rel_rms(out_a, out_b) <= 1e-2
 

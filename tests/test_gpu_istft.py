@@ -51,6 +51,30 @@ def test_batched_istft_matches_oracle(gpu):
         assert rel_rms(y[u], ref) < 1e-4, (u, rel_rms(y[u], ref))
 
 
+def test_fused_istft_at_e2e_size_matches_oracle(gpu):
+    """The ISTFT launch of BASELINE configs[4] (bench.py --e2e): 667 3-s utterances (10,005 clips) in ONE avse_istft
+    call — every persistent block walks many output chunks — each utterance against the oracle's
+    reconstruct_speech_signal.  The input is a perturbed copy of the mixture's own slices (a network-like
+    prediction), so amplitudes span the whole dB range."""
+    from avse_amd import ops
+    U = 667
+    rng = np.random.default_rng(667)
+    x = synth_audio(rng, U, 48000)
+    xt = torch.from_numpy(x).to(gpu)
+    mel, D = ops.spectrogram(xt, frames_per_slice=20, return_stft=True)     # [667, 15, 80, 20], [667, 321, 301]
+    pred = mel + torch.from_numpy(rng.normal(0, 1.0, tuple(mel.shape)).astype(np.float32)).to(gpu)
+    y = ops.istft(pred, D).cpu().numpy()
+    assert y.shape == (U, 47840)
+    assert np.isfinite(y).all()
+    pred_np = pred.cpu().numpy()
+    worst = 0.0
+    for u in range(U):
+        ref = R.reconstruct_speech_signal(x[u], 16000, pred_np[u], 25.0)
+        worst = max(worst, rel_rms(y[u], ref))
+    print(f"ISTFT 667 utterances: worst waveform rel RMS {worst:.3e}")
+    assert worst < 1e-4, worst
+
+
 def test_reconstruct_signal_from_spectrogram_api(gpu):
     from avse_amd import data_processor as dp
     from avse_amd.audio_io import AudioSignal

@@ -110,7 +110,21 @@ def main():
                     e["mfma_busy_frac"] = round(busy / (1024 * gui / 8), 4)
                     e["eff_clock_ghz"] = round(gui / 8 / dur, 3) if dur else None
             e["dispatches"] = len(fetch.get(lab, []))
-    res = {"tag": tag, "batch": 512, "source": "rocprofv3 --pmc passes FETCH_SIZE | WRITE_SIZE | "
+    # rocprofv3 --kernel-trace --stats averages of the same tree (the bench's HIP-event figure is a separate run)
+    stats_avg_ms = {}
+    if stats:
+        for r in csv.DictReader(open(stats[0])):
+            k = short(r["Name"])
+            for prefix, labels in LABELS:
+                if k.startswith(prefix) and len(labels) == 1:
+                    stats_avg_ms[labels[0]] = round(float(r["AverageNs"]) / 1e6, 5)
+                    break
+    sys.path.insert(0, ROOT)
+    import avse_pkg
+    avse_pkg.load()
+    from avse_amd import _lib
+    res = {"tag": tag, "batch": 512, "source_digest": _lib.source_digest(),
+           "kernel_stats_avg_ms": stats_avg_ms, "source": "rocprofv3 --pmc passes FETCH_SIZE | WRITE_SIZE | "
            "SQ_VALU_MFMA_BUSY_CYCLES+GRBM_GUI_ACTIVE over tools/fwd_loop.py (B=512 bf16 spectrogram + forward) and "
            "FETCH_SIZE | WRITE_SIZE over AVSE_MODE=stft (B=4096, 5 rotated buffer sets)", "kernels": kern}
     with open(os.path.join(prof, f"{tag}_pmc.json"), "w") as fh:
