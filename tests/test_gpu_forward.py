@@ -21,7 +21,8 @@ pytestmark = pytest.mark.gpu
 
 FP32_ABS = 1e-4     # north star: enhanced magnitude within 1e-4 RMS of the CPU reference
 FP32_REL = 1e-5
-BF16_REL = 5e-3     # ~2x the measured 2.3e-3 (N = 301 / 512, profiles/r02i_bench.json parity)
+BF16_REL_BENCH = 5e-3   # the benchmarked launches (N = 301 / 512 / 1024): ~2x the measured 2.3e-3 (bench parity field)
+BF16_REL = 1.5e-2       # few-clip launches (N = 1..130): ~1.6x the worst measured, 9.3e-3 at N = 3 (profiles/r03a_gputest.log)
 BF16_LAYER_REL = 1.5e-2
 
 BUF_NAMES = ["video_in", "audio_in", "a_conv1", "a_conv2", "a_conv3", "a_conv4", "v_conv1", "v_conv2", "v_conv3",
@@ -189,7 +190,7 @@ def test_bf16_bench_batch_matches_oracle(gpu, N):
     layers = {k: rel_rms(sc[k], inter[k]) for k in CHECKED}
     print(f"bf16 N={N}: output rel RMS {err:.3e}; per layer {layers}")
     assert np.isfinite(out).all()
-    assert err <= BF16_REL, (err, layers)
+    assert err <= BF16_REL_BENCH, (err, layers)
     for k, e in layers.items():
         assert e <= BF16_LAYER_REL, (k, e)
 
