@@ -165,13 +165,19 @@ __global__ __launch_bounds__(512, 1) void k_conv_v1r(HaloArgs a) {
         const int c4 = (L & 31) * 4;
         float osc[4], osh[4];
         const int Wp = a.Wc / 2;
+        // store offsets: a lane-constant VGPR part (pixel column L >> 5, channels c4) and a wave-uniform part per
+        // tile and row, passed as the store's soffset.  (A per-tile 32-bit VGPR product here was emitted as
+        // v_mad_u64_u32 whose undefined high addend half reused a window-load destination register, so the
+        // compiler's waitcnt pass drained every window load in flight at each output pass.)
+        const int ovlane = ((L >> 5) * a.out_pix_stride + a.out_c_off + c4) * 2;
+        const int orow = Wp * a.out_pix_stride * 2;
         auto out_pass = [&](int k) {
             int clip, oy0, ox0;
             tile_origin(k, clip, oy0, ox0);
             const long long cb = a.out_clip_stride * 2;
             const __amdgpu_buffer_rsrc_t ors = make_rsrc(reinterpret_cast<const char*>(a.out) + (long long)clip * cb, cb);
             const char* sbase = stg + (k & 1) * STG + (L >> 5) * SPITCH + c4 * 4;
-            const int obase = ((oy0 >> 1) * Wp + (ox0 >> 1) + (L >> 5)) * a.out_pix_stride + a.out_c_off + c4;
+            const int otile = __builtin_amdgcn_readfirstlane(((oy0 >> 1) * Wp + (ox0 >> 1)) * a.out_pix_stride * 2);
 #pragma unroll
             for (int r = 0; r < 8; ++r) {   // pooled pixel (r, L >> 5) of the 8 x 8 tile
                 const f32x4 m = *reinterpret_cast<const f32x4*>(sbase + 8 * r * SPITCH);
@@ -184,7 +190,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_v1r(HaloArgs a) {
                 const bf16x2 lo = __builtin_convertvector((f32x2){v[0], v[1]}, bf16x2);
                 const bf16x2 hi = __builtin_convertvector((f32x2){v[2], v[3]}, bf16x2);
                 const i32x2 o = {__builtin_bit_cast(int, lo), __builtin_bit_cast(int, hi)};
-                __builtin_amdgcn_raw_buffer_store_b64(o, ors, (obase + r * Wp * a.out_pix_stride) * 2, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b64(o, ors, ovlane, otile + r * orow, 0);
             }
         };
         using Q0 = std::integral_constant<int, 0>;
@@ -212,13 +218,9 @@ __global__ __launch_bounds__(512, 1) void k_conv_v1r(HaloArgs a) {
             const bool out = k >= 1 && !(ABL & 1);
             if (out) out_pass(k - 1);
             if (k + 2 < nmine && !(ABL & 2)) {
-                // younger than window k+2's loads: tile k-1's stores (k >= 2), window k+3's loads (issued
-                // one iteration later, k+3 < nmine) and this iteration's stores
-                const int n = ((k >= 2 && !(ABL & 1)) ? 8 : 0) + (k + 3 < nmine ? 8 : 0) + (out ? 8 : 0);
-                if (n >= 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
-                else if (n >= 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-                else if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                // no hand-counted vmcnt here: the window registers are ordinary results of the buffer-load
+                // builtins, so the compiler's waitcnt pass waits for exactly the loads each store reads (with
+                // the stores and window k+3's loads issued after them still in flight; DESIGN.md §3 v_conv1)
                 win_store(set, (k + 2) % NWS);     // slot of window k-1, last read during tile k-1
                 if (k + 4 < nmine) win_load(set, k + 4);
             }
