@@ -44,6 +44,9 @@ SIGNATURES = {
                           _c_void_p, _c_void_p]),
     "avse_weights_blob_floats": (_i64, []),
     "avse_weights_load": (_int, [_c_void_p, _c_void_p, _i64, _int, ctypes.POINTER(_c_void_p)]),
+    "avse_weights_blob_floats_shape": (_i64, [_int, _int]),
+    "avse_weights_load_shape": (_int, [_c_void_p, _c_void_p, _i64, _int, _int, _int, ctypes.POINTER(_c_void_p)]),
+    "avse_weights_shape": (_int, [_c_void_p, ctypes.POINTER(_int), ctypes.POINTER(_int)]),
     "avse_weights_destroy": (None, [_c_void_p]),
     "avse_forward": (_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _c_void_p,
                             _c_void_p]),
@@ -53,6 +56,7 @@ SIGNATURES = {
                                     _c_void_p, _c_void_p, ctypes.POINTER(_flt)]),
     "avse_debug_scratch": (_int, [_c_void_p, _i64, _int, ctypes.POINTER(_c_void_p), ctypes.POINTER(_i64)]),
     "avse_trainer_create": (_int, [_c_void_p, _c_void_p, _i64, _i64, ctypes.POINTER(_c_void_p)]),
+    "avse_trainer_create_shape": (_int, [_c_void_p, _c_void_p, _i64, _i64, _int, _int, ctypes.POINTER(_c_void_p)]),
     "avse_trainer_destroy": (None, [_c_void_p]),
     "avse_trainer_step": (_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _flt, _flt,
                                  ctypes.c_uint32, _int, _c_void_p, _c_void_p]),

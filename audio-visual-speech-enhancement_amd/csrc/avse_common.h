@@ -253,8 +253,8 @@ struct HaloArgs {
 int launch_conv_stream(const HaloArgs& a, hipStream_t s);   // conv_stream.hip (non-V1 variants)
 int launch_conv_v1r(const HaloArgs& a, hipStream_t s);      // conv_v1r.hip (v_conv1, kernel-row runs)
 int launch_video_prep(const float* video, const float* mean, const float* stdv, void* out, int64_t N,
-                      int dtype, hipStream_t s);
-int launch_audio_prep(const float* audio, void* out, int64_t N, int dtype, hipStream_t s);
+                      int F, int dtype, hipStream_t s);
+int launch_audio_prep(const float* audio, void* out, int64_t npix, int dtype, hipStream_t s);
 int launch_out_conv(const void* in, const float* w64, float bias, float* out, int64_t npix, int dtype,
                     hipStream_t s);
 int launch_broadcast_row(const void* src, void* dst, int64_t rows, int64_t row_bytes, int64_t stride_bytes,

@@ -122,10 +122,11 @@ struct avse_ctx {
     unsigned* umax = nullptr;
     int64_t umax_cap = 0;
     float* mse_partial = nullptr;
-    float* zero_video = nullptr;    // one all-zero [128][128][5] clip (video == NULL forwards)
+    float* zero_video = nullptr;    // one all-zero [128][128][8] clip (video == NULL forwards, any F <= 8)
     int* gemm_counters = nullptr;   // gemm.hip split-K tickets (zero between launches)
     char* arena = nullptr;
     size_t arena_bytes = 0;
+    NetPlan last_plan = kPlan25;    // the network shape of the last forward (avse_debug_scratch's arena layout)
     // side stream for the audio branch of the forward (runs concurrently with the video encoder)
     hipStream_t side = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
@@ -187,6 +188,7 @@ struct avse_weights {
     int dtype = 0;
     int device = 0;
     uint64_t serial = 0;                // unique per created weights object (graph-cache key: addresses get reused)
+    NetPlan plan = kPlan25;             // the network shape these weights were built for (netplan.h)
     GpuLayer layers[kNumLayers - 1];  // all but d_deconv6
     float* d6_w = nullptr;
     float d6_bias = 0.f;
@@ -222,10 +224,14 @@ struct Arena {
 };
 enum Buf { B_VIN, B_AIN, B_A1, B_A2, B_A3, B_A4, B_V1, B_V2, B_V3, B_V4, B_V5, B_CAT, B_E1, B_E2, B_E3,
            B_D1, B_D2, B_D3, B_D4, B_D5, B_COUNT };
-const size_t kBufElems[B_COUNT] = {128 * 128 * 8, 80 * 20 * 8, 40 * 10 * 64, 40 * 10 * 64, 20 * 5 * 128,
-                                   10 * 5 * 128, 64 * 64 * 128, 32 * 32 * 128, 16 * 16 * 256, 8 * 8 * 256,
-                                   4 * 4 * 512, 5248, 1312, 1312, 3200, 10 * 5 * 128, 20 * 5 * 128,
-                                   40 * 10 * 128, 40 * 10 * 64, 80 * 20 * 64};
+size_t buf_elems(const NetPlan& p, int b) {
+    const size_t T = p.T, w1 = (T + 1) / 2, w3 = p.W5;
+    const size_t e[B_COUNT] = {128 * 128 * 8, 80 * T * 8, 40 * w1 * 64, 40 * w1 * 64, 20 * w3 * 128,
+                               10 * w3 * 128, 64 * 64 * 128, 32 * 32 * 128, 16 * 16 * 256, 8 * 8 * 256,
+                               4 * 4 * 512, (size_t)p.cat, (size_t)p.emb, (size_t)p.emb, (size_t)p.aemb,
+                               10 * w3 * 128, 20 * w3 * 128, 40 * 2 * w3 * 128, 40 * 2 * w3 * 64, 80 * 4 * w3 * 64};
+    return e[b];
+}
 
 // Split-K plan for a single-phase GEMM of M rows x Co columns x kpad on k_conv: double the split while the
 // grid stays <= ~1024 workgroups and every split keeps >= 16 k-slabs (64-byte slabs).
@@ -239,8 +245,9 @@ int choose_ksplit(int64_t M, int Co, int kpad, int dtype) {
 }
 
 // fp32 partial-sum workspace needed by the split-K layers (enc/dec dense, v_conv6) at batch N
-size_t split_ws_bytes(int64_t N, int dtype, const Options& o) {
-    const struct { int64_t M; int Co, kpad; } g[4] = {{N, 1312, 5248}, {N, 1312, 1312}, {N, 3200, 1312}, {N * 16, 512, 4608}};
+size_t split_ws_bytes(int64_t N, int dtype, const Options& o, const NetPlan& p) {
+    const struct { int64_t M; int Co, kpad; } g[4] = {{N, p.emb, (p.cat + 31) / 32 * 32}, {N, p.emb, (p.emb + 31) / 32 * 32},
+                                                      {N, p.aemb, (p.emb + 31) / 32 * 32}, {N * 16, 512, 4608}};
     size_t mx = 0;
     for (const auto& x : g) {
         const int ks = choose_ksplit(x.M, x.Co, x.kpad, dtype);
@@ -253,20 +260,20 @@ size_t split_ws_bytes(int64_t N, int dtype, const Options& o) {
     return mx;
 }
 
-size_t arena_bytes(int64_t clips, int dtype, const Options& o, size_t* offs) {
+size_t arena_bytes(int64_t clips, int dtype, const Options& o, size_t* offs, const NetPlan& p) {
     const size_t es = dtype == AVSE_BF16 ? 2 : 4;
     size_t off = 0;
     for (int b = 0; b < B_COUNT; ++b) {
         if (offs) offs[b] = off;
-        off += (kBufElems[b] * es * (size_t)clips + 255) & ~(size_t)255;
+        off += (buf_elems(p, b) * es * (size_t)clips + 255) & ~(size_t)255;
     }
     if (offs) offs[B_COUNT] = off;   // split-K partials
-    off += (split_ws_bytes(clips, dtype, o) + 255) & ~(size_t)255;
+    off += (split_ws_bytes(clips, dtype, o, p) + 255) & ~(size_t)255;
     return off;
 }
 
-int ensure_arena(avse_ctx* c, int64_t clips, int dtype) {
-    const size_t need = arena_bytes(clips, dtype, c->opt, nullptr);
+int ensure_arena(avse_ctx* c, int64_t clips, int dtype, const NetPlan& p) {
+    const size_t need = arena_bytes(clips, dtype, c->opt, nullptr, p);
     if (need <= c->arena_bytes) return 0;
     if (c->arena) (void)hipFree(c->arena);
     c->arena = nullptr;
@@ -433,9 +440,10 @@ int ensure_istft_tables(avse_ctx* c, int sr, int n_fft, int n_mels, double fmin,
 }
 
 // Build phase/tap tables + packed [Cout][Kpad] weights for one layer.
-int build_layer(avse_weights* W, const LayerDef& L, const float* kernel, const float* bias, const float* bn,
+int build_layer(avse_weights* W, int li, const float* kernel, const float* bias, const float* bn,
                 const Options& opt) {
-    GpuLayer& G = W->layers[&L - kLayers];
+    const LayerDef& L = W->plan.L[li];
+    GpuLayer& G = W->layers[li];
     G.def = L;
     const int CHUNK_ELEMS = 8;   // channel padding so a 16-B chunk never straddles a tap (bf16: 8)
     G.cin_pad = (L.cin % CHUNK_ELEMS) ? ((L.cin + CHUNK_ELEMS - 1) / CHUNK_ELEMS) * CHUNK_ELEMS : L.cin;
@@ -559,7 +567,8 @@ int build_layer(avse_weights* W, const LayerDef& L, const float* kernel, const f
     // + tap; conv_v1r.hip (v_conv1) [kernel row][Cout][32].  Options::no_halo keeps the generic k_conv.
     if (W->dtype == AVSE_BF16 && L.kind == CONV && L.pool && L.hin >= 8 && !opt.no_halo) {
         const int ntap = L.kh * L.kw;
-        if (L.cin == 5) G.halo = HALO_V1;
+        if (L.cin == 5 && L.kh == 5) G.halo = HALO_V1;   // conv_v1r.hip: 5 frames (25 / 29.97 fps)
+        else if (L.cin % 128) G.halo = HALO_NONE;         // 6 frames (30 fps): generic k_conv
         else if (L.kh == 5) G.halo = HALO_K5;
         else if (L.hin >= 16) G.halo = HALO_K3_16;
         else G.halo = HALO_K3_8;
@@ -571,6 +580,7 @@ int build_layer(avse_weights* W, const LayerDef& L, const float* kernel, const f
             sgn[n] = scale[n] < 0.f ? -1.f : 1.f;
             scale_h[n] = std::fabs(scale[n]);
         }
+        if (G.halo == HALO_NONE) return 0;
         if ((rc = upload(W, scale_h, &G.scale_h))) return rc;
         std::vector<uint16_t> hp;
         if (G.halo == HALO_V1) {
@@ -803,7 +813,7 @@ int avse_ctx_get_option(avse_ctx* c, const char* name, int* value) {
 int avse_ctx_reserve(avse_ctx* c, int64_t max_clips, int dtype) {
     if (!c || max_clips < 0 || (dtype != AVSE_F32 && dtype != AVSE_BF16)) return fail(AVSE_ERR_INVALID, "bad reserve args");
     AVSE_HIP_CHECK(hipSetDevice(c->device));
-    return ensure_arena(c, max_clips, dtype);
+    return ensure_arena(c, max_clips, dtype, kPlan25);   // the 25-fps network's scratch (other shapes grow it on use)
 }
 
 int avse_spectrogram(avse_ctx* c, const float* sig, int64_t n_utt, int64_t n_samples, int sr, int n_fft, int hop,
@@ -898,23 +908,46 @@ int avse_istft(avse_ctx* c, const float* mel_db, const float* stft_ri, int64_t n
     return launch_istft(a, (hipStream_t)stream);
 }
 
-int64_t avse_weights_blob_floats(void) { return blob_floats(); }
+int64_t avse_weights_blob_floats(void) { return blob_floats(kPlan25); }
+
+int64_t avse_weights_blob_floats_shape(int spec_frames, int video_frames) {
+    if (!plan_valid(spec_frames, video_frames)) return -1;
+    return blob_floats(make_plan(spec_frames, video_frames));
+}
 
 int avse_weights_load(avse_ctx* c, const float* blob, int64_t n_floats, int dtype, avse_weights** out) {
+    return avse_weights_load_shape(c, blob, n_floats, dtype, kPlan25.T, kPlan25.F, out);
+}
+
+int avse_weights_shape(const avse_weights* w, int* spec_frames, int* video_frames) {
+    if (!w || !spec_frames || !video_frames) return fail(AVSE_ERR_INVALID, "NULL argument");
+    *spec_frames = w->plan.T;
+    *video_frames = w->plan.F;
+    return 0;
+}
+
+int avse_weights_load_shape(avse_ctx* c, const float* blob, int64_t n_floats, int dtype, int spec_frames,
+                            int video_frames, avse_weights** out) {
     if (!c || !blob || !out) return fail(AVSE_ERR_INVALID, "NULL argument");
     if (dtype != AVSE_F32 && dtype != AVSE_BF16) return fail(AVSE_ERR_INVALID, "bad compute dtype");
-    if (n_floats != blob_floats())
+    if (!plan_valid(spec_frames, video_frames))
+        return fail(AVSE_ERR_UNSUPPORTED, "network shape [80, " + std::to_string(spec_frames) + "] x [128, 128, " +
+                                              std::to_string(video_frames) + "]: the decoder reproduces 80 x T only for "
+                                              "T a multiple of 4; video frames must be 1..8");
+    const NetPlan plan = make_plan(spec_frames, video_frames);
+    if (n_floats != blob_floats(plan))
         return fail(AVSE_ERR_INVALID, "weight blob has " + std::to_string(n_floats) + " floats, expected " +
-                                          std::to_string(blob_floats()));
+                                          std::to_string(blob_floats(plan)));
     AVSE_HIP_CHECK(hipSetDevice(c->device));
     avse_weights* W = new avse_weights();
     static std::atomic<uint64_t> next_serial{1};
     W->serial = next_serial++;
     W->dtype = dtype;
     W->device = c->device;
+    W->plan = plan;
     const float* p = blob;
     for (int i = 0; i < kNumLayers; ++i) {
-        const LayerDef& L = kLayers[i];
+        const LayerDef& L = plan.L[i];
         const float* kernel = p;
         p += (size_t)L.kh * L.kw * L.cin * L.cout;
         const float* bias = p;
@@ -931,7 +964,7 @@ int avse_weights_load(avse_ctx* c, const float* blob, int64_t n_floats, int dtyp
             W->d6_bias = bias[0];
             continue;
         }
-        int rc = build_layer(W, L, kernel, bias, bn, c->opt);
+        int rc = build_layer(W, i, kernel, bias, bn, c->opt);
         if (rc) { delete W; return rc; }
     }
     *out = W;
@@ -957,11 +990,14 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
     if (N == 0) return 0;
     if (W->device != c->device) return fail(AVSE_ERR_INVALID, "weights and context are on different devices");
     AVSE_HIP_CHECK(hipSetDevice(c->device));
-    int rc = ensure_arena(c, N, W->dtype);
+    const NetPlan& P = W->plan;
+    int rc = ensure_arena(c, N, W->dtype, P);
     if (rc) return rc;
+    c->last_plan = P;
     const int dt = W->dtype;
     size_t off[B_COUNT + 1];
-    arena_bytes(N, dt, c->opt, off);
+    arena_bytes(N, dt, c->opt, off, P);
+    const long long CAT = P.cat, AEMB = P.aemb, EMB = P.emb;
     const Options& opt = c->opt;
     auto buf = [&](int b) { return (void*)(c->arena + off[b]); };
     // dense layers and v_conv6 on gemm.hip (bf16; Options::no_gemm keeps k_conv + split-K reduce)
@@ -1010,7 +1046,7 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
     if (dt == AVSE_BF16) {
         aa.mel = audio;
         aa.out = reinterpret_cast<bf16_t*>(buf(B_CAT));
-        aa.out_clip_stride = 5248;
+        aa.out_clip_stride = CAT;
         aa.N = (int)N;
         const void* ws[5] = {L(0).w_dense, L(1).w, L(2).w, L(3).w, L(4).w};
         const LayerDef* d = &L(0).def;
@@ -1049,13 +1085,13 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
         for (int k = 0; k < 6; ++k)
             if ((rc = mark())) return rc;   // audio_prep (= the fused kernel), a_conv1..a_conv5
     }
-    if (!aud_fused && ((rc = launch_audio_prep(audio, buf(B_AIN), N, dt, sa)) || (rc = mark()))) return rc;
+    if (!aud_fused && ((rc = launch_audio_prep(audio, buf(B_AIN), N * kMels * P.T, dt, sa)) || (rc = mark()))) return rc;
     const int a_in[5] = {B_AIN, B_A1, B_A2, B_A3, B_A4};
     for (int i = 0; i < 5 && !aud_fused; ++i) {
         const GpuLayer& G = L(i);
         const long long in_cs = (long long)G.def.hin * G.def.win * (i == 0 ? G.cin_pad : G.def.cin);
         ConvArgs a = (i < 4) ? conv_args(G, buf(a_in[i]), in_cs, buf(a_in[i + 1]), (long long)G.ho * G.wo * G.def.cout, G.def.cout, 0, N)
-                             : conv_args(G, buf(a_in[i]), in_cs, buf(B_CAT), 5248, G.def.cout, 0, N);   // Flatten -> concat[0:3200]
+                             : conv_args(G, buf(a_in[i]), in_cs, buf(B_CAT), CAT, G.def.cout, 0, N);   // Flatten -> concat[0:aemb]
         if ((rc = launch_conv(a, dt, sa)) || (rc = mark())) return rc;
     }
     if (concurrent) AVSE_HIP_CHECK(hipEventRecord(c->join, sa));
@@ -1064,13 +1100,13 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
                              void* cat) -> int {
         auto vb = [&](int b) { return (void*)(c->arena + o[b]); };
         const int v_in[6] = {B_VIN, B_V1, B_V2, B_V3, B_V4, B_V5};
-        if (L(5).halo == HALO_NONE && (rc = launch_video_prep(vid, vm, vs, vb(B_VIN), n, dt, s))) return rc;
+        if (L(5).halo == HALO_NONE && (rc = launch_video_prep(vid, vm, vs, vb(B_VIN), n, P.F, dt, s))) return rc;
         for (int i = 0; i < 6; ++i) {
             const GpuLayer& G = L(5 + i);
             if (G.halo != HALO_NONE) {
                 HaloArgs h = (i < 5) ? halo_args(G, vb(v_in[i]), vid, vm, vs, vb(v_in[i + 1]),
                                                  (long long)G.ho * G.wo * G.def.cout, G.def.cout, 0, n, opt)
-                                     : halo_args(G, vb(v_in[i]), vid, vm, vs, cat, 5248, G.def.cout, 3200, n, opt);
+                                     : halo_args(G, vb(v_in[i]), vid, vm, vs, cat, CAT, G.def.cout, AEMB, n, opt);
                 h.rev = opt.tile_alt && (i == 1 || i == 3);   // v_conv1 / v_conv3 write their last tiles last
                 rc = G.halo == HALO_V1 ? launch_conv_v1r(h, s) : launch_conv_stream(h, s);
                 if (rc || (rc = mark())) return rc;
@@ -1079,11 +1115,11 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
             const long long in_cs = (long long)G.def.hin * G.def.win * (i == 0 ? G.cin_pad : G.def.cin);
             if (i == 5 && use_gemm && G.def.hin == 4 && G.def.win == 4 && G.def.cin == 512 && G.def.kh == 3 && G.def.pool &&
                 G.ph[0].kpad == 9 * 512) {
-                if ((rc = gemm(G, vb(v_in[i]), in_cs, cat, 5248, 3200, 1, n)) || (rc = mark())) return rc;   // concat[3200:5248]
+                if ((rc = gemm(G, vb(v_in[i]), in_cs, cat, CAT, AEMB, 1, n)) || (rc = mark())) return rc;   // concat[aemb:]
                 continue;
             }
             ConvArgs a = (i < 5) ? conv_args(G, vb(v_in[i]), in_cs, vb(v_in[i + 1]), (long long)G.ho * G.wo * G.def.cout, G.def.cout, 0, n)
-                                 : conv_args(G, vb(v_in[i]), in_cs, cat, 5248, G.def.cout, 3200, n);  // concat[3200:5248]
+                                 : conv_args(G, vb(v_in[i]), in_cs, cat, CAT, G.def.cout, AEMB, n);  // concat[aemb:]
             if (i == 5) split(a);
             if ((rc = launch_conv(a, dt, s)) || (rc = mark())) return rc;
         }
@@ -1103,13 +1139,13 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
                 if (cs != hipStreamCaptureStatusNone)
                     return fail(AVSE_ERR_INVALID, "the all-zero-video embedding must be computed before graph capture");
                 if (!c->zero_video) {
-                    AVSE_HIP_CHECK(hipMalloc((void**)&c->zero_video, sizeof(float) * 128 * 128 * 5));
-                    AVSE_HIP_CHECK(hipMemsetAsync(c->zero_video, 0, sizeof(float) * 128 * 128 * 5, s));
+                    AVSE_HIP_CHECK(hipMalloc((void**)&c->zero_video, sizeof(float) * 128 * 128 * 8));
+                    AVSE_HIP_CHECK(hipMemsetAsync(c->zero_video, 0, sizeof(float) * 128 * 128 * 8, s));
                 }
                 void* emb = nullptr;
                 AVSE_HIP_CHECK(hipMalloc(&emb, 2048 * es));
                 size_t o1[B_COUNT + 1];
-                arena_bytes(1, dt, opt, o1);
+                arena_bytes(1, dt, opt, o1, P);
                 hipEvent_t* keep = ev;
                 const int keep_stage = stage;
                 ev = nullptr;   // the one-off N = 1 encoder is not a profiled stage
@@ -1117,30 +1153,30 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
                 ev = keep;
                 stage = keep_stage;
                 if (rc) { (void)hipFree(emb); return rc; }
-                AVSE_HIP_CHECK(hipMemcpyAsync(emb, c->arena + o1[B_CAT] + 3200 * es, 2048 * es, hipMemcpyDeviceToDevice, s));
+                AVSE_HIP_CHECK(hipMemcpyAsync(emb, c->arena + o1[B_CAT] + AEMB * es, 2048 * es, hipMemcpyDeviceToDevice, s));
                 // one-time: the embedding is complete before any stream can see the pointer
                 AVSE_HIP_CHECK(hipStreamSynchronize(s));
                 W->vzero_emb.store(emb, std::memory_order_release);
             }
         }
-        if ((rc = launch_broadcast_row(W->vzero_emb.load(std::memory_order_acquire), (char*)buf(B_CAT) + 3200 * es, N, 2048 * es, 5248 * es, s))) return rc;
+        if ((rc = launch_broadcast_row(W->vzero_emb.load(std::memory_order_acquire), (char*)buf(B_CAT) + AEMB * es, N, 2048 * es, CAT * es, s))) return rc;
         for (int k = 0; k < 6; ++k)
             if ((rc = mark())) return rc;   // v_conv1..v_conv6 stages (the broadcast shows as v_conv1)
     }
     if (concurrent) AVSE_HIP_CHECK(hipStreamWaitEvent(s, c->join, 0));
     // fusion + decoder dense (network.py:53-58, :66-78)
     if (use_gemm) {
-        if ((rc = gemm(L(11), buf(B_CAT), 5248, buf(B_E1), 1312, 0, 0, N)) || (rc = mark())) return rc;
-        if ((rc = gemm(L(12), buf(B_E1), 1312, buf(B_E2), 1312, 0, 0, N)) || (rc = mark())) return rc;
-        if ((rc = gemm(L(13), buf(B_E2), 1312, buf(B_E3), 3200, 0, 0, N)) || (rc = mark())) return rc;
+        if ((rc = gemm(L(11), buf(B_CAT), CAT, buf(B_E1), EMB, 0, 0, N)) || (rc = mark())) return rc;
+        if ((rc = gemm(L(12), buf(B_E1), EMB, buf(B_E2), EMB, 0, 0, N)) || (rc = mark())) return rc;
+        if ((rc = gemm(L(13), buf(B_E2), EMB, buf(B_E3), AEMB, 0, 0, N)) || (rc = mark())) return rc;
     } else {
-        ConvArgs a = conv_args(L(11), buf(B_CAT), 5248, buf(B_E1), 1312, 1312, 0, N);
+        ConvArgs a = conv_args(L(11), buf(B_CAT), CAT, buf(B_E1), EMB, EMB, 0, N);
         split(a);
         if ((rc = launch_conv(a, dt, s)) || (rc = mark())) return rc;
-        a = conv_args(L(12), buf(B_E1), 1312, buf(B_E2), 1312, 1312, 0, N);
+        a = conv_args(L(12), buf(B_E1), EMB, buf(B_E2), EMB, EMB, 0, N);
         split(a);
         if ((rc = launch_conv(a, dt, s)) || (rc = mark())) return rc;
-        a = conv_args(L(13), buf(B_E2), 1312, buf(B_E3), 3200, 3200, 0, N);
+        a = conv_args(L(13), buf(B_E2), EMB, buf(B_E3), AEMB, AEMB, 0, N);
         split(a);
         if ((rc = launch_conv(a, dt, s)) || (rc = mark())) return rc;
     }
@@ -1170,7 +1206,7 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
             DecHeadArgs ha;
             std::memset(&ha, 0, sizeof(ha));
             ha.in = reinterpret_cast<const bf16_t*>(buf(B_E3));
-            ha.in_clip_stride = 3200;
+            ha.in_clip_stride = AEMB;
             ha.out = reinterpret_cast<bf16_t*>(buf(B_D3));
             ha.out_clip_stride = 40 * 10 * 128;
             ha.N = (int)N;
@@ -1204,7 +1240,7 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
         if ((rc = launch_conv(a, dt, s)) || (rc = mark())) return rc;
     }
     if (opt.unfused_tail) {
-        if ((rc = launch_out_conv(buf(B_D5), W->d6_w, W->d6_bias, out, N * 80 * 20, dt, s)) || (rc = mark())) return rc;
+        if ((rc = launch_out_conv(buf(B_D5), W->d6_w, W->d6_bias, out, N * kMels * P.T, dt, s)) || (rc = mark())) return rc;
     } else if ((rc = mark())) {   // d_deconv6: fused into d_deconv5 above
         return rc;
     }
@@ -1227,7 +1263,7 @@ int avse_forward(avse_ctx* c, const avse_weights* W, const float* audio, const f
         return forward_impl(c, W, audio, video, vmean, vstd, N, out, (hipStream_t)stream, nullptr);
     AVSE_HIP_CHECK(hipSetDevice(c->device));
     if (W->device != c->device) return fail(AVSE_ERR_INVALID, "weights and context are on different devices");
-    int rc = ensure_arena(c, N, W->dtype);   // no allocation inside the capture
+    int rc = ensure_arena(c, N, W->dtype, W->plan);   // no allocation inside the capture
     if (rc) return rc;
     const void* key[8] = {(const void*)W->serial, audio, video, vmean, vstd, out, c->arena, (const void*)c->arena_bytes};
     avse_ctx::Graph* hit = nullptr;
@@ -1309,7 +1345,7 @@ int avse_mse(avse_ctx* c, const float* pred, const float* target, int64_t n, flo
 int avse_debug_scratch(avse_ctx* c, int64_t N, int dtype, void** base, int64_t* offsets) {
     if (!c || !base || !offsets || N <= 0) return fail(AVSE_ERR_INVALID, "bad debug_scratch args");
     size_t off[B_COUNT + 1];
-    const size_t need = arena_bytes(N, dtype, c->opt, off);
+    const size_t need = arena_bytes(N, dtype, c->opt, off, c->last_plan);
     if (!c->arena || need > c->arena_bytes) return fail(AVSE_ERR_INVALID, "no forward scratch of that size yet");
     *base = c->arena;
     for (int b = 0; b < B_COUNT; ++b) offsets[b] = (int64_t)off[b];

@@ -478,32 +478,30 @@ __global__ void k_splitk_reduce_tiles(ConvArgs a) {
     }
 }
 
-// video [N][128][128][5] f32 -> (x - mean) / std -> T [N][128][128][8] (channels 5..7 zero)
+// video [N][128][128][F] f32 -> (x - mean) / std -> T [N][128][128][8] (channels F..7 zero; F <= 8)
 template <typename T>
 __global__ void k_video_prep(const float* __restrict__ v, const float* __restrict__ mean, const float* __restrict__ stdv,
-                             T* __restrict__ out, long long npix) {
+                             T* __restrict__ out, long long npix, int F) {
     for (long long p = blockIdx.x * (long long)blockDim.x + threadIdx.x; p < npix; p += (long long)gridDim.x * blockDim.x) {
         const int hw = (int)(p % (128 * 128));
-        const float* src = v + p * 5;
+        const float* src = v + p * F;
         float m = 0.f, s = 1.f;
         const bool norm = mean != nullptr;
         if (norm) { m = mean[hw]; s = stdv[hw]; }
         T o[8];
 #pragma unroll
-        for (int c = 0; c < 5; ++c) {
-            float x = src[c];
-            if (norm) x = (x - m) / s;
+        for (int c = 0; c < 8; ++c) {
+            float x = c < F ? src[c] : 0.f;
+            if (norm && c < F) x = (x - m) / s;
             o[c] = from_f<T>(x);
         }
-#pragma unroll
-        for (int c = 5; c < 8; ++c) o[c] = from_f<T>(0.f);
         T* dst = out + p * 8;
 #pragma unroll
         for (int c = 0; c < 8; ++c) dst[c] = o[c];
     }
 }
 
-// audio [N][80][20] f32 -> T [N][80][20][8] (channel 0 = value, 1..7 zero)
+// audio [N][80][T] f32 -> T [N][80][T][8] (channel 0 = value, 1..7 zero)
 template <typename T>
 __global__ void k_audio_prep(const float* __restrict__ a, T* __restrict__ out, long long npix) {
     for (long long p = blockIdx.x * (long long)blockDim.x + threadIdx.x; p < npix; p += (long long)gridDim.x * blockDim.x) {
@@ -646,17 +644,17 @@ int launch_broadcast_row(const void* src, void* dst, int64_t rows, int64_t row_b
     return 0;
 }
 
-int launch_video_prep(const float* video, const float* mean, const float* stdv, void* out, int64_t N, int dtype,
+int launch_video_prep(const float* video, const float* mean, const float* stdv, void* out, int64_t N, int F, int dtype,
                       hipStream_t s) {
     const long long npix = (long long)N * 128 * 128;
-    if (dtype == 1) hipLaunchKernelGGL(k_video_prep<bf16_t>, dim3(grid_for(npix, 256)), dim3(256), 0, s, video, mean, stdv, (bf16_t*)out, npix);
-    else hipLaunchKernelGGL(k_video_prep<float>, dim3(grid_for(npix, 256)), dim3(256), 0, s, video, mean, stdv, (float*)out, npix);
+    if (F < 1 || F > 8) { set_error("video frames per slice must be 1..8"); return 1; }
+    if (dtype == 1) hipLaunchKernelGGL(k_video_prep<bf16_t>, dim3(grid_for(npix, 256)), dim3(256), 0, s, video, mean, stdv, (bf16_t*)out, npix, F);
+    else hipLaunchKernelGGL(k_video_prep<float>, dim3(grid_for(npix, 256)), dim3(256), 0, s, video, mean, stdv, (float*)out, npix, F);
     AVSE_HIP_CHECK(hipGetLastError());
     return 0;
 }
 
-int launch_audio_prep(const float* audio, void* out, int64_t N, int dtype, hipStream_t s) {
-    const long long npix = (long long)N * 80 * 20;
+int launch_audio_prep(const float* audio, void* out, int64_t npix, int dtype, hipStream_t s) {
     if (dtype == 1) hipLaunchKernelGGL(k_audio_prep<bf16_t>, dim3(grid_for(npix, 256)), dim3(256), 0, s, audio, (bf16_t*)out, npix);
     else hipLaunchKernelGGL(k_audio_prep<float>, dim3(grid_for(npix, 256)), dim3(256), 0, s, audio, (float*)out, npix);
     AVSE_HIP_CHECK(hipGetLastError());

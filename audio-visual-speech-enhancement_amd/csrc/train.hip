@@ -65,23 +65,22 @@ __global__ void k_gather(float* __restrict__ dst, const int* __restrict__ map, c
     }
 }
 
-// video [N][128][128][5] -> (x - mean) / std (VideoNormalizer, data_processor.py:208-212) -> [N][128][128][8]
+// video [N][128][128][F] -> (x - mean) / std (VideoNormalizer, data_processor.py:208-212) -> [N][128][128][8]
 __global__ void k_prep_video(const float* __restrict__ v, const float* __restrict__ mean, const float* __restrict__ stdv,
-                             float* __restrict__ out, long long npix, int hw) {
+                             float* __restrict__ out, long long npix, int hw, int F) {
     for (long long p = blockIdx.x * (long long)blockDim.x + threadIdx.x; p < npix; p += (long long)gridDim.x * blockDim.x) {
         const int q = (int)(p % hw);
         const float m = mean ? mean[q] : 0.f, s = stdv ? stdv[q] : 1.f;
         float o[8];
 #pragma unroll
-        for (int c = 0; c < 5; ++c) o[c] = mean ? (v[p * 5 + c] - m) / s : v[p * 5 + c];
-        o[5] = o[6] = o[7] = 0.f;
+        for (int c = 0; c < 8; ++c) o[c] = c >= F ? 0.f : mean ? (v[p * F + c] - m) / s : v[p * F + c];
         float4* d = reinterpret_cast<float4*>(out + p * 8);
         d[0] = make_float4(o[0], o[1], o[2], o[3]);
         d[1] = make_float4(o[4], o[5], o[6], o[7]);
     }
 }
 
-// audio [N][80][20] -> [N][80][20][8] (expand_dims(-1), network.py:181, channel padded to the 8-wide chunk)
+// audio [N][80][T] -> [N][80][T][8] (expand_dims(-1), network.py:181, channel padded to the 8-wide chunk)
 __global__ void k_prep_audio(const float* __restrict__ a, float* __restrict__ out, long long npix) {
     for (long long p = blockIdx.x * (long long)blockDim.x + threadIdx.x; p < npix; p += (long long)gridDim.x * blockDim.x) {
         float4* d = reinterpret_cast<float4*>(out + p * 8);
@@ -107,11 +106,18 @@ __global__ __launch_bounds__(256) void k_colreduce(const float* __restrict__ x, 
     if (c < C) {
         const float mu = (MODE >= 1) ? mean[c] : 0.f;
         const float iv = (MODE == 2) ? inv[c] : 0.f;
-        for (long long r = r0 + rg; r < r1; r += 4) {
-            const float v = x[r * ld + c];
-            if (MODE == 0) a0 += v;
-            if (MODE == 1) { const float d = v - mu; a0 = fmaf(d, d, a0); }
-            if (MODE == 2) { a0 += v; a1 = fmaf(v, (z[r * C + c] - mu) * iv, a1); }
+        // two-level sums (see kWgGroup): partials p0 / p1 over 64 rows per thread, then into a0 / a1
+        for (long long g = r0 + rg; g < r1; g += 256) {
+            float p0 = 0.f, p1 = 0.f;
+            const long long ge = min(r1, g + 256);
+            for (long long r = g; r < ge; r += 4) {
+                const float v = x[r * ld + c];
+                if (MODE == 0) p0 += v;
+                if (MODE == 1) { const float d = v - mu; p0 = fmaf(d, d, p0); }
+                if (MODE == 2) { p0 += v; p1 = fmaf(v, (z[r * C + c] - mu) * iv, p1); }
+            }
+            a0 += p0;
+            a1 += p1;
         }
     }
     s0[rg][cl] = a0;
@@ -315,6 +321,22 @@ __device__ __forceinline__ void row_nyx(long long r, int Hh, int Wh, int& n, int
     x = rem - y * Wh;
 }
 
+// Row sums of the weight gradients and column statistics are two-level: a thread sums kWgGroup rows into a partial that
+// is then added to its running total, so no fp32 sum runs sequentially over more than ~kWgGroup + rows / kWgGroup
+// terms.  BN-backed gradients are small differences of large sums (dz has zero column mean): a one-level sum over the
+// ~5,000 rows per split of a 1023-clip batch left ~1.5e-2 relative RMS in every gradient (profiles/r03a_gputest.log).
+constexpr int kWgGroup = 256;
+template <int A, int B>
+__device__ __forceinline__ void flush_partial(float (&acc)[A][B], float (&p)[A][B]) {
+#pragma unroll
+    for (int i = 0; i < A; ++i)
+#pragma unroll
+        for (int j = 0; j < B; ++j) {
+            acc[i][j] += p[i][j];
+            p[i][j] = 0.f;
+        }
+}
+
 __global__ __launch_bounds__(256) void k_wgrad(WgArgs w) {
     __shared__ float gs[16][68], hs[16][68];
     const int tid = threadIdx.x, ta = tid >> 4, tb = tid & 15;
@@ -324,9 +346,10 @@ __global__ __launch_bounds__(256) void k_wgrad(WgArgs w) {
     const int2 t = w.taps[tap];
     const long long R = (long long)w.N * w.Hh * w.Wh;
     const long long r0 = blockIdx.z * w.rows_per_split, r1 = min(R, r0 + w.rows_per_split);
-    float acc[4][4] = {};
+    float acc[4][4] = {}, p[4][4] = {};
     const int lr = tid >> 4, lc = (tid & 15) * 4;   // loader: row lr of the chunk, 4 columns lc..lc+3
     for (long long rc = r0; rc < r1; rc += 16) {
+        if (((rc - r0) & (kWgGroup - 1)) == 0) flush_partial(acc, p);
         const long long r = rc + lr;
         float4 gv = make_float4(0.f, 0.f, 0.f, 0.f), hv = gv;
         if (r < r1) {
@@ -362,9 +385,10 @@ __global__ __launch_bounds__(256) void k_wgrad(WgArgs w) {
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
-                for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(av[i], bv[j], acc[i][j]);
+                for (int j = 0; j < 4; ++j) p[i][j] = fmaf(av[i], bv[j], p[i][j]);
         }
     }
+    flush_partial(acc, p);
     float* out = w.part + ((long long)blockIdx.z * w.ntaps + tap) * w.A * w.B;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -388,8 +412,9 @@ __global__ __launch_bounds__(256) void k_wgrad_na(WgArgs w) {
     const int2 t = w.taps[tap];
     const long long R = (long long)w.N * w.Hh * w.Wh;
     const long long r0 = blockIdx.z * w.rows_per_split, r1 = min(R, r0 + w.rows_per_split);
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    float acc[1][4] = {{0.f, 0.f, 0.f, 0.f}}, p[1][4] = {{0.f, 0.f, 0.f, 0.f}};
     for (long long rc = r0; rc < r1; rc += 32) {
+        if (((rc - r0) & (kWgGroup - 1)) == 0) flush_partial(acc, p);
         float gv = 0.f;
         {   // G: row tid / 8, channel tid % 8
             const long long r = rc + (tid >> 3);
@@ -427,16 +452,17 @@ __global__ __launch_bounds__(256) void k_wgrad_na(WgArgs w) {
         for (int k = 0; k < 32; ++k) {
             const float hb = hs[k][tb];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) acc[i] = fmaf(gs[k][ta * 4 + i], hb, acc[i]);
+            for (int i = 0; i < 4; ++i) p[0][i] = fmaf(gs[k][ta * 4 + i], hb, p[0][i]);
         }
     }
+    flush_partial(acc, p);
     float* out = w.part + ((long long)blockIdx.z * w.ntaps + tap) * w.A * w.B;
     const int b = b0 + tb;
     if (b < w.B)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int a = ta * 4 + i;
-            if (a < w.A) out[(long long)a * w.B + b] = acc[i];
+            if (a < w.A) out[(long long)a * w.B + b] = acc[0][i];
         }
 }
 
@@ -608,6 +634,7 @@ struct avse_trainer {
     int64_t max_n = 0;
     int64_t nparams = 0;
     int64_t step = 0;         // Adam iterations done (Keras `iterations`)
+    NetPlan plan = kPlan25;   // network shape (netplan.h)
     std::vector<TLayer> layers;
     float *P = nullptr, *Gr = nullptr, *Mo = nullptr, *Vo = nullptr;
     float *wfwd = nullptr, *wdg = nullptr;
@@ -655,7 +682,7 @@ int build_plan(avse_trainer* t, const float* host_blob) {
     std::vector<int> mf, md;   // forward / dgrad gather maps
     for (int i = 0; i < kNumLayers; ++i) {
         TLayer& T = t->layers[i];
-        const LayerDef& L = kLayers[i];
+        const LayerDef& L = t->plan.L[i];
         T.L = L;
         T.cin_pad = (L.kind == DENSE) ? L.cin : ((L.cin + 7) / 8) * 8;
         T.o_k = off;
@@ -802,7 +829,7 @@ int build_plan(avse_trainer* t, const float* host_blob) {
             }
         }
     }
-    if (off != blob_floats()) return tfail(AVSE_ERR_INVALID, "trainer plan / blob size mismatch");
+    if (off != blob_floats(t->plan)) return tfail(AVSE_ERR_INVALID, "trainer plan / blob size mismatch");
     t->nparams = off;
     t->n_fwd = (long long)mf.size();
     t->n_dg = (long long)md.size();
@@ -839,13 +866,16 @@ bool wg_all_taps(const TLayer& T) {
 
 // wgrad work split over the reduction rows: ~2048 blocks in total, >= 256 rows per split (k_wgrad_nat: ~512
 // blocks of >= 256 rows, each covering every tap: its partials are 25 taps deep)
+constexpr long long kNatMaxRows = 2048;
 long long wg_splits(const TLayer& T, int64_t N) {
     const LayerDef& L = T.L;
     const int A = (L.kind == DECONV) ? L.cout : L.cin, B = (L.kind == DECONV) ? L.cin : L.cout;
     const long long R = N * (long long)((L.kind == DECONV) ? L.hin * L.win : T.hq * T.wq);
     if (wg_all_taps(T)) {
+        // its per-thread row sums are one-level (112 accumulators leave no registers for a second set), so a split
+        // never exceeds kNatMaxRows rows (more, smaller partial slabs at large batches; 16,000 floats each)
         const long long bt = (B + 127) / 128;
-        return std::max(1LL, std::min((512 + bt - 1) / bt, (R + 255) / 256));
+        return std::max({1LL, std::min((512 + bt - 1) / bt, (R + 255) / 256), (R + kNatMaxRows - 1) / kNatMaxRows});
     }
     const long long tiles = (A <= 8 ? (long long)((B + 127) / 128) : (long long)((A + 63) / 64) * ((B + 63) / 64)) * L.kh * L.kw;
     return std::max(1LL, std::min((2048 + tiles - 1) / tiles, (R + 255) / 256));
@@ -856,15 +886,16 @@ int alloc_tensors(avse_trainer* t) {
     // unit scale / zero shift of the bias-only and dgrad convolutions: one entry per output channel (the widest
     // is enc_dense's input gradient, 5248 channels)
     int cmax = 0;
-    for (int i = 0; i < kNumLayers; ++i) cmax = std::max({cmax, kLayers[i].cin, kLayers[i].cout});
+    for (int i = 0; i < kNumLayers; ++i) cmax = std::max({cmax, t->plan.L[i].cin, t->plan.L[i].cout});
     std::vector<float> one(cmax, 1.f);
     if (int rc = talloc(t, &t->ones, cmax)) return rc;
     if (int rc = talloc(t, &t->zeros, cmax)) return rc;
     AVSE_HIP_CHECK(hipMemcpy(t->ones, one.data(), cmax * sizeof(float), hipMemcpyHostToDevice));
-    if (int rc = talloc(t, &t->in_audio, N * 80 * 20 * 8)) return rc;
+    const long long spec = (long long)kMels * t->plan.T;
+    if (int rc = talloc(t, &t->in_audio, N * spec * 8)) return rc;
     if (int rc = talloc(t, &t->in_video, N * 128 * 128 * 8)) return rc;
-    if (int rc = talloc(t, &t->concat, N * 5248)) return rc;
-    if (int rc = talloc(t, &t->g6, N * 80 * 20 * 8)) return rc;
+    if (int rc = talloc(t, &t->concat, N * t->plan.cat)) return rc;
+    if (int rc = talloc(t, &t->g6, N * spec * 8)) return rc;
     long long zmax = 0, red = 0, wmax = 0;
     for (int i = 0; i < kNumLayers; ++i) {
         TLayer& T = t->layers[i];
@@ -896,9 +927,9 @@ int alloc_tensors(avse_trainer* t) {
     for (int i = 0; i < kNumLayers; ++i) {
         TLayer& T = t->layers[i];
         const LayerDef& L = T.L;
-        if (i == 0) { T.in = t->in_audio; T.in_clip = 80 * 20 * 8; }
+        if (i == 0) { T.in = t->in_audio; T.in_clip = (long long)kMels * t->plan.T * 8; }
         else if (std::strcmp(L.name, "v_conv1") == 0) { T.in = t->in_video; T.in_clip = 128 * 128 * 8; }
-        else if (std::strcmp(L.name, "enc_dense") == 0) { T.in = t->concat; T.in_clip = 5248; }
+        else if (std::strcmp(L.name, "enc_dense") == 0) { T.in = t->concat; T.in_clip = t->plan.cat; }
         else {
             const long long el = (long long)L.hin * L.win * T.cin_pad;
             if (int rc = talloc(t, &T.in, N * el)) return rc;
@@ -920,8 +951,8 @@ void out_view(avse_trainer* t, int i, float** buf, float** gbuf, long long* clip
         const TLayer& E = t->layers[11];   // enc_dense
         *buf = t->concat;
         *gbuf = E.gin;
-        *clip = 5248;
-        *coff = std::strcmp(nm, "a_conv5") == 0 ? 0 : 3200;
+        *clip = t->plan.cat;
+        *coff = std::strcmp(nm, "a_conv5") == 0 ? 0 : t->plan.aemb;
         return;
     }
     const TLayer& Nx = t->layers[i + 1];
@@ -1066,9 +1097,10 @@ int step_impl(avse_trainer* t, const float* audio, const float* video, const flo
     AVSE_HIP_CHECK(hipGetLastError());
     AVSE_HIP_CHECK(hipMemsetAsync(t->Gr, 0, sizeof(float) * t->nparams, s));
     // ---- inputs ----
-    hipLaunchKernelGGL(k_prep_audio, dim3(grid_for(N * 1600)), dim3(256), 0, s, audio, t->in_audio, (long long)N * 1600);
+    const long long spec = (long long)kMels * t->plan.T;
+    hipLaunchKernelGGL(k_prep_audio, dim3(grid_for(N * spec)), dim3(256), 0, s, audio, t->in_audio, (long long)N * spec);
     hipLaunchKernelGGL(k_prep_video, dim3(grid_for(N * 16384)), dim3(256), 0, s, video, vmean, vstd, t->in_video,
-                       (long long)N * 16384, 16384);
+                       (long long)N * 16384, 16384, t->plan.F);
     AVSE_HIP_CHECK(hipGetLastError());
     // ---- forward ----
     for (int i = 0; i < kNumLayers; ++i) {
@@ -1086,7 +1118,7 @@ int step_impl(avse_trainer* t, const float* audio, const float* video, const flo
         std::memset(&aa, 0, sizeof(aa));
         aa.z = T.z; aa.N = (int)N; aa.C = C;
         aa.Hq = (L.kind == DENSE) ? ((std::strcmp(L.name, "dec_dense2") == 0) ? 5 : 1) : T.hq;
-        aa.Wq = (L.kind == DENSE) ? ((std::strcmp(L.name, "dec_dense2") == 0) ? 5 : 1) : T.wq;
+        aa.Wq = (L.kind == DENSE) ? ((std::strcmp(L.name, "dec_dense2") == 0) ? t->plan.W5 : 1) : T.wq;
         aa.mean = T.mean; aa.inv = T.inv; aa.gamma = P + T.o_g; aa.beta = P + T.o_be;
         aa.pool = L.pool ? 1 : 0;
         aa.drop = L.pool ? drop : 0.f;   // Dropout(0.25) follows each video pooling (network.py:142-174)
@@ -1099,7 +1131,7 @@ int step_impl(avse_trainer* t, const float* audio, const float* video, const flo
     }
     // ---- loss ----
     TLayer& D6 = t->layers[kNumLayers - 1];
-    const long long nout = N * 80 * 20;
+    const long long nout = N * spec;
     const unsigned lb = grid_for(nout, 256, 1024);
     hipLaunchKernelGGL(k_mse, dim3(lb), dim3(256), 0, s, (const float*)D6.z, target, nout, D6.zc, t->g6, t->red);
     hipLaunchKernelGGL(k_mse_finish, dim3(1), dim3(64), 0, s, (const float*)t->red, (int)lb, nout, t->loss);
@@ -1120,7 +1152,7 @@ int step_impl(avse_trainer* t, const float* audio, const float* video, const flo
             std::memset(&aa, 0, sizeof(aa));
             aa.z = T.z; aa.N = (int)N; aa.C = C;
             aa.Hq = (L.kind == DENSE) ? ((std::strcmp(L.name, "dec_dense2") == 0) ? 5 : 1) : T.hq;
-            aa.Wq = (L.kind == DENSE) ? ((std::strcmp(L.name, "dec_dense2") == 0) ? 5 : 1) : T.wq;
+            aa.Wq = (L.kind == DENSE) ? ((std::strcmp(L.name, "dec_dense2") == 0) ? t->plan.W5 : 1) : T.wq;
             aa.mean = T.mean; aa.inv = T.inv; aa.gamma = t->P + T.o_g; aa.beta = t->P + T.o_be;
             aa.pool = L.pool ? 1 : 0;
             aa.drop = L.pool ? drop : 0.f;
@@ -1170,12 +1202,20 @@ int step_impl(avse_trainer* t, const float* audio, const float* video, const flo
 extern "C" {
 
 int avse_trainer_create(avse_ctx* c, const float* host_blob, int64_t n_floats, int64_t max_batch, avse_trainer** out) {
+    return avse_trainer_create_shape(c, host_blob, n_floats, max_batch, kPlan25.T, kPlan25.F, out);
+}
+
+int avse_trainer_create_shape(avse_ctx* c, const float* host_blob, int64_t n_floats, int64_t max_batch, int spec_frames,
+                              int video_frames, avse_trainer** out) {
     if (!c || !host_blob || !out) return tfail(AVSE_ERR_INVALID, "NULL argument");
-    if (n_floats != blob_floats()) return tfail(AVSE_ERR_INVALID, "weight blob has the wrong size");
+    if (!plan_valid(spec_frames, video_frames)) return tfail(AVSE_ERR_UNSUPPORTED, "unsupported network shape");
+    const NetPlan plan = make_plan(spec_frames, video_frames);
+    if (n_floats != blob_floats(plan)) return tfail(AVSE_ERR_INVALID, "weight blob has the wrong size");
     // <= 1023 keeps every activation tensor (v_conv1's pre-pool z: 128 x 128 x 128 per clip) below 2^31 elements,
     // so the element-wise kernels index in 32 bits
     if (max_batch < 1 || max_batch > 1023) return tfail(AVSE_ERR_INVALID, "max_batch must be in [1, 1023]");
     auto* t = new avse_trainer();
+    t->plan = plan;
     t->device = ctx_device_index(c);
     t->max_n = max_batch;
     int rc = hipSetDevice(t->device) == hipSuccess ? 0 : tfail(AVSE_ERR_HIP, "hipSetDevice failed");

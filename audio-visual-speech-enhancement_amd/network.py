@@ -1,7 +1,8 @@
 """SpeechEnhancementNetwork — drop-in for /root/reference/network.py's inference API on MI355X.
 
 build / predict / evaluate / load / save keep the reference's signatures and tensor shapes
-(`predict` takes [N, 80, 20] + [N, 128, 128, 5] and returns np.squeeze of [N, 80, 20, 1]).
+(`predict` takes [N, 80, 20] + [N, 128, 128, 5] and returns np.squeeze of [N, 80, 20, 1]; a network built for
+another frame rate — build((80, 24), (128, 128, 5 or 6)) at 29.97 / 30 fps — takes and returns its own shapes).
 The forward pass is libavse's avse_forward (HIP kernels); there is no Keras and no CPU fallback.
 train (network.py:177-206) runs Keras-semantics fit steps on libavse's training step (fit.py, csrc/train.hip).
 """
@@ -9,7 +10,7 @@ import numpy as np
 import torch
 
 from . import ops
-from .model import AUDIO_SHAPE, VIDEO_SHAPE, KerasModel
+from .model import KerasModel, shape_supported
 
 
 class SpeechEnhancementNetwork(object):
@@ -31,12 +32,16 @@ class SpeechEnhancementNetwork(object):
 
     @classmethod
     def build(cls, audio_spectrogram_shape, video_shape, seed=0, compute_dtype="float32"):
-        """network.py:17-40 — fresh Keras-default-initialised network for these input shapes."""
-        if tuple(audio_spectrogram_shape) != AUDIO_SHAPE or tuple(video_shape) != VIDEO_SHAPE:
+        """network.py:17-40 — fresh Keras-default-initialised network for these input shapes: audio [80, T] (T = 20 at
+        25 fps, 24 at 29.97 / 30 fps), video [128, 128, F] (F = 5, or 6 at 30 fps).  The layer widths follow the
+        shapes as in Keras (model.layers).  Shapes whose decoder cannot reproduce 80 x T (T not a multiple of 4)
+        raise NotImplementedError."""
+        a, v = tuple(int(x) for x in audio_spectrogram_shape), tuple(int(x) for x in video_shape)
+        if len(a) != 2 or a[0] != 80 or len(v) != 3 or v[:2] != (128, 128) or not shape_supported(a[1], v[2]):
             raise NotImplementedError(
-                f"kernels are specialised for audio {AUDIO_SHAPE} and video {VIDEO_SHAPE} "
-                f"(16 kHz / 25 fps, 200-ms slices); got {tuple(audio_spectrogram_shape)}, {tuple(video_shape)}")
-        return SpeechEnhancementNetwork(KerasModel.init(seed=seed), compute_dtype)
+                f"audio [80, T] with T a multiple of 4 and video [128, 128, F <= 8] are implemented (16 kHz, 200-ms "
+                f"slices: T = 20 at 25 fps, 24 at 29.97 / 30 fps); got {a}, {v}")
+        return SpeechEnhancementNetwork(KerasModel.init(seed=seed, audio_shape=a, video_shape=v), compute_dtype)
 
     def train(self, train_mixed_spectrograms, train_video_samples, train_speech_spectrograms,
               validation_mixed_spectrograms, validation_video_samples, validation_speech_spectrograms,
@@ -56,9 +61,9 @@ class SpeechEnhancementNetwork(object):
         return history
 
     def predict_device(self, mixed_spectrograms, video_samples, video_normalizer=None):
-        """Device-tensor forward: [N, 80, 20] x [N, 128, 128, 5] -> [N, 80, 20] (no squeeze)."""
+        """Device-tensor forward: [N, 80, T] x [N, 128, 128, F] -> [N, 80, T] (no squeeze)."""
         a = ops.to_device(mixed_spectrograms, self.__device)
-        v = ops.to_device(video_samples, a.device)
+        v = None if video_samples is None else ops.to_device(video_samples, a.device)   # None: all-zero video
         m = s = None
         if video_normalizer is not None:
             m, s = video_normalizer.device_stats(a.device)

@@ -109,12 +109,18 @@ class DeviceWeights:
             raise TypeError("model must be a KerasModel")
         self.dtype = DTYPES[dtype] if isinstance(dtype, str) else int(dtype)
         self.ctx = _lib.context(device)
+        self.T, self.F = model.T, model.F
         blob = model.to_blob()
-        assert blob.size == blob_floats() == _lib.load().avse_weights_blob_floats()
+        assert blob.size == blob_floats(self.T, self.F) == _lib.load().avse_weights_blob_floats_shape(self.T, self.F)
         self.handle = ctypes.c_void_p()
         with torch.cuda.device(self.ctx.device_index):
-            _lib.check(_lib.load().avse_weights_load(self.ctx.handle, blob.ctypes.data_as(ctypes.c_void_p), blob.size,
-                                                     self.dtype, ctypes.byref(self.handle)), "avse_weights_load")
+            _lib.check(_lib.load().avse_weights_load_shape(self.ctx.handle, blob.ctypes.data_as(ctypes.c_void_p),
+                                                           blob.size, self.dtype, self.T, self.F,
+                                                           ctypes.byref(self.handle)), "avse_weights_load_shape")
+
+    @property
+    def audio_shape(self):
+        return (80, self.T)
 
     def __del__(self):
         h = getattr(self, "handle", None)
@@ -124,10 +130,10 @@ class DeviceWeights:
 
 
 def _check_forward_args(weights, audio, video, vnorm_mean, vnorm_std):
-    _dev_f32(audio, "audio", (80, 20))
+    _dev_f32(audio, "audio", (80, weights.T))
     N = audio.shape[0]
     if video is not None:
-        _dev_f32(video, "video", (128, 128, 5))
+        _dev_f32(video, "video", (128, 128, weights.F))
         if video.shape[0] != N:
             raise ValueError("audio and video batch sizes differ")
     if (vnorm_mean is None) != (vnorm_std is None):
@@ -146,16 +152,17 @@ def _check_forward_args(weights, audio, video, vnorm_mean, vnorm_std):
 
 def forward(weights, audio, video, vnorm_mean=None, vnorm_std=None, out=None):
     """K2-K5: network forward.  audio [N, 80, 20], video [N, 128, 128, 5] float32 device tensors
-    (video un-normalised when vnorm_* are given).  Returns [N, 80, 20] float32.
+    (video un-normalised when vnorm_* are given).  Returns [N, 80, 20] float32.  ([N, 80, T] / [N, 128, 128, F]
+    for weights of another network shape, e.g. T = 24 at 29.97 fps.)
 
     video=None means an all-zero video input (BASELINE configs[2], the audio branch alone): the video
     encoder's output is then one constant vector, computed once per weights object and broadcast."""
     N = _check_forward_args(weights, audio, video, vnorm_mean, vnorm_std)
     if out is None:
-        out = torch.empty((N, 80, 20), dtype=torch.float32, device=audio.device)
-    _dev_f32(out, "out", (80, 20))
+        out = torch.empty((N, 80, weights.T), dtype=torch.float32, device=audio.device)
+    _dev_f32(out, "out", (80, weights.T))
     if out.device != audio.device or out.shape[0] != N:
-        raise ValueError("out must be [N, 80, 20] on the inputs' device")
+        raise ValueError(f"out must be [N, 80, {weights.T}] on the inputs' device")
     with torch.cuda.device(audio.device):
         _lib.check(_lib.load().avse_forward(weights.ctx.handle, weights.handle, _lib.ptr(audio), _lib.ptr(video),
                                             _lib.ptr(vnorm_mean), _lib.ptr(vnorm_std), N, _lib.ptr(out),
@@ -167,7 +174,7 @@ def forward_profile(weights, audio, video, vnorm_mean=None, vnorm_std=None, out=
     """forward() with HIP events between kernel launches (synchronises); returns (out, {stage: ms})."""
     N = _check_forward_args(weights, audio, video, vnorm_mean, vnorm_std)
     if out is None:
-        out = torch.empty((N, 80, 20), dtype=torch.float32, device=audio.device)
+        out = torch.empty((N, 80, weights.T), dtype=torch.float32, device=audio.device)
     ms = (ctypes.c_float * _lib.AVSE_NUM_STAGES)()
     with torch.cuda.device(audio.device):
         _lib.check(_lib.load().avse_forward_profile(weights.ctx.handle, weights.handle, _lib.ptr(audio), _lib.ptr(video),
@@ -222,20 +229,22 @@ class Trainer:
             raise TypeError("model must be a KerasModel")
         self.ctx = _lib.context(device)
         self.max_batch = int(max_batch)
+        self.T, self.F = model.T, model.F
         blob = model.to_blob()
         self.handle = ctypes.c_void_p()
         with torch.cuda.device(self.ctx.device_index):
-            _lib.check(_lib.load().avse_trainer_create(self.ctx.handle, blob.ctypes.data_as(ctypes.c_void_p), blob.size,
-                                                       self.max_batch, ctypes.byref(self.handle)), "avse_trainer_create")
+            _lib.check(_lib.load().avse_trainer_create_shape(self.ctx.handle, blob.ctypes.data_as(ctypes.c_void_p),
+                                                             blob.size, self.max_batch, self.T, self.F,
+                                                             ctypes.byref(self.handle)), "avse_trainer_create_shape")
         self._loss = torch.zeros((), dtype=torch.float32, device=torch.device("cuda", self.ctx.device_index))
 
     def step(self, audio, video, target, vnorm_mean=None, vnorm_std=None, lr=5e-4, dropout=0.25, seed=0,
              grads_only=False):
         """One fit step on a batch: audio / target [N, 80, 20], video [N, 128, 128, 5] (raw crops when vnorm_* are
         given) float32 device tensors.  Returns the batch MSE before the update as a 0-dim device tensor."""
-        _dev_f32(audio, "audio", (80, 20))
-        _dev_f32(target, "target", (80, 20))
-        _dev_f32(video, "video", (128, 128, 5))
+        _dev_f32(audio, "audio", (80, self.T))
+        _dev_f32(target, "target", (80, self.T))
+        _dev_f32(video, "video", (128, 128, self.F))
         N = audio.shape[0]
         if video.shape[0] != N or target.shape[0] != N:
             raise ValueError("audio, video and target batch sizes differ")
@@ -255,18 +264,18 @@ class Trainer:
         return self._loss.clone()
 
     def _read(self, what):
-        out = np.empty(blob_floats(), dtype=np.float32)
+        out = np.empty(blob_floats(self.T, self.F), dtype=np.float32)
         _lib.check(_lib.load().avse_trainer_read(self.handle, what, out.ctypes.data_as(ctypes.c_void_p), out.size),
                    "avse_trainer_read")
         return out
 
     def model(self):
         """Current parameters (incl. BN moving statistics) as a KerasModel."""
-        return KerasModel.from_blob(self._read(_lib.AVSE_TRAIN_PARAMS))
+        return KerasModel.from_blob(self._read(_lib.AVSE_TRAIN_PARAMS), self.T, self.F)
 
     def gradients(self):
         """Gradients of the last step, {tensor name: array} (moving statistics: zero)."""
-        return KerasModel.from_blob(self._read(_lib.AVSE_TRAIN_GRADS)).tensors
+        return KerasModel.from_blob(self._read(_lib.AVSE_TRAIN_GRADS), self.T, self.F).tensors
 
     @property
     def iterations(self):

@@ -51,6 +51,9 @@ class Enhancer:
         if signals.shape[1] != L:
             signals = torch.nn.functional.pad(signals, (0, max(0, L - signals.shape[1])))[:, :L].contiguous()
         spf = g["spectrogram_samples_per_slice"]
+        if spf != self.weights.T or video.shape[-1] != self.weights.F:
+            raise ValueError(f"{self.fps} fps gives [80, {spf}] slices with {video.shape[-1]} video frames; the weights "
+                             f"are for [80, {self.weights.T}] x {self.weights.F} frames (build the network for this rate)")
         mel, stft = ops.spectrogram(signals, sample_rate=self.sr, n_fft=g["n_fft"], hop_length=g["hop_length"],
                                     n_mels=data_processor.N_MELS, fmin=data_processor.MEL_FMIN,
                                     fmax=data_processor.MEL_FMAX, frames_per_slice=spf, return_stft=True)

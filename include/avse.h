@@ -115,8 +115,17 @@ int avse_istft(avse_ctx* ctx, const float* mel_db, const float* stft_ri, int64_t
 
 /* ---- network --------------------------------------------------------------------------- */
 
-/* Number of float32 values in a canonical weight blob (see avse_weights_load). */
+/* Number of float32 values in a canonical weight blob (see avse_weights_load): the 25-fps network
+ * (build((80, 20), (128, 128, 5))). */
 int64_t avse_weights_blob_floats(void);
+
+/* The same for the network SpeechEnhancementNetwork.build((80, spec_frames), (128, 128, video_frames)) builds
+ * (network.py:17-40; data_processor.py:44-52: spec_frames = int(slice samples / hop) = 20 at 25 fps, 24 at
+ * 29.97 / 30 fps; video_frames = int(0.2 * fps) = 5 at 25 / 29.97 fps, 6 at 30 fps).  The shapes set the audio
+ * embedding (5 x ceil(spec_frames / 4) x 128), the concat width (+ 2048) and the dense widths (concat / 4,
+ * network.py:55).  -1 for shapes the kernels do not implement (spec_frames not a multiple of 4 — the decoder
+ * would not reproduce 80 x spec_frames — or video_frames outside 1..8). */
+int64_t avse_weights_blob_floats_shape(int spec_frames, int video_frames);
 
 /* Replaces SpeechEnhancementNetwork.load (network.py:222-226) for the build's own weight format.
  * host_blob: the Keras-layout tensors of network.py's layers in creation order (float32):
@@ -130,19 +139,28 @@ int64_t avse_weights_blob_floats(void);
  * GEMM and uploaded in compute_dtype (AVSE_F32 or AVSE_BF16).  Synchronous. */
 int avse_weights_load(avse_ctx* ctx, const float* host_blob, int64_t n_floats, int compute_dtype,
                       avse_weights** out);
+/* avse_weights_load for the network of build((80, spec_frames), (128, 128, video_frames)); the weights remember
+ * the shape, and avse_forward then takes audio [N][80][spec_frames] and video [N][128][128][video_frames].
+ * The fused per-clip kernels cover the 25-fps shape (and v_conv1's 5-frame kernel every 5-frame shape); other
+ * shapes run the generic implicit-GEMM path.  AVSE_ERR_UNSUPPORTED as avse_weights_blob_floats_shape's -1. */
+int avse_weights_load_shape(avse_ctx* ctx, const float* host_blob, int64_t n_floats, int compute_dtype,
+                            int spec_frames, int video_frames, avse_weights** out);
+/* The shape the weights were loaded for. */
+int avse_weights_shape(const avse_weights* w, int* spec_frames, int* video_frames);
 void avse_weights_destroy(avse_weights* w);
 
 /* Replaces SpeechEnhancementNetwork.predict's Model.predict (network.py:208-212) and the
  * VideoNormalizer.normalize it is preceded by (data_processor.py:208-212,
  * speech_enhancer.py:74), fused:
- *   audio      [N][80][20]        mixed mel-dB spectrograms (the expand_dims(-1) is implicit)
- *   video      [N][128][128][5]   mouth crops, NOT normalised; NULL = an all-zero video input (the audio
+ *   audio      [N][80][20]        mixed mel-dB spectrograms (the expand_dims(-1) is implicit);
+ *                                 [N][80][T] for weights loaded with avse_weights_load_shape(T, F)
+ *   video      [N][128][128][5]   mouth crops ([N][128][128][F]), NOT normalised; NULL = an all-zero video input (the audio
  *                                 branch alone, BASELINE configs[2]: the video encoder's output is then one
  *                                 constant vector, computed once per weights object and broadcast;
  *                                 vnorm_* must be NULL)
  *   vnorm_mean [128][128]         nullable: VideoNormalizer mean image (applied in-kernel)
  *   vnorm_std  [128][128]         nullable: VideoNormalizer std image
- *   out        [N][80][20]        predicted speech mel-dB spectrograms (float32)
+ *   out        [N][80][20]        predicted speech mel-dB spectrograms (float32; [N][80][T])
  * Computes in the weights' compute dtype, accumulating in float32. */
 int avse_forward(avse_ctx* ctx, const avse_weights* w, const float* audio, const float* video,
                  const float* vnorm_mean, const float* vnorm_std, int64_t N, float* out,
@@ -190,6 +208,11 @@ enum avse_train_flags { AVSE_TRAIN_GRADS_ONLY = 1, AVSE_TRAIN_DEBUG_STOP = 2, AV
  * 1..1023 (activation tensors stay below 2^31 elements). */
 int avse_trainer_create(avse_ctx* ctx, const float* host_blob, int64_t n_floats, int64_t max_batch,
                         avse_trainer** out);
+/* avse_trainer_create for the network of build((80, spec_frames), (128, 128, video_frames)) (see
+ * avse_weights_blob_floats_shape); avse_trainer_step then takes audio / target [N][80][spec_frames] and video
+ * [N][128][128][video_frames]. */
+int avse_trainer_create_shape(avse_ctx* ctx, const float* host_blob, int64_t n_floats, int64_t max_batch,
+                              int spec_frames, int video_frames, avse_trainer** out);
 void avse_trainer_destroy(avse_trainer* t);
 
 /* audio [N][80][20] mixed mel-dB, video [N][128][128][5] raw mouth crops (normalised in-kernel when vnorm_* are

@@ -94,7 +94,7 @@ def forward(weights, mixed_spectrograms, video_samples, dtype=torch.float64, thr
 
     weights: dict name -> dict of Keras-layout arrays ('kernel', 'bias'; BN layers under
     name + '_bn' with gamma/beta/moving_mean/moving_variance).
-    mixed_spectrograms [N, 80, 20]; video_samples [N, 128, 128, 5] (already normalised), or None for an
+    mixed_spectrograms [N, 80, T]; video_samples [N, 128, 128, F] (already normalised), or None for an
     all-zero video input (BASELINE configs[2]): the video branch then runs once on one zero clip and its
     embedding is shared by every clip, which is what a zero batch computes clip by clip.
     intermediates: optional dict, filled with each layer's NHWC output (after BN/LReLU/pool).
@@ -108,7 +108,7 @@ def forward(weights, mixed_spectrograms, video_samples, dtype=torch.float64, thr
     with torch.no_grad():
         a = _t(mixed_spectrograms, dtype)[:, None, :, :]          # expand_dims(-1) -> NCHW, C=1
         if video_samples is None:
-            video_samples = np.zeros((1, 128, 128, 5), np.float32)
+            video_samples = np.zeros((1, 128, 128, weights["v_conv1"]["kernel"].shape[2]), np.float32)
         v = _t(video_samples, dtype).permute(0, 3, 1, 2)           # NHWC -> NCHW
         for name, kind, f, k, s, has_bn, pool, _ in AUDIO_ENCODER:
             a = lrelu(bn(conv_same(a, weights[name]["kernel"], weights[name]["bias"], s, dtype), weights[name + "_bn"], dtype))

@@ -13,6 +13,9 @@ decides by itself:
   network_spec.json  SpeechEnhancementNetwork.build((80, 20), (128, 128, 5)) (network.py:17-40)
                      against a symbolic Keras stub: every layer constructor call in order with its
                      arguments and the propagated output shape, plus the compile() call.
+  network_spec_2997fps.json / network_spec_30fps.json
+                     the same for the shapes the reference's preprocessing produces at 29.97 fps
+                     ((80, 24), (128, 128, 5)) and 30 fps ((80, 24), (128, 128, 6)) (data_processor.py:24, :44-52).
 
 The reference never travels: only these JSON outputs (data) are committed.
 Run:  python tests/golden/make_fixtures.py
@@ -139,7 +142,7 @@ def slicing_fixture():
 # ------------------------------------------------------------------------------------------
 # network.py with a symbolic keras stub
 # ------------------------------------------------------------------------------------------
-def network_fixture():
+def network_fixture(audio_shape=(80, 20), video_shape=(128, 128, 5)):
     log = []
 
     class Shape(tuple):
@@ -238,9 +241,9 @@ def network_fixture():
     try:
         _clear(["network"])
         import network
-        network.SpeechEnhancementNetwork.build((80, 20), (128, 128, 5))
+        network.SpeechEnhancementNetwork.build(audio_shape, video_shape)
         return {"source": "network.py:17-175 executed against a symbolic keras stub (tests/golden/make_fixtures.py)",
-                "build_args": [[80, 20], [128, 128, 5]], "graph": log}
+                "build_args": [list(audio_shape), list(video_shape)], "graph": log}
     finally:
         sys.path.remove(REF)
         _clear(["network"])
@@ -256,9 +259,12 @@ def main():
         raise SystemExit(f"{REF} not present: fixtures can only be regenerated in the build container")
     with open(os.path.join(HERE, "slicing.json"), "w") as f:
         json.dump(slicing_fixture(), f, indent=1)
-    with open(os.path.join(HERE, "network_spec.json"), "w") as f:
-        json.dump(network_fixture(), f, indent=1, default=lambda o: o.item() if hasattr(o, "item") else str(o))
-    print("wrote slicing.json, network_spec.json")
+    for name, a, v in [("network_spec.json", (80, 20), (128, 128, 5)),
+                       ("network_spec_2997fps.json", (80, 24), (128, 128, 5)),
+                       ("network_spec_30fps.json", (80, 24), (128, 128, 6))]:
+        with open(os.path.join(HERE, name), "w") as f:
+            json.dump(network_fixture(a, v), f, indent=1, default=lambda o: o.item() if hasattr(o, "item") else str(o))
+    print("wrote slicing.json, network_spec*.json")
 
 
 if __name__ == "__main__":

@@ -156,13 +156,23 @@ def test_preprocessed_blob_and_normalizer_round_trip(tmp_path):
     assert np.array_equal(back.mean_image, norm.mean_image) and np.array_equal(back.std_image, norm.std_image)
 
 
-def test_non_25_fps_network_shape_is_refused():
-    """At 29.97 fps the reference slices [80, 24] spectrograms (data_processor.py:44-49) and Keras would build a
-    different network (Dense widths follow the audio embedding: 5888 -> 1472, network.py:53-54).  The kernels and
-    the weight blob are specialised for the 25-fps graph, so build() refuses other shapes up front (the STFT /
-    ISTFT themselves do run at 29.97 fps: tests/test_gpu_stft.py, tests/test_gpu_istft.py)."""
+def test_other_frame_rate_networks_build_and_bad_shapes_are_refused():
+    """At 29.97 / 30 fps the reference slices [80, 24] spectrograms (data_processor.py:44-52) with 5 / 6 video frames
+    per slice (:24), and Keras builds the matching network (concat 5888 -> Dense 1472, network.py:53-55; graphs
+    pinned in tests/golden/network_spec_*fps.json).  build() makes those; the C library sizes their weight blobs
+    the same way; shapes whose decoder cannot give back 80 x T (T not a multiple of 4) are refused up front."""
+    from avse_amd import _lib
+    from avse_amd.model import blob_floats
     from avse_amd.network import SpeechEnhancementNetwork
-    with pytest.raises(NotImplementedError, match=r"\(80, 20\)"):
-        SpeechEnhancementNetwork.build((80, 24), (128, 128, 5))
+    lib = _lib.load()
+    for T, F in [(20, 5), (24, 5), (24, 6), (8, 1)]:
+        assert lib.avse_weights_blob_floats_shape(T, F) == blob_floats(T, F), (T, F)
+    net = SpeechEnhancementNetwork.build((80, 24), (128, 128, 6))
+    assert (net.model.T, net.model.F) == (24, 6)
+    assert net.model.tensors["enc_dense/kernel"].shape == (5888, 1472)
+    assert net.model.tensors["dec_dense2/kernel"].shape == (1472, 3840)
+    assert lib.avse_weights_blob_floats_shape(22, 5) == -1 and lib.avse_weights_blob_floats_shape(24, 9) == -1
+    with pytest.raises(NotImplementedError):
+        SpeechEnhancementNetwork.build((80, 22), (128, 128, 5))
     with pytest.raises(NotImplementedError):
         SpeechEnhancementNetwork.build((80, 20), (64, 64, 5))

@@ -65,9 +65,18 @@ def test_oracle_reconstruct_length():
 
 
 # ---------------------------------------------------------------- network spec (pinned)
-def test_layer_spec_matches_reference_graph():
-    from avse_amd.model import LAYERS
-    graph = load("network_spec.json")["graph"]
+SPECS = [("network_spec.json", 20, 5), ("network_spec_2997fps.json", 24, 5), ("network_spec_30fps.json", 24, 6)]
+
+
+@pytest.mark.parametrize("fixture,T,F", SPECS)
+def test_layer_spec_matches_reference_graph(fixture, T, F):
+    """model.layers(T, F) against the graph the reference's build((80, T), (128, 128, F)) creates: 25 fps, and the
+    29.97 / 30 fps shapes its preprocessing produces (concat 5888 -> Dense 1472, dec_dense2 3840 = 5 x 6 x 128)."""
+    from avse_amd.model import layers
+    LAYERS = layers(T, F)
+    spec = load(fixture)
+    assert spec["build_args"] == [[80, T], [128, 128, F]]
+    graph = spec["graph"]
     convs = [e for e in graph if e["layer"] in ("Conv2D", "Conv2DTranspose", "Dense")]
     assert len(convs) == len(LAYERS) == 20
     # reference creation order: audio enc, video enc, enc dense, dec dense x2, deconvs
@@ -96,12 +105,16 @@ def test_layer_spec_matches_reference_graph():
     assert comp["loss"] == "mean_squared_error" and comp["optimizer"] == ["adam", 0.0005]
 
 
-def test_shapes_propagate_like_reference():
-    graph = load("network_spec.json")["graph"]
+@pytest.mark.parametrize("fixture,T,F", SPECS)
+def test_shapes_propagate_like_reference(fixture, T, F):
+    from avse_amd.model import embedding
+    graph = load(fixture)["graph"]
+    aemb, cat_w, emb = embedding(T)
     cat = [e for e in graph if e["layer"] == "Concatenate"][0]
-    assert cat["in"] == [[3200], [2048]] and cat["out"] == [5248]
+    assert cat["in"] == [[aemb], [2048]] and cat["out"] == [cat_w]
+    assert [e["out"] for e in graph if e["layer"] == "Dense"] == [[emb], [emb], [aemb]]
     outs = [e["out"] for e in graph if e["layer"] == "Conv2DTranspose"]
-    assert outs[-1] == [80, 20, 1]
+    assert outs[-1] == [80, T, 1]
 
 
 def test_param_count():
