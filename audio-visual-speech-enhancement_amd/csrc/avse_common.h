@@ -33,9 +33,7 @@ struct Options {
     int unfused_tail = 0;     // AVSE_UNFUSED_TAIL: d_deconv6 as its own kernel (d_deconv5 activation materialised)
     int no_halo = 0;          // AVSE_NO_HALO: video convs on k_conv (read when weights are loaded)
     int mfma32 = 0;           // AVSE_MFMA32: 32x32x16 compute waves in the stream convolutions
-    int tile_alt = 0;         // AVSE_TILE_ALT: v_conv2 / v_conv4 walk their tiles last-first (MALL reuse A/B)
     int serial = 0;           // AVSE_SERIAL: one stream for the whole forward
-    int aud_side = 0;         // AVSE_AUD_SIDE: fused audio encoder on the side stream
     int graph = 0;            // AVSE_GRAPH: avse_forward replays a hipGraph per argument set
     int gemm_ksplit_cap = 0;  // AVSE_GEMM_KSPLIT: cap k_gemm's split-K factor (0 = no cap)
     int dense_istft = 0;      // AVSE_DENSE_ISTFT: ISTFT through the dense pinv + scratch frames + k_ola (not fused)
@@ -246,7 +244,6 @@ struct HaloArgs {
     int out_pix_stride;
     int out_c_off;
     int mfma32;              // conv_stream.hip: 1 = v_mfma_f32_32x32x16_bf16 compute waves (A/B variant)
-    int rev;                 // conv_stream.hip: 1 = tiles walked from the last: the previous layer wrote those last
     unsigned long long* prof;   // ablation harness only (ABL & 128): per-wave cycle counters, else unused
 };
 

@@ -176,9 +176,7 @@ const OptionName kOptionNames[] = {
     {"unfused_tail", "AVSE_UNFUSED_TAIL", &Options::unfused_tail},
     {"no_halo", "AVSE_NO_HALO", &Options::no_halo},
     {"mfma32", "AVSE_MFMA32", &Options::mfma32},
-    {"tile_alt", "AVSE_TILE_ALT", &Options::tile_alt},
     {"serial", "AVSE_SERIAL", &Options::serial},
-    {"aud_side", "AVSE_AUD_SIDE", &Options::aud_side},
     {"graph", "AVSE_GRAPH", &Options::graph},
     {"gemm_ksplit_cap", "AVSE_GEMM_KSPLIT", &Options::gemm_ksplit_cap},
     {"dense_istft", "AVSE_DENSE_ISTFT", &Options::dense_istft},
@@ -1066,9 +1064,9 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
     // AVSE_SERIAL=1 forces it).  The fork waits for everything enqueued on s before this call.
     // The fused audio encoder runs on the caller's stream: beside the persistent video convolutions its 152-KB
     // workgroups hold whole CUs they wait for (measured: concurrent 2.377 ms vs serial 2.304 ms per step), and the
-    // fork / join events alone cost ~25 us of idle GPU per step (rocprof trace); AVSE_AUD_SIDE=1 keeps the side stream.
-    const bool aud_side = opt.aud_side != 0;
-    const bool concurrent = ev == nullptr && !opt.serial && (!aud_fused || aud_side);
+    // fork / join events alone cost ~25 us of idle GPU per step (rocprof trace).  (The side-stream option for it was
+    // removed in round 3, as was tile_alt, v_conv2 / v_conv4 tiles walked last-first: both measured no gain.)
+    const bool concurrent = ev == nullptr && !opt.serial && !aud_fused;
     hipStream_t sa = s;
     if (concurrent) {
         if (!c->side) {
@@ -1081,7 +1079,7 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
         sa = c->side;
     }
     if (aud_fused) {
-        if ((rc = launch_aud_enc(aa, aud_side ? sa : s))) return rc;
+        if ((rc = launch_aud_enc(aa, s))) return rc;
         for (int k = 0; k < 6; ++k)
             if ((rc = mark())) return rc;   // audio_prep (= the fused kernel), a_conv1..a_conv5
     }
@@ -1107,7 +1105,6 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
                 HaloArgs h = (i < 5) ? halo_args(G, vb(v_in[i]), vid, vm, vs, vb(v_in[i + 1]),
                                                  (long long)G.ho * G.wo * G.def.cout, G.def.cout, 0, n, opt)
                                      : halo_args(G, vb(v_in[i]), vid, vm, vs, cat, CAT, G.def.cout, AEMB, n, opt);
-                h.rev = opt.tile_alt && (i == 1 || i == 3);   // v_conv1 / v_conv3 write their last tiles last
                 rc = G.halo == HALO_V1 ? launch_conv_v1r(h, s) : launch_conv_stream(h, s);
                 if (rc || (rc = mark())) return rc;
                 continue;

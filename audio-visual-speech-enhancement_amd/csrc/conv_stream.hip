@@ -157,7 +157,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
     const long long clip_bytes = (long long)a.Hc * a.Wc * a.Ci * 2;
 
     auto tile_origin = [&](int k, int& clip0, int& oy0, int& ox0) {
-        const int t = a.rev ? ntiles - 1 - (slot + k * gxs) : slot + k * gxs;
+        const int t = slot + k * gxs;
         clip0 = (ABL & 64) ? 0 : (t / tiles_per_clip) * NCLIP;
         const int tt = t % tiles_per_clip;
         oy0 = (tt / tiles_x) * TH;

@@ -62,7 +62,7 @@ void avse_ctx_destroy(avse_ctx* ctx);
  *   unfused_tail (AVSE_UNFUSED_TAIL) d_deconv6 as its own kernel (d_deconv5 activation materialised)
  *   no_halo (AVSE_NO_HALO)           video convs on k_conv (applies to weights loaded afterwards)
  *   mfma32 (AVSE_MFMA32)             32x32x16 compute waves in the stream convolutions
- *   serial / aud_side                one stream / audio encoder on the side stream
+ *   serial (AVSE_SERIAL)             the per-layer audio branch on the caller's stream (not the side stream)
  *   graph (AVSE_GRAPH)               avse_forward replays a hipGraph per argument set
  *   gemm_ksplit_cap (AVSE_GEMM_KSPLIT) cap on k_gemm's split-K factor (0 = none)
  *   dense_istft (AVSE_DENSE_ISTFT)   avse_istft through the dense pinv + frame scratch + overlap-add pass
@@ -191,7 +191,9 @@ int avse_mse(avse_ctx* ctx, const float* pred, const float* target, int64_t n, f
 /* ---- training (SpeechEnhancementNetwork.train, network.py:177-206) ---------------------- */
 
 /* One Keras fit step of the model compiled at network.py:35-36 (Adam(lr) on mean_squared_error), in float32:
- * BatchNormalization on batch statistics (biased variance, eps 1e-3) with moving-average updates (momentum 0.99),
+ * BatchNormalization on batch statistics (biased variance, eps 1e-3) with moving-average updates (momentum 0.99; the
+ * moving variance takes the BIASED batch variance as Keras 2.0.x does — Keras >= 2.1.3 applies an n / (n - 1)
+ * correction there; the reference pins only keras >= 2.0.4 (README), so which one it trained with is unpinned),
  * LeakyReLU(0.3), MaxPooling2D(2, 2), Dropout(dropout_rate) after each video pooling (the reference uses 0.25),
  * MSE over every element, Keras-2.0 Adam (beta1 0.9, beta2 0.999, epsilon 1e-8, bias-corrected step size).
  * Parameters, gradients and Adam moments are kept in the canonical blob layout of avse_weights_load. */

@@ -10,7 +10,9 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
-import avse_pkg  # noqa: E402,F401
+import avse_pkg  # noqa: E402
+
+avse_pkg.load()
 from avse_amd import ops  # noqa: E402
 from avse_amd.model import KerasModel  # noqa: E402
 from test_gpu_train import batch, rel_rms  # noqa: E402
