@@ -98,9 +98,9 @@ struct IstftArgs {
     float* frames;            // scratch [n_utt][T][N] (unfused path only)
     float* sig;               // [n_utt][hop (T - 1)]
     // fused n_fft 640 / hop 160 path: pinv(M) y = M^T (M M^T)^{-1} y with M M^T tridiagonal (adjacent Slaney
-    // triangles overlap, nothing else does), so the 321 x 80 dense pinv becomes a Thomas solve + a 2-tap expansion
-    const float4* tri;        // [n_mels] (sub-diagonal a_i, 1 / pivot_i, c'_i, 0) of the Thomas recurrence; null = dense
+    // triangles overlap, nothing else does), so the 321 x 80 dense pinv becomes an 80 x 80 solve + a 2-tap expansion
     const float4* bins;       // [nb] (M[j0][k], M[j0+1][k], j0 as int bits, 0): the <= 2 filters covering bin k
+    const float* gram_inv;    // [80][80] (M M^T)^{-1} (symmetric; the fused kernel's MFMA solve), null = Thomas
 };
 
 int launch_istft(const IstftArgs& a, hipStream_t s);

@@ -108,8 +108,8 @@ struct IstftTables {
     float* pinvT = nullptr;     // [n_mels][nb]
     float2* twiddle = nullptr;  // [N]
     float* window = nullptr;    // [N]
-    float4* tri = nullptr;      // [n_mels] Thomas coefficients of M M^T (null when it is not tridiagonal)
     float4* bins = nullptr;     // [nb] the <= 2 adjacent filters covering each bin
+    float* gram_inv = nullptr;  // [n_mels][n_mels] (M M^T)^{-1} in float (n_mels == 80 only)
 };
 
 struct avse_ctx {
@@ -330,7 +330,7 @@ int ensure_istft_tables(avse_ctx* c, int sr, int n_fft, int n_mels, double fmin,
     IstftTables& t = c->istft;
     if (t.sr == sr && t.n_fft == n_fft && t.n_mels == n_mels && t.fmin == fmin && t.fmax == fmax) return 0;
     (void)hipFree(t.pinvT); (void)hipFree(t.twiddle); (void)hipFree(t.window);
-    (void)hipFree(t.tri); (void)hipFree(t.bins);
+    (void)hipFree(t.bins); (void)hipFree(t.gram_inv);
     t = IstftTables();
     const int nb = 1 + n_fft / 2, N = 2 * (nb - 1);
     const std::vector<double> M = mel_filterbank(sr, n_fft, n_mels, fmin, fmax);
@@ -415,21 +415,51 @@ int ensure_istft_tables(avse_ctx* c, int sr, int n_fft, int n_mels, double fmin,
                 for (int k = 0; k < nb; ++k) acc += M[(size_t)i * nb + k] * M[(size_t)j * nb + k];
                 return acc;
             };
-            std::vector<float4> tri(n_mels);
+            // M M^T must be tridiagonal (adjacent Slaney triangles overlap, nothing else does) and its LU pivots
+            // non-zero: the checks that make M^T (M M^T)^{-1} = pinv(M) computable from the band-local pieces
             double cprev = 0;
             for (int i = 0; i < n_mels && ok; ++i) {
+                for (int j = 0; j < i - 1 && ok; ++j)
+                    if (gram(i, j) != 0.0) ok = false;
                 const double ai = i > 0 ? gram(i, i - 1) : 0.0, bi = gram(i, i);
                 const double ci = i + 1 < n_mels ? gram(i, i + 1) : 0.0;
                 const double piv = bi - ai * cprev;
                 if (!(std::fabs(piv) > 1e-300)) { ok = false; break; }
                 cprev = ci / piv;
-                tri[i] = make_float4((float)ai, (float)(1.0 / piv), (float)cprev, 0.f);
             }
             if (ok) {
-                AVSE_HIP_CHECK(hipMalloc(&t.tri, sizeof(float4) * n_mels));
                 AVSE_HIP_CHECK(hipMalloc(&t.bins, sizeof(float4) * nb));
-                AVSE_HIP_CHECK(hipMemcpy(t.tri, tri.data(), sizeof(float4) * n_mels, hipMemcpyHostToDevice));
                 AVSE_HIP_CHECK(hipMemcpy(t.bins, bins.data(), sizeof(float4) * nb, hipMemcpyHostToDevice));
+                if (n_mels == 80) {
+                    // (M M^T)^{-1} by Gauss-Jordan in double (the Gram matrix is symmetric positive definite, cond ~20):
+                    // the fused kernel solves all frames of a chunk at once as a [frames x 80] x [80 x 80] fp32 MFMA
+                    // product (round 2: one Thomas recurrence per frame and lane)
+                    const int n = n_mels;
+                    std::vector<double> g((size_t)n * n), inv((size_t)n * n, 0.0);
+                    for (int i = 0; i < n; ++i) {
+                        inv[(size_t)i * n + i] = 1.0;
+                        for (int j = std::max(0, i - 1); j <= std::min(n - 1, i + 1); ++j) g[(size_t)i * n + j] = gram(i, j);
+                    }
+                    for (int c = 0; c < n && ok; ++c) {
+                        const double piv = g[(size_t)c * n + c];
+                        if (!(std::fabs(piv) > 1e-300)) { ok = false; break; }
+                        for (int j = 0; j < n; ++j) { g[(size_t)c * n + j] /= piv; inv[(size_t)c * n + j] /= piv; }
+                        for (int r = 0; r < n; ++r) {
+                            if (r == c) continue;
+                            const double f = g[(size_t)r * n + c];
+                            if (f == 0.0) continue;
+                            for (int j = 0; j < n; ++j) {
+                                g[(size_t)r * n + j] -= f * g[(size_t)c * n + j];
+                                inv[(size_t)r * n + j] -= f * inv[(size_t)c * n + j];
+                            }
+                        }
+                    }
+                    if (ok) {
+                        std::vector<float> fi(inv.begin(), inv.end());
+                        AVSE_HIP_CHECK(hipMalloc(&t.gram_inv, sizeof(float) * n * n));
+                        AVSE_HIP_CHECK(hipMemcpy(t.gram_inv, fi.data(), sizeof(float) * n * n, hipMemcpyHostToDevice));
+                    }
+                }
             }
         }
     }
@@ -774,7 +804,7 @@ void avse_ctx_destroy(avse_ctx* c) {
     (void)hipFree(c->spec.twiddle); (void)hipFree(c->spec.window);
     (void)hipFree(c->spec.mel.start); (void)hipFree(c->spec.mel.width); (void)hipFree(c->spec.mel.weight);
     (void)hipFree(c->istft.pinvT); (void)hipFree(c->istft.twiddle); (void)hipFree(c->istft.window);
-    (void)hipFree(c->istft.tri); (void)hipFree(c->istft.bins);
+    (void)hipFree(c->istft.bins); (void)hipFree(c->istft.gram_inv);
     (void)hipFree(c->frames);
     (void)hipFree(c->umax);
     (void)hipFree(c->mse_partial);
@@ -901,8 +931,8 @@ int avse_istft(avse_ctx* c, const float* mel_db, const float* stft_ri, int64_t n
     a.window = c->istft.window;
     a.frames = c->frames;
     a.sig = sig;
-    a.tri = c->opt.dense_istft ? nullptr : c->istft.tri;
     a.bins = c->istft.bins;
+    a.gram_inv = c->opt.dense_istft ? nullptr : c->istft.gram_inv;
     return launch_istft(a, (hipStream_t)stream);
 }
 
@@ -1036,6 +1066,70 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
     };
     if ((rc = mark())) return rc;   // video_prep stage: now the video encoder's first launch (k_conv path only)
     if ((rc = mark())) return rc;
+    // video encoder (network.py:138-175) over n clips, activations at the arena offsets o, embedding into cat
+    auto video_encoder = [&](const float* vid, const float* vm, const float* vs, int64_t n, const size_t* o,
+                             void* cat) -> int {
+        auto vb = [&](int b) { return (void*)(c->arena + o[b]); };
+        const int v_in[6] = {B_VIN, B_V1, B_V2, B_V3, B_V4, B_V5};
+        if (L(5).halo == HALO_NONE && (rc = launch_video_prep(vid, vm, vs, vb(B_VIN), n, P.F, dt, s))) return rc;
+        for (int i = 0; i < 6; ++i) {
+            const GpuLayer& G = L(5 + i);
+            if (G.halo != HALO_NONE) {
+                HaloArgs h = (i < 5) ? halo_args(G, vb(v_in[i]), vid, vm, vs, vb(v_in[i + 1]),
+                                                 (long long)G.ho * G.wo * G.def.cout, G.def.cout, 0, n, opt)
+                                     : halo_args(G, vb(v_in[i]), vid, vm, vs, cat, CAT, G.def.cout, AEMB, n, opt);
+                rc = G.halo == HALO_V1 ? launch_conv_v1r(h, s) : launch_conv_stream(h, s);
+                if (rc || (rc = mark())) return rc;
+                continue;
+            }
+            const long long in_cs = (long long)G.def.hin * G.def.win * (i == 0 ? G.cin_pad : G.def.cin);
+            if (i == 5 && use_gemm && G.def.hin == 4 && G.def.win == 4 && G.def.cin == 512 && G.def.kh == 3 && G.def.pool &&
+                G.ph[0].kpad == 9 * 512) {
+                if ((rc = gemm(G, vb(v_in[i]), in_cs, cat, CAT, AEMB, 1, n)) || (rc = mark())) return rc;   // concat[aemb:]
+                continue;
+            }
+            ConvArgs a = (i < 5) ? conv_args(G, vb(v_in[i]), in_cs, vb(v_in[i + 1]), (long long)G.ho * G.wo * G.def.cout, G.def.cout, 0, n)
+                                 : conv_args(G, vb(v_in[i]), in_cs, cat, CAT, G.def.cout, AEMB, n);  // concat[aemb:]
+            if (i == 5) split(a);
+            if ((rc = launch_conv(a, dt, s)) || (rc = mark())) return rc;
+        }
+        return 0;
+    };
+    // all-zero video: the embedding is one constant 2048-vector, computed once per weights object by an N = 1 video
+    // encoder in the N = 1 arena layout.  It runs here, before the audio branch is launched: the per-layer audio
+    // branch runs on the side stream and its N-clip buffers overlap the N = 1 layout (round 3: a race that broke
+    // video == NULL forwards whenever the audio encoder was not the fused kernel, e.g. at 29.97 fps)
+    if (!video) {
+        const size_t es = dt == AVSE_BF16 ? 2 : 4;
+        if (!W->vzero_emb.load(std::memory_order_acquire)) {
+            std::lock_guard<std::mutex> lk(W->vzero_mu);
+            if (!W->vzero_emb.load(std::memory_order_relaxed)) {
+                hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+                AVSE_HIP_CHECK(hipStreamIsCapturing(s, &cs));
+                if (cs != hipStreamCaptureStatusNone)
+                    return fail(AVSE_ERR_INVALID, "the all-zero-video embedding must be computed before graph capture");
+                if (!c->zero_video) {
+                    AVSE_HIP_CHECK(hipMalloc((void**)&c->zero_video, sizeof(float) * 128 * 128 * 8));
+                    AVSE_HIP_CHECK(hipMemsetAsync(c->zero_video, 0, sizeof(float) * 128 * 128 * 8, s));
+                }
+                void* emb = nullptr;
+                AVSE_HIP_CHECK(hipMalloc(&emb, 2048 * es));
+                size_t o1[B_COUNT + 1];
+                arena_bytes(1, dt, opt, o1, P);
+                hipEvent_t* keep = ev;
+                const int keep_stage = stage;
+                ev = nullptr;   // the one-off N = 1 encoder is not a profiled stage
+                rc = video_encoder(c->zero_video, nullptr, nullptr, 1, o1, c->arena + o1[B_CAT]);
+                ev = keep;
+                stage = keep_stage;
+                if (rc) { (void)hipFree(emb); return rc; }
+                AVSE_HIP_CHECK(hipMemcpyAsync(emb, c->arena + o1[B_CAT] + AEMB * es, 2048 * es, hipMemcpyDeviceToDevice, s));
+                // one-time: the embedding is complete before any stream can see the pointer
+                AVSE_HIP_CHECK(hipStreamSynchronize(s));
+                W->vzero_emb.store(emb, std::memory_order_release);
+            }
+        }
+    }
     // audio encoder (network.py:88-109): one fused kernel per clip (conv_aud.hip) when the layers have the network's
     // shapes (AVSE_NO_AUDENC=1: per-layer launches); profiled, its time shows as the audio_prep stage
     bool aud_fused = false;
@@ -1093,69 +1187,11 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
         if ((rc = launch_conv(a, dt, sa)) || (rc = mark())) return rc;
     }
     if (concurrent) AVSE_HIP_CHECK(hipEventRecord(c->join, sa));
-    // video encoder (network.py:138-175) over n clips, activations at the arena offsets o, embedding into cat
-    auto video_encoder = [&](const float* vid, const float* vm, const float* vs, int64_t n, const size_t* o,
-                             void* cat) -> int {
-        auto vb = [&](int b) { return (void*)(c->arena + o[b]); };
-        const int v_in[6] = {B_VIN, B_V1, B_V2, B_V3, B_V4, B_V5};
-        if (L(5).halo == HALO_NONE && (rc = launch_video_prep(vid, vm, vs, vb(B_VIN), n, P.F, dt, s))) return rc;
-        for (int i = 0; i < 6; ++i) {
-            const GpuLayer& G = L(5 + i);
-            if (G.halo != HALO_NONE) {
-                HaloArgs h = (i < 5) ? halo_args(G, vb(v_in[i]), vid, vm, vs, vb(v_in[i + 1]),
-                                                 (long long)G.ho * G.wo * G.def.cout, G.def.cout, 0, n, opt)
-                                     : halo_args(G, vb(v_in[i]), vid, vm, vs, cat, CAT, G.def.cout, AEMB, n, opt);
-                rc = G.halo == HALO_V1 ? launch_conv_v1r(h, s) : launch_conv_stream(h, s);
-                if (rc || (rc = mark())) return rc;
-                continue;
-            }
-            const long long in_cs = (long long)G.def.hin * G.def.win * (i == 0 ? G.cin_pad : G.def.cin);
-            if (i == 5 && use_gemm && G.def.hin == 4 && G.def.win == 4 && G.def.cin == 512 && G.def.kh == 3 && G.def.pool &&
-                G.ph[0].kpad == 9 * 512) {
-                if ((rc = gemm(G, vb(v_in[i]), in_cs, cat, CAT, AEMB, 1, n)) || (rc = mark())) return rc;   // concat[aemb:]
-                continue;
-            }
-            ConvArgs a = (i < 5) ? conv_args(G, vb(v_in[i]), in_cs, vb(v_in[i + 1]), (long long)G.ho * G.wo * G.def.cout, G.def.cout, 0, n)
-                                 : conv_args(G, vb(v_in[i]), in_cs, cat, CAT, G.def.cout, AEMB, n);  // concat[aemb:]
-            if (i == 5) split(a);
-            if ((rc = launch_conv(a, dt, s)) || (rc = mark())) return rc;
-        }
-        return 0;
-    };
     if (video) {
         if ((rc = video_encoder(video, vmean, vstd, N, off, buf(B_CAT)))) return rc;
     } else {
-        // all-zero video: the embedding is one constant 2048-vector, computed once per weights object (clip 0 of an
-        // N = 1 run whose activations use the N = 1 arena layout, stream-ordered before this forward's buffers)
+        // all-zero video: broadcast the constant embedding computed above
         const size_t es = dt == AVSE_BF16 ? 2 : 4;
-        if (!W->vzero_emb.load(std::memory_order_acquire)) {
-            std::lock_guard<std::mutex> lk(W->vzero_mu);
-            if (!W->vzero_emb.load(std::memory_order_relaxed)) {
-                hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-                AVSE_HIP_CHECK(hipStreamIsCapturing(s, &cs));
-                if (cs != hipStreamCaptureStatusNone)
-                    return fail(AVSE_ERR_INVALID, "the all-zero-video embedding must be computed before graph capture");
-                if (!c->zero_video) {
-                    AVSE_HIP_CHECK(hipMalloc((void**)&c->zero_video, sizeof(float) * 128 * 128 * 8));
-                    AVSE_HIP_CHECK(hipMemsetAsync(c->zero_video, 0, sizeof(float) * 128 * 128 * 8, s));
-                }
-                void* emb = nullptr;
-                AVSE_HIP_CHECK(hipMalloc(&emb, 2048 * es));
-                size_t o1[B_COUNT + 1];
-                arena_bytes(1, dt, opt, o1, P);
-                hipEvent_t* keep = ev;
-                const int keep_stage = stage;
-                ev = nullptr;   // the one-off N = 1 encoder is not a profiled stage
-                rc = video_encoder(c->zero_video, nullptr, nullptr, 1, o1, c->arena + o1[B_CAT]);
-                ev = keep;
-                stage = keep_stage;
-                if (rc) { (void)hipFree(emb); return rc; }
-                AVSE_HIP_CHECK(hipMemcpyAsync(emb, c->arena + o1[B_CAT] + AEMB * es, 2048 * es, hipMemcpyDeviceToDevice, s));
-                // one-time: the embedding is complete before any stream can see the pointer
-                AVSE_HIP_CHECK(hipStreamSynchronize(s));
-                W->vzero_emb.store(emb, std::memory_order_release);
-            }
-        }
         if ((rc = launch_broadcast_row(W->vzero_emb.load(std::memory_order_acquire), (char*)buf(B_CAT) + AEMB * es, N, 2048 * es, CAT * es, s))) return rc;
         for (int k = 0; k < 6; ++k)
             if ((rc = mark())) return rc;   // v_conv1..v_conv6 stages (the broadcast shows as v_conv1)

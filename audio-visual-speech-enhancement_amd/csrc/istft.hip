@@ -28,7 +28,9 @@ namespace avse {
 namespace {
 
 constexpr int FPG = 3;
-constexpr int ZS = 340;
+// frame slot stride in float2: >= 340 (the 20 x 17 layout of the DFT steps); 353 makes 2 ZS = 2 (mod 32) dwords, so
+// the step-3 stores of 16 consecutive frames at one bin (ds_write_b64 lane groups) hit distinct bank pairs (340: 4-way)
+constexpr int ZS = 353;
 
 __device__ __forceinline__ float mel_at(const IstftArgs& a, long long u, int m, int t) {
     if (a.spf > 0) {
@@ -146,23 +148,61 @@ __global__ __launch_bounds__(64) void k_istft640(IstftArgs a) {
 // k_ola, and its per-bin 80-term dense pinv dot (25.7K global-load MACs per frame) was the dominant cost
 // (2.4 ms for 10k clips).  Per chunk:
 //   1. amp = 10^(dB/20) for the 24 frames -> LDS [24][80]
-//   2. y = (M M^T)^{-1} amp by the Thomas recurrence (one lane per frame, coefficients from the host)
+//   2. y = (M M^T)^{-1} amp for all 24 frames as one fp32 MFMA product with the host-inverted Gram matrix
+//      (round 2: a Thomas recurrence, one lane per frame)
 //   3. X[k] = M[j0][k] y[j0] + M[j0+1][k] y[j0+1] (pinv(M) amp = M^T y), times the mixture's unit phase,
 //      read bin-major / frame-minor (24-frame runs of the [bin][frame] STFT); folded into the 320-point
 //      complex sequence Z' of the real inverse FFT, both halves (k, 320 - k) by one lane
-//   4. the in-register 20 x 16 DFTs of K1 (3 frames per wave) -> time samples in the frame's slot
-//   5. window x overlap-add in increasing frame order / window sum-square -> the trimmed signal, coalesced
-constexpr int OF = 21;                       // output hops per chunk
+//   4. the in-register 20 x 16 DFTs of K1 (3 frames per wave) -> windowed time samples in the frame's slot
+//   5. overlap-add in increasing frame order x 1 / window sum-square (a per-position table in the interior)
+//      -> the trimmed signal, coalesced; first, the next chunk's global loads are issued (software pipeline)
+#ifndef AVSE_ISTFT_OF                         // A/B builds (tools/stft_time.py variant libraries)
+#define AVSE_ISTFT_OF 21
+#endif
+#ifndef AVSE_ISTFT_ATTR
+#define AVSE_ISTFT_ATTR
+#endif
+#ifndef AVSE_ISTFT_BPC
+#define AVSE_ISTFT_BPC 2
+#endif
+constexpr int OF = AVSE_ISTFT_OF;            // output hops per chunk
 constexpr int FW = OF + 3;                   // frames per chunk (n_fft / hop - 1 = 3 extra)
+static_assert(FW % FPG == 0, "whole waves of 3 frames");
 constexpr int IWAVES = FW / FPG;             // 8
+constexpr int NMEL = 80;                     // bands (host-checked: the fused kernel runs only for n_mels == 80)
 
 __device__ __forceinline__ void ibarrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-__global__ __launch_bounds__(64 * IWAVES) void k_istft_fused(IstftArgs a, int n_chunks, int n_items) {
+// AVSE_ISTFT_STAMP (diagnostic variant builds only, never the library): thread 0 of each block adds the s_memtime
+// cycles of every phase of every item into g_ist_stamps[block][phase]; avse_istft_stamps() copies them out
+#ifdef AVSE_ISTFT_STAMP
+__device__ unsigned long long g_ist_stamps[1024][9];
+#define IST_STAMP_INIT unsigned long long ist_t0 = __builtin_amdgcn_s_memtime();
+#define IST_STAMP(i)                                                                 \
+    if (threadIdx.x == 0) {                                                          \
+        const unsigned long long t1 = __builtin_amdgcn_s_memtime();                  \
+        g_ist_stamps[blockIdx.x & 1023][i] += t1 - ist_t0;                           \
+        ist_t0 = t1;                                                                 \
+    }
+#else
+#define IST_STAMP_INIT
+#define IST_STAMP(i)
+#endif
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t ist_rsrc(const void* base, long long bytes) {
+    const int nrec = bytes > 0x7fffff00 ? 0x7fffff00 : (int)bytes;
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, nrec, 0x00020000);
+}
+
+__global__ __launch_bounds__(64 * IWAVES) AVSE_ISTFT_ATTR void k_istft_fused(IstftArgs a, int n_chunks, int n_items) {
     __shared__ float2 zbuf[FW * ZS];            // frame f's slot: zbuf + f * ZS (Z', then 640 time samples)
-    __shared__ float amp[FW][80];               // amplitudes, then y in place
-    __shared__ float4 tri_l[80];
+    // amplitudes, then y in place; row pitch 84 floats (80 put the step-3 reads of 24 consecutive frames at one band
+    // on two banks)
+    __shared__ __attribute__((aligned(16))) float amp[FW][84];
     __shared__ float win_l[640];
+    __shared__ float ws_l[640];                 // window / 320: applied as the DFT's samples are stored
+    __shared__ float iwss_l[160];               // 1 / window sum-square of an interior sample, by position mod 160
+    __shared__ float ginv_l[NMEL * NMEL];       // (M M^T)^{-1} for the MFMA solve of step 2
     __shared__ float2 tw[640];                  // W640^k
     __shared__ float4 bins_l[321];              // per bin: the two pinv weights and the first mel band
     const int T = a.T, n_mels = a.n_mels;
@@ -170,15 +210,73 @@ __global__ __launch_bounds__(64 * IWAVES) void k_istft_fused(IstftArgs a, int n_
 
     // tables -> LDS once per (persistent) block: the DFT twiddles and bin weights were global-memory reads in
     // every item's dependency chain
-    for (int i = threadIdx.x; i < n_mels; i += 64 * IWAVES) tri_l[i] = a.tri[i];
     for (int i = threadIdx.x; i < 640; i += 64 * IWAVES) {
         win_l[i] = a.window[i];
+        ws_l[i] = a.window[i] * (1.0f / 320.0f);
         tw[i] = a.twiddle[i];
     }
     for (int i = threadIdx.x; i < 321; i += 64 * IWAVES) bins_l[i] = a.bins[i];
+    for (int i = threadIdx.x; i < NMEL * NMEL; i += 64 * IWAVES) ginv_l[i] = a.gram_inv[i];
+    for (int i = threadIdx.x; i < 160; i += 64 * IWAVES) {   // the four overlapping frames, increasing t
+        float wss = 0.f;
+#pragma unroll
+        for (int q = 3; q >= 0; --q) {
+            const float w = a.window[i + 160 * q];
+            wss += w * w;
+        }
+        iwss_l[i] = 1.0f / wss;
+    }
     __syncthreads();
 
+    // the global loads of an item (mel-dB for step 1, the mixture STFT for step 3) are issued by the previous item's
+    // step 5, before its output stores: vmcnt retires in order, so loads issued at the top of an item waited for the
+    // previous item's stores too (step 1 measured 12.4K cycles of a 47K-cycle item, tools/istft_stamps.py)
+    constexpr int IT1 = (FW * 80 + 64 * IWAVES - 1) / (64 * IWAVES);   // 4 (n_mels == 80, host-checked)
+    constexpr int IT3 = (161 * FW + 64 * IWAVES - 1) / (64 * IWAVES);  // 8
+    float mv[IT1];
+    float2 dk[IT3], dm[IT3];
+    // per-utterance buffer resources and 32-bit offsets (the 64-bit pointer math of 20 loads per lane was most of
+    // the issuing step's VALU work)
+    auto issue_loads = [&](int item) {
+        int tid = threadIdx.x;
+        asm volatile("" : "+v"(tid));
+        const int u = item / n_chunks, b = item - u * n_chunks;
+        const int t_lo = max(0, b * OF - 1);
+        const int nfr = min(T - 1, b * OF + OF + 1) - t_lo + 1;
+        const long long mel_u = a.spf > 0 ? (long long)a.n_slices * n_mels * a.spf : (long long)n_mels * T;
+        const __amdgpu_buffer_rsrc_t rsM = ist_rsrc(a.mel_db + u * mel_u, mel_u * 4);
+#pragma unroll
+        for (int j = 0; j < IT1; ++j) {
+            const int it = min(tid + 64 * IWAVES * j, FW * n_mels - 1);
+            const int m = it / FW, f = it - FW * m;
+            const int t = t_lo + min(f, nfr - 1);
+            int e;
+            if (a.spf > 0) {
+                const int sl = t / a.spf;
+                e = (sl * n_mels + m) * a.spf + (t - sl * a.spf);
+            } else {
+                e = m * T + t;
+            }
+            mv[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsM, e * 4, 0, 0));
+        }
+        const long long stft_u = (long long)a.nb * a.stft_frames;
+        const __amdgpu_buffer_rsrc_t rsD = ist_rsrc(a.stft + u * stft_u, stft_u * 8);
+#pragma unroll
+        for (int j = 0; j < IT3; ++j) {
+            const int it = tid + 64 * IWAVES * j;
+            const int k = it / FW, f = it - FW * k;
+            if (k <= 160 && f < nfr) {
+                const int ok = (k * a.stft_frames + t_lo + f) * 8;
+                const int om = ((k == 0 ? 320 : 320 - k) * a.stft_frames + t_lo + f) * 8;
+                dk[j] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rsD, ok, 0, 0));
+                dm[j] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rsD, om, 0, 0));
+            }
+        }
+    };
+    if (blockIdx.x < n_items) issue_loads(blockIdx.x);
+
     for (int item = blockIdx.x; item < n_items; item += gridDim.x) {
+        IST_STAMP_INIT
         int tid = threadIdx.x;
         asm volatile("" : "+v"(tid));           // keep index math inside the loop (see k_spec640)
         const int lane = tid & 63, wave = tid >> 6;
@@ -187,85 +285,65 @@ __global__ __launch_bounds__(64 * IWAVES) void k_istft_fused(IstftArgs a, int n_
         const int t_hi = min(T - 1, b * OF + OF + 1);
         const int nfr = t_hi - t_lo + 1;
 
-        // ---- 1. amplitudes (frame fastest: runs of consecutive frames of one band); all of a lane's loads
-        //         (clamped in range) are issued before the first is used ----
+        // ---- 1. amplitudes (frame fastest: runs of consecutive frames of one band) ----
         {
-            constexpr int IT1 = (FW * 80 + 64 * IWAVES - 1) / (64 * IWAVES);   // 4 (n_mels <= 80, host-checked)
-            float mv[IT1];
-#pragma unroll
-            for (int j = 0; j < IT1; ++j) {
-                const int it = min(tid + 64 * IWAVES * j, FW * n_mels - 1);
-                const int m = it / FW, f = it - FW * m;
-                mv[j] = mel_at(a, u, m, t_lo + min(f, nfr - 1));
-            }
 #pragma unroll
             for (int j = 0; j < IT1; ++j) {
                 const int it = tid + 64 * IWAVES * j;
                 const int m = it / FW, f = it - FW * m;
-                if (it < FW * n_mels && f < nfr) amp[f][m] = sqrtf(exp10f(0.1f * mv[j]));
+                // db_to_amplitude: 10^(dB / 20) = 2^(dB log2(10) / 20) by the hardware v_exp_f32 (1 ulp; the
+                // exp10f + sqrtf sequence was ~40 instructions): relative error ~|dB| 2^-24 log2(10) / 20 <= 1e-6
+                if (it < FW * n_mels && f < nfr) amp[f][m] = __builtin_amdgcn_exp2f(0.16609640474436813f * mv[j]);
             }
         }
         ibarrier();
-        // ---- 2. Thomas solve, lanes 0..2 of every wave = frames wave + 8 lane; 8 bands per batch of loads ----
-        if (lane < FPG) {
-            const int f = wave + IWAVES * lane;
-            if (f < nfr) {
-                float* d = amp[f];
-                float prev = 0.f;
-                for (int i0 = 0; i0 < n_mels; i0 += 8) {
-                    float dv[8];
-                    float2 cv[8];
+        IST_STAMP(0)
+        // ---- 2. y = (M M^T)^{-1} amp for the chunk's frames ----
+        // MFMA form: Y [32 frames (24 used) x 80] = A [32 x 80] x G [80 x 80], G = (M M^T)^{-1} (host, double ->
+        // float): v_mfma_f32_16x16x4_f32 (exact fp32 products) over 2 x 5 tiles, wave w < 5 owns the band tile w of
+        // both frame tiles; every operand is read into registers before the barrier, then y overwrites amp.  The
+        // Thomas chain it replaces (one lane per frame, 159 dependent steps) took 8.5K of a 34K-cycle item.
+        {
+            f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+            float fa[2][NMEL / 4], fb[NMEL / 4];
+            const int r16 = lane & 15, kq = lane >> 4;
+            if (wave < NMEL / 16) {
 #pragma unroll
-                    for (int q = 0; q < 8; ++q)
-                        if (i0 + q < n_mels) {
-                            dv[q] = d[i0 + q];
-                            cv[q] = make_float2(tri_l[i0 + q].x, tri_l[i0 + q].y);
-                        }
+                for (int st = 0; st < NMEL / 4; ++st) {
+                    fb[st] = ginv_l[(4 * st + kq) * NMEL + 16 * wave + r16];
 #pragma unroll
-                    for (int q = 0; q < 8; ++q)
-                        if (i0 + q < n_mels) {
-                            prev = (dv[q] - cv[q].x * prev) * cv[q].y;
-                            d[i0 + q] = prev;
-                        }
+                    for (int r = 0; r < 2; ++r) {
+                        const int f = 16 * r + r16;
+                        fa[r][st] = f < nfr ? amp[f < FW ? f : 0][4 * st + kq] : 0.f;
+                    }
                 }
-                for (int i1 = n_mels - 2; i1 >= 0; i1 -= 8) {
-                    float dv[8], cz[8];
+            }
+            ibarrier();
+            if (wave < NMEL / 16) {
 #pragma unroll
-                    for (int q = 0; q < 8; ++q)
-                        if (i1 - q >= 0) {
-                            dv[q] = d[i1 - q];
-                            cz[q] = tri_l[i1 - q].z;
-                        }
+                for (int st = 0; st < NMEL / 4; ++st)
 #pragma unroll
-                    for (int q = 0; q < 8; ++q)
-                        if (i1 - q >= 0) {
-                            prev = dv[q] - cz[q] * prev;
-                            d[i1 - q] = prev;
-                        }
-                }
+                    for (int r = 0; r < 2; ++r)
+                        acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[r][st], fb[st], acc[r], 0, 0, 0);
+#pragma unroll
+                for (int r = 0; r < 2; ++r)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int f = 16 * r + 4 * kq + i;
+                        if (f < nfr) amp[f][16 * wave + r16] = acc[r][i];
+                    }
             }
         }
         ibarrier();
+        IST_STAMP(1)
         // ---- 3. spectrum x unit phase, folded into Z' = conj(E + i O) (k) and E - i O (320 - k) ----
-        // All of a lane's mixture-STFT loads are issued before any is used (one HBM latency per chunk).
+        // (the mixture-STFT loads dk / dm were issued at the start of the item)
         {
-            constexpr int IT3 = (161 * FW + 64 * IWAVES - 1) / (64 * IWAVES);   // 8
-            const float2* __restrict__ D = a.stft + (long long)u * a.nb * a.stft_frames + t_lo;
-            float2 dk[IT3], dm[IT3];
 #pragma unroll
             for (int j = 0; j < IT3; ++j) {
                 const int it = tid + 64 * IWAVES * j;
                 const int k = it / FW, f = it - FW * k;
-                if (k <= 160 && f < nfr) {
-                    dk[j] = D[(long long)k * a.stft_frames + f];
-                    dm[j] = D[(long long)(k == 0 ? 320 : 320 - k) * a.stft_frames + f];
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < IT3; ++j) {
-                const int it = tid + 64 * IWAVES * j;
-                const int k = it / FW, f = it - FW * k;
-                asm volatile("" ::: "memory");           // one iteration's table loads at a time (register pressure)
+                if ((j & 1) == 0) asm volatile("" ::: "memory");   // two iterations' table loads at a time (registers)
                 if (k > 160 || f >= nfr) continue;
                 const int km = k == 0 ? 320 : 320 - k;
                 const float4 bk = bins_l[k], bm = bins_l[km];
@@ -287,6 +365,7 @@ __global__ __launch_bounds__(64 * IWAVES) void k_istft_fused(IstftArgs a, int n_
             }
         }
         ibarrier();
+        IST_STAMP(2)
         // ---- 4. forward 320-point DFT of Z' per frame (wave = 3 frames) -> windowed samples ----
         {
             const int f = FPG * wave + (lane >> 4), n1 = lane & 15;
@@ -297,6 +376,7 @@ __global__ __launch_bounds__(64 * IWAVES) void k_istft_fused(IstftArgs a, int n_
                 for (int n2 = 0; n2 < 20; ++n2) v[n2] = zbuf[f * ZS + n1 + 16 * n2];
             }
             ibarrier();
+            IST_STAMP(3)
             if (act) {
                 dft20(v, tw);
                 float2* zf = zbuf + f * ZS;
@@ -312,6 +392,7 @@ __global__ __launch_bounds__(64 * IWAVES) void k_istft_fused(IstftArgs a, int n_
             }
         }
         ibarrier();
+        IST_STAMP(4)
         {
             const int f = FPG * wave + lane / 20, k2 = lane - 20 * (lane / 20);
             const bool act = lane < 20 * FPG && f < nfr;
@@ -322,23 +403,26 @@ __global__ __launch_bounds__(64 * IWAVES) void k_istft_fused(IstftArgs a, int n_
                 for (int n1 = 0; n1 < 16; ++n1) v[n1] = zf[k2 * 17 + n1];
             }
             ibarrier();
+            IST_STAMP(5)
             if (act) {
                 dft16(v, tw);
                 float* fr = reinterpret_cast<float*>(zf);
-                const float s = 1.0f / 320.0f;
 #pragma unroll
                 for (int c = 0; c < 4; ++c)
 #pragma unroll
                     for (int d = 0; d < 4; ++d) {
-                        const int n = k2 + 20 * (c + 4 * d);       // z[n] = conj(out[n]) / 320
+                        const int n = k2 + 20 * (c + 4 * d);       // z[n] = conj(out[n]) / 320, then windowed
                         const float2 o = v[4 * c + d];
-                        fr[2 * n] = o.x * s;                          // windowed in the overlap-add
-                        fr[2 * n + 1] = -o.y * s;
+                        const float2 w = *reinterpret_cast<const float2*>(ws_l + 2 * n);
+                        fr[2 * n] = o.x * w.x;
+                        fr[2 * n + 1] = -o.y * w.y;
                     }
             }
         }
         ibarrier();
-        // ---- 5. overlap-add + window-sum-square + centre trim ----
+        IST_STAMP(6)
+        // ---- 5. overlap-add + window-sum-square + centre trim (first: the next item's loads) ----
+        if (item + (int)gridDim.x < n_items) issue_loads(item + gridDim.x);
         {
             const long long i0 = (long long)b * OF * 160;
             const int n_out = (int)min((long long)OF * 160, Lout - i0);
@@ -346,23 +430,33 @@ __global__ __launch_bounds__(64 * IWAVES) void k_istft_fused(IstftArgs a, int n_
 #pragma unroll 1
             for (int j = tid; j < n_out; j += 64 * IWAVES) {
                 const int p = (int)(i0 + j) + 320;                 // position in the untrimmed signal
-                const int tlo = max(0, (p - 640 + 160) / 160);     // first frame t with t*160 + 639 >= p
-                const int thi = min(T - 1, p / 160);
-                float yv = 0.f, wss = 0.f;
+                const int hq = p / 160, o0 = p - 160 * hq;
+                float yv = 0.f;
+                if (hq >= 3 && hq <= T - 1) {                      // interior: four frames, constant sum-square
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {                      // <= 4 frames overlap, increasing t
-                    const int t = thi - 3 + q;
-                    if (t < tlo) continue;
-                    const int o = p - 160 * t;
-                    const float w = win_l[o];
-                    yv += reinterpret_cast<const float*>(zbuf + (t - t_lo) * ZS)[o] * w;
-                    wss += w * w;
+                    for (int q = 0; q < 4; ++q)                    // increasing t = hq - 3 + q
+                        yv += reinterpret_cast<const float*>(zbuf + (hq - 3 + q - t_lo) * ZS)[o0 + 160 * (3 - q)];
+                    yv *= iwss_l[o0];
+                } else {                                           // the utterance's first / last hops
+                    const int tlo = max(0, (p - 640 + 160) / 160); // first frame t with t*160 + 639 >= p
+                    const int thi = min(T - 1, hq);
+                    float wss = 0.f;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int t = thi - 3 + q;
+                        if (t < tlo) continue;
+                        const int o = p - 160 * t;
+                        const float w = win_l[o];
+                        yv += reinterpret_cast<const float*>(zbuf + (t - t_lo) * ZS)[o];
+                        wss += w * w;
+                    }
+                    if (wss > 1.17549435e-38f) yv /= wss;
                 }
-                if (wss > 1.17549435e-38f) yv /= wss;
                 out[j] = yv;
             }
         }
         ibarrier();
+        IST_STAMP(7)
     }
 }
 
@@ -420,9 +514,22 @@ __global__ void k_ola(IstftArgs a) {
 
 }  // namespace
 
+#ifdef AVSE_ISTFT_STAMP
+extern "C" int avse_istft_stamps(unsigned long long* host, int reset) {
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ist_stamps), sizeof(unsigned long long) * 1024 * 9) != hipSuccess) return 2;
+    if (reset) {
+        static unsigned long long zero[1024 * 9];
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_ist_stamps), zero, sizeof(zero)) != hipSuccess) return 2;
+    }
+    return 0;
+}
+#endif
+
 int launch_istft(const IstftArgs& a, hipStream_t s) {
     if (a.n_utt <= 0 || a.T <= 0) return 0;
-    if (a.N == 640 && a.hop == 160 && a.tri && a.bins) {
+    // fused path: 32-bit offsets into one utterance's STFT (nb x frames x 8 B < 2 GiB: ~2 hours at 16 kHz)
+    if (a.N == 640 && a.hop == 160 && a.n_mels == NMEL && a.gram_inv && a.bins &&
+        (long long)a.nb * a.stft_frames * 8 < 0x7fffff00LL) {
         if (a.T < 2) return 0;
         const int n_chunks = (a.T - 1 + OF - 1) / OF;
         const long long items = (long long)n_chunks * a.n_utt;
@@ -433,7 +540,7 @@ int launch_istft(const IstftArgs& a, hipStream_t s) {
         int dev = 0, cus = 256;
         AVSE_HIP_CHECK(hipGetDevice(&dev));
         AVSE_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-        const int grid = (int)std::min<long long>(items, 2LL * cus);
+        const int grid = (int)std::min<long long>(items, (long long)AVSE_ISTFT_BPC * cus);
         hipLaunchKernelGGL(k_istft_fused, dim3(grid), dim3(64 * IWAVES), 0, s, a, n_chunks, (int)items);
         AVSE_HIP_CHECK(hipGetLastError());
         return 0;

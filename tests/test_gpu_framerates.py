@@ -110,3 +110,23 @@ def test_enhancer_at_2997_fps(gpu):
         err = rel_rms(got[u, :n], ref[:n])
         print(f"29.97 fps utterance {u}: waveform rel RMS {err:.2e} ({got.shape[1]} vs {len(ref)} samples)")
         assert got.shape[1] == len(ref) and err <= 1e-4, (u, err)
+
+
+def test_zero_video_with_layer_by_layer_audio_branch(gpu):
+    """video=None with the per-layer audio encoder (no_audenc: it runs on the side stream, concurrently with the
+    N = 1 encoder that computes the constant video embedding).  Round 3 found those two racing for the arena at
+    29.97 fps, where the fused audio kernel does not apply; the embedding is now computed before the audio branch
+    is launched.  25 fps, fp32 and bf16 against the oracle."""
+    from avse_amd import ops
+    from avse_amd.model import KerasModel
+    model = KerasModel.init(seed=5, randomize=True)
+    rng = np.random.default_rng(3)
+    x = synth_audio(rng, 6, 3200)
+    mel = np.stack([R.signal_to_spectrogram(x[i], 16000, 640, 160)[0][:, :20] for i in range(6)]).astype(np.float32)
+    ref = K.forward(model.layer_dict(), mel, None)
+    for dtype, tol in (("float32", 1e-5), ("bfloat16", 1.5e-2)):
+        ctx = ops.DeviceWeights(model, dtype).ctx
+        with ctx.options(no_audenc=1):
+            dw = ops.DeviceWeights(model, dtype)
+            got = ops.forward(dw, ops.to_device(mel), None).cpu().numpy()
+        assert rel_rms(got, ref) <= tol, (dtype, rel_rms(got, ref))
