@@ -196,9 +196,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t ist_rsrc(const void* base, lon
 
 __global__ __launch_bounds__(64 * IWAVES) AVSE_ISTFT_ATTR void k_istft_fused(IstftArgs a, int n_chunks, int n_items) {
     __shared__ float2 zbuf[FW * ZS];            // frame f's slot: zbuf + f * ZS (Z', then 640 time samples)
-    // amplitudes, then y in place; row pitch 84 floats (80 put the step-3 reads of 24 consecutive frames at one band
-    // on two banks)
-    __shared__ __attribute__((aligned(16))) float amp[FW][84];
+    // amplitudes, then y in place; odd row pitch (81 floats): the MFMA fragment reads (16 consecutive frames at one
+    // band) are conflict-free and step 3's frame-pair lanes 2-way (a pitch of 80 put them on 2 banks)
+    __shared__ float amp[FW][81];
     __shared__ float win_l[640];
     __shared__ float ws_l[640];                 // window / 320: applied as the DFT's samples are stored
     __shared__ float iwss_l[160];               // 1 / window sum-square of an interior sample, by position mod 160
@@ -232,48 +232,65 @@ __global__ __launch_bounds__(64 * IWAVES) AVSE_ISTFT_ATTR void k_istft_fused(Ist
     // step 5, before its output stores: vmcnt retires in order, so loads issued at the top of an item waited for the
     // previous item's stores too (step 1 measured 12.4K cycles of a 47K-cycle item, tools/istft_stamps.py)
     constexpr int IT1 = (FW * 80 + 64 * IWAVES - 1) / (64 * IWAVES);   // 4 (n_mels == 80, host-checked)
-    constexpr int IT3 = (161 * FW + 64 * IWAVES - 1) / (64 * IWAVES);  // 8
+    // step 3 works on (bin k, frame pair): the pair's two STFT values are one 16-B load (the [bin][frame] layout keeps
+    // a bin's frames adjacent); 8-B loads of single frames issued ~4.4K cycles per item (tools/istft_stamps.py)
+    constexpr int FP = FW / 2;                                          // frame pairs per chunk
+    constexpr int IT3 = (161 * FP + 64 * IWAVES - 1) / (64 * IWAVES);  // 4
     float mv[IT1];
-    float2 dk[IT3], dm[IT3];
+    float4 dk[IT3], dm[IT3];
     // per-utterance buffer resources and 32-bit offsets (the 64-bit pointer math of 20 loads per lane was most of
     // the issuing step's VALU work)
-    auto issue_loads = [&](int item) {
+    const float inv_spf = a.spf > 0 ? 1.0f / (float)a.spf : 0.f;
+    // part < 0: the mel-dB loads; part j >= 0: the STFT frame pairs of iteration j (spread over step 4's sub-steps so
+    // the texture unit streams them while the DFTs compute: issued as one burst they took ~3.2K cycles of issue)
+    auto issue_loads = [&](int item, int part) {
         int tid = threadIdx.x;
         asm volatile("" : "+v"(tid));
         const int u = item / n_chunks, b = item - u * n_chunks;
         const int t_lo = max(0, b * OF - 1);
         const int nfr = min(T - 1, b * OF + OF + 1) - t_lo + 1;
-        const long long mel_u = a.spf > 0 ? (long long)a.n_slices * n_mels * a.spf : (long long)n_mels * T;
-        const __amdgpu_buffer_rsrc_t rsM = ist_rsrc(a.mel_db + u * mel_u, mel_u * 4);
+        if (part < 0) {
+            const long long mel_u = a.spf > 0 ? (long long)a.n_slices * n_mels * a.spf : (long long)n_mels * T;
+            const __amdgpu_buffer_rsrc_t rsM = ist_rsrc(a.mel_db + u * mel_u, mel_u * 4);
 #pragma unroll
-        for (int j = 0; j < IT1; ++j) {
-            const int it = min(tid + 64 * IWAVES * j, FW * n_mels - 1);
-            const int m = it / FW, f = it - FW * m;
-            const int t = t_lo + min(f, nfr - 1);
-            int e;
-            if (a.spf > 0) {
-                const int sl = t / a.spf;
-                e = (sl * n_mels + m) * a.spf + (t - sl * a.spf);
-            } else {
-                e = m * T + t;
+            for (int j = 0; j < IT1; ++j) {
+                const int it = min(tid + 64 * IWAVES * j, FW * n_mels - 1);
+                const int m = it / FW, f = it - FW * m;
+                const int t = t_lo + min(f, nfr - 1);
+                int e;
+                if (a.spf > 0) {   // t / spf by a float reciprocal and one correction (t < 2^24)
+                    int sl = (int)((float)t * inv_spf);
+                    sl -= sl * a.spf > t;
+                    sl += (sl + 1) * a.spf <= t;
+                    e = (sl * n_mels + m) * a.spf + (t - sl * a.spf);
+                } else {
+                    e = m * T + t;
+                }
+                mv[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsM, e * 4, 0, 0));
             }
-            mv[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsM, e * 4, 0, 0));
+            return;
         }
         const long long stft_u = (long long)a.nb * a.stft_frames;
         const __amdgpu_buffer_rsrc_t rsD = ist_rsrc(a.stft + u * stft_u, stft_u * 8);
 #pragma unroll
         for (int j = 0; j < IT3; ++j) {
+            if (j != part) continue;
             const int it = tid + 64 * IWAVES * j;
-            const int k = it / FW, f = it - FW * k;
-            if (k <= 160 && f < nfr) {
+            const int k = it / FP, f = 2 * (it - FP * k);
+            if (k <= 160 && f < nfr) {   // the pair's second frame may lie past the chunk / utterance: not used
                 const int ok = (k * a.stft_frames + t_lo + f) * 8;
                 const int om = ((k == 0 ? 320 : 320 - k) * a.stft_frames + t_lo + f) * 8;
-                dk[j] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rsD, ok, 0, 0));
-                dm[j] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rsD, om, 0, 0));
+                dk[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsD, ok, 0, 0));
+                dm[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsD, om, 0, 0));
             }
         }
     };
-    if (blockIdx.x < n_items) issue_loads(blockIdx.x);
+    auto issue_all = [&](int item) {
+        issue_loads(item, -1);
+#pragma unroll
+        for (int j = 0; j < IT3; ++j) issue_loads(item, j);
+    };
+    if (blockIdx.x < n_items) issue_all(blockIdx.x);
 
     for (int item = blockIdx.x; item < n_items; item += gridDim.x) {
         IST_STAMP_INIT
@@ -342,30 +359,38 @@ __global__ __launch_bounds__(64 * IWAVES) AVSE_ISTFT_ATTR void k_istft_fused(Ist
 #pragma unroll
             for (int j = 0; j < IT3; ++j) {
                 const int it = tid + 64 * IWAVES * j;
-                const int k = it / FW, f = it - FW * k;
-                if ((j & 1) == 0) asm volatile("" ::: "memory");   // two iterations' table loads at a time (registers)
-                if (k > 160 || f >= nfr) continue;
+                const int k = it / FP, f0 = 2 * (it - FP * k);
+                if (k > 160 || f0 >= nfr) continue;
                 const int km = k == 0 ? 320 : 320 - k;
                 const float4 bk = bins_l[k], bm = bins_l[km];
                 const int jk = __float_as_int(bk.z), jm = __float_as_int(bm.z);
-                const float* y = amp[f];
-                const float ak = (jk >= 0 ? bk.x * y[jk] : 0.f) + (jk + 1 < n_mels && jk >= 0 ? bk.y * y[jk + 1] : 0.f);
-                const float am = (jm >= 0 ? bm.x * y[jm] : 0.f) + (jm + 1 < n_mels && jm >= 0 ? bm.y * y[jm + 1] : 0.f);
-                const float2 pk = unit_phase(dk[j]);
-                const float2 pm = unit_phase(dm[j]);
-                float2 xk = make_float2(ak * pk.x, ak * pk.y);
-                float2 xm = make_float2(am * pm.x, am * pm.y);
-                if (k == 0) { xk.y = 0.f; xm.y = 0.f; }           // irfft ignores the DC / Nyquist imaginary parts
-                const float2 cxm = cconj(xm);
-                const float2 E = make_float2(0.5f * (xk.x + cxm.x), 0.5f * (xk.y + cxm.y));
-                const float2 O = cmul(make_float2(0.5f * (xk.x - cxm.x), 0.5f * (xk.y - cxm.y)), cconj(tw[k]));
-                float2* zf = zbuf + f * ZS;
-                zf[k] = make_float2(E.x - O.y, -(E.y + O.x));          // conj(E + i O)
-                if (k != 0 && k != 160) zf[320 - k] = make_float2(E.x + O.y, E.y - O.x);   // E - i O
+                const float2 twk = cconj(tw[k]);
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int f = f0 + h;
+                    if (h == 1 && f >= nfr) break;
+                    const float* y = amp[f];
+                    const float ak = (jk >= 0 ? bk.x * y[jk] : 0.f) + (jk + 1 < n_mels && jk >= 0 ? bk.y * y[jk + 1] : 0.f);
+                    const float am = (jm >= 0 ? bm.x * y[jm] : 0.f) + (jm + 1 < n_mels && jm >= 0 ? bm.y * y[jm + 1] : 0.f);
+                    const float2 pk = unit_phase(h ? make_float2(dk[j].z, dk[j].w) : make_float2(dk[j].x, dk[j].y));
+                    const float2 pm = unit_phase(h ? make_float2(dm[j].z, dm[j].w) : make_float2(dm[j].x, dm[j].y));
+                    float2 xk = make_float2(ak * pk.x, ak * pk.y);
+                    float2 xm = make_float2(am * pm.x, am * pm.y);
+                    if (k == 0) { xk.y = 0.f; xm.y = 0.f; }       // irfft ignores the DC / Nyquist imaginary parts
+                    const float2 cxm = cconj(xm);
+                    const float2 E = make_float2(0.5f * (xk.x + cxm.x), 0.5f * (xk.y + cxm.y));
+                    const float2 O = cmul(make_float2(0.5f * (xk.x - cxm.x), 0.5f * (xk.y - cxm.y)), twk);
+                    float2* zf = zbuf + f * ZS;
+                    zf[k] = make_float2(E.x - O.y, -(E.y + O.x));          // conj(E + i O)
+                    if (k != 0 && k != 160) zf[320 - k] = make_float2(E.x + O.y, E.y - O.x);   // E - i O
+                }
             }
         }
         ibarrier();
         IST_STAMP(2)
+        const bool more = item + (int)gridDim.x < n_items;   // the next item's loads, spread over step 4
+        if (more) { issue_loads(item + gridDim.x, -1); issue_loads(item + gridDim.x, 0); }
+        asm volatile("" ::: "memory");
         // ---- 4. forward 320-point DFT of Z' per frame (wave = 3 frames) -> windowed samples ----
         {
             const int f = FPG * wave + (lane >> 4), n1 = lane & 15;
@@ -377,6 +402,7 @@ __global__ __launch_bounds__(64 * IWAVES) AVSE_ISTFT_ATTR void k_istft_fused(Ist
             }
             ibarrier();
             IST_STAMP(3)
+            if (more) issue_loads(item + gridDim.x, 1);
             if (act) {
                 dft20(v, tw);
                 float2* zf = zbuf + f * ZS;
@@ -393,6 +419,7 @@ __global__ __launch_bounds__(64 * IWAVES) AVSE_ISTFT_ATTR void k_istft_fused(Ist
         }
         ibarrier();
         IST_STAMP(4)
+        if (more) issue_loads(item + gridDim.x, 2);
         {
             const int f = FPG * wave + lane / 20, k2 = lane - 20 * (lane / 20);
             const bool act = lane < 20 * FPG && f < nfr;
@@ -404,6 +431,7 @@ __global__ __launch_bounds__(64 * IWAVES) AVSE_ISTFT_ATTR void k_istft_fused(Ist
             }
             ibarrier();
             IST_STAMP(5)
+            if (more) issue_loads(item + gridDim.x, 3);
             if (act) {
                 dft16(v, tw);
                 float* fr = reinterpret_cast<float*>(zf);
@@ -422,7 +450,6 @@ __global__ __launch_bounds__(64 * IWAVES) AVSE_ISTFT_ATTR void k_istft_fused(Ist
         ibarrier();
         IST_STAMP(6)
         // ---- 5. overlap-add + window-sum-square + centre trim (first: the next item's loads) ----
-        if (item + (int)gridDim.x < n_items) issue_loads(item + gridDim.x);
         {
             const long long i0 = (long long)b * OF * 160;
             const int n_out = (int)min((long long)OF * 160, Lout - i0);

@@ -18,7 +18,7 @@ sys.modules["avse_amd"]._lib.LIB_PATH = os.path.abspath(sys.argv[1])
 from avse_amd import _lib, ops  # noqa: E402
 
 PHASES = ["1 amplitudes", "2 Thomas", "3 spectrum x phase", "4a Z' -> regs", "4b dft20 -> LDS", "4c -> regs",
-          "4d dft16 -> LDS", "5 overlap-add"]
+          "4d dft16 -> LDS", "5b overlap-add", "5a next item's loads"]
 
 
 def main():
@@ -43,7 +43,7 @@ def main():
     torch.cuda.synchronize()
     fn(buf.ctypes.data, 1)
     items = U * ((300 - 1 + 20) // 21) * reps
-    tot = buf[:, :8].sum(axis=0).astype(np.float64)
+    tot = buf[:, :9].sum(axis=0).astype(np.float64)
     print(f"cycles per item (thread 0 of each block, {items} items):")
     for name, v in zip(PHASES, tot):
         print(f"  {name:22s} {v / items:9.0f}")
