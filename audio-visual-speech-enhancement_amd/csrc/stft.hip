@@ -138,8 +138,25 @@ __device__ __forceinline__ void load_frame(float2 (&x)[20], const float* __restr
 // RI: the complex STFT is stored too (bin-major over the whole chunk: block barriers between the steps).  Without it
 // every step until the top_db maximum touches only the wave's own three frames, so the waves hand off through LDS
 // wave-synchronously and one block barrier remains per item.
+// AVSE_STFT_STAMP (diagnostic variant builds only, never the library): thread 0 of every block adds the s_memtime
+// cycles of each step to its block's slot of g_spec_stamps; avse_spec_stamps() copies them out (tools/stft_stamps.py)
+#ifdef AVSE_STFT_STAMP
+__device__ unsigned long long g_spec_stamps[4096][8];   // per block slot (blockIdx % 4096): no atomics
+#define SPEC_STAMP_INIT unsigned long long spec_t0 = __builtin_amdgcn_s_memtime();
+#define SPEC_STAMP(i)                                                                \
+    if (threadIdx.x == 0) {                                                          \
+        const unsigned long long t1 = __builtin_amdgcn_s_memtime();                  \
+        g_spec_stamps[blockIdx.x & 4095][i] += t1 - spec_t0;                         \
+        spec_t0 = t1;                                                                \
+    }
+#else
+#define SPEC_STAMP_INIT
+#define SPEC_STAMP(i)
+#endif
+
 template <bool FAST_MEL, bool RI>
 __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec640(SpecArgs a, int n_chunks) {
+    SPEC_STAMP_INIT
     __shared__ float2 zbuf[WAVES * FPG * ZS];
     __shared__ float dbuf[80 * CHUNK];
     __shared__ float2 twl[640];
@@ -173,6 +190,7 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec640(SpecArgs a, in
             load_frame(x, a.sig + (long long)u * L, L, (chunk * CHUNK + g + f1) * a.hop - 320, n1, a.pad_mode);
     }
     __syncthreads();
+    SPEC_STAMP(0)
     {
         const int parity = 0;   // (wmax slot of the item)
         const int t0 = chunk * CHUNK;
@@ -202,6 +220,7 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec640(SpecArgs a, in
                 }
         }
         if constexpr (RI) lds_barrier(); else wave_lds_sync();
+        SPEC_STAMP(1)
         // ---- step 2: 16-point DFTs over n1, lane = (f, k2) ----
         {
             const int f = lane / 20, k2 = lane - 20 * (lane / 20);
@@ -213,6 +232,7 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec640(SpecArgs a, in
                 for (int n = 0; n < 16; ++n) w[n] = zf[k2 * 17 + n];
             }
             if constexpr (RI) lds_barrier(); else wave_lds_sync();
+            SPEC_STAMP(2)
             if (act) {
                 dft16(w, twl);
 #pragma unroll
@@ -221,6 +241,7 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec640(SpecArgs a, in
                     for (int d = 0; d < 4; ++d) zf[k2 + 20 * (c + 4 * d)] = w[4 * c + d];
             }
         }
+        SPEC_STAMP(3)
         if constexpr (RI) {
             lds_barrier();
             // ---- step 3: real-FFT untangling + magnitude over the chunk, item = (k, f), f fastest ----
@@ -289,6 +310,7 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec640(SpecArgs a, in
                 }
             wave_lds_sync();
         }
+        SPEC_STAMP(4)
         // ---- step 4: Slaney mel + dB, item = (f, m) ----
         float vmax = -INFINITY;
         for (int it = lane; it < ng * n_mels; it += 64) {
@@ -318,6 +340,7 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec640(SpecArgs a, in
         for (int o = 32; o > 0; o >>= 1) vmax = fmaxf(vmax, __shfl_xor(vmax, o));
         if (lane == 0) wmax[parity][wave] = vmax;
         lds_barrier();
+        SPEC_STAMP(5)
         vmax = wmax[parity][0];
 #pragma unroll
         for (int w = 1; w < WAVES; ++w) vmax = fmaxf(vmax, wmax[parity][w]);
@@ -330,6 +353,7 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec640(SpecArgs a, in
             if (oi >= 0) a.mel_db[oi] = fmaxf(dbuf[m * CHUNK + tl], floor_db);
         }
         if (!single && tid == 0) atomicMax(a.umax + u, f2ord(vmax));
+        SPEC_STAMP(6)
     }
 }
 
@@ -387,6 +411,17 @@ __global__ void k_spec_clamp(SpecArgs a) {
 }
 
 }  // namespace
+
+#ifdef AVSE_STFT_STAMP
+extern "C" int avse_spec_stamps(unsigned long long* host, int reset) {
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_spec_stamps), sizeof(unsigned long long) * 4096 * 8) != hipSuccess) return 2;
+    if (reset) {
+        static unsigned long long zero[4096 * 8];
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_spec_stamps), zero, sizeof(zero)) != hipSuccess) return 2;
+    }
+    return 0;
+}
+#endif
 
 int launch_spectrogram(const SpecArgs& a, hipStream_t s) {
     if (a.n_utt <= 0) return 0;
