@@ -67,4 +67,98 @@ __device__ __forceinline__ void dft16(float2 (&v)[16], const float2* __restrict_
     for (int c = 0; c < 4; ++c) dft4(v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3]);
 }
 
+// ---- packed-fp32 forms (v_pk_add / v_pk_mul / v_pk_fma: one instruction per complex add, two per complex product) ----
+// A complex value is one 64-bit register pair (re, im).  Auto-vectorised float2 code pairs values across different
+// complex numbers and spends ~40 % of its instructions on v_mov re-pairing (r03, K1 step 1: 211 of 532); these
+// helpers keep (re, im) together and fold the quarter turns into the op_sel / neg modifiers.
+typedef float v2f __attribute__((ext_vector_type(2)));
+
+// b + (-i) e = (b.x + e.y, b.y - e.x)
+__device__ __forceinline__ v2f pk_add_mi(v2f b, v2f e) {
+    v2f r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(b), "v"(e));
+    return r;
+}
+// b - (-i) e = (b.x - e.y, b.y + e.x)
+__device__ __forceinline__ v2f pk_sub_mi(v2f b, v2f e) {
+    v2f r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(b), "v"(e));
+    return r;
+}
+// b + conj(e), b - conj(e)
+__device__ __forceinline__ v2f pk_add_conj(v2f b, v2f e) {
+    v2f r;
+    asm("v_pk_add_f32 %0, %1, %2 neg_hi:[0,1]" : "=v"(r) : "v"(b), "v"(e));
+    return r;
+}
+__device__ __forceinline__ v2f pk_sub_conj(v2f b, v2f e) {
+    v2f r;
+    asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1]" : "=v"(r) : "v"(b), "v"(e));
+    return r;
+}
+// a * w, with wq = i w = (-w.y, w.x) supplied (a table entry or a constant): v_pk_mul + v_pk_fma
+__device__ __forceinline__ v2f pk_cmul(v2f a, v2f w, v2f wq) {
+    return __builtin_elementwise_fma(__builtin_shufflevector(a, a, 1, 1), wq, __builtin_shufflevector(a, a, 0, 0) * w);
+}
+__device__ __forceinline__ v2f pk_cmul_c(v2f a, float wr, float wi) { return pk_cmul(a, v2f{wr, wi}, v2f{-wi, wr}); }
+
+// W20^m, W16^m = e^{-2 pi i m / N} (double literals rounded to float)
+__device__ constexpr float kW20[13][2] = {
+    {1.0, 0.0}, {0.9510565162951535, -0.3090169943749474}, {0.8090169943749475, -0.5877852522924731},
+    {0.5877852522924731, -0.8090169943749475}, {0.30901699437494745, -0.9510565162951535}, {0.0, -1.0},
+    {-0.30901699437494734, -0.9510565162951536}, {-0.587785252292473, -0.8090169943749475},
+    {-0.8090169943749473, -0.5877852522924732}, {-0.9510565162951535, -0.3090169943749475}, {-1.0, 0.0},
+    {-0.9510565162951538, 0.3090169943749469}, {-0.8090169943749476, 0.587785252292473}};
+__device__ constexpr float kW16[10][2] = {
+    {1.0, 0.0}, {0.9238795325112867, -0.3826834323650898}, {0.7071067811865476, -0.7071067811865475},
+    {0.38268343236508984, -0.9238795325112867}, {0.0, -1.0}, {-0.3826834323650897, -0.9238795325112867},
+    {-0.7071067811865475, -0.7071067811865476}, {-0.9238795325112867, -0.3826834323650899}, {-1.0, 0.0},
+    {-0.9238795325112868, 0.38268343236508967}};
+
+__device__ __forceinline__ void pk_dft4(v2f& x0, v2f& x1, v2f& x2, v2f& x3) {
+    const v2f a = x0 + x2, b = x0 - x2, c = x1 + x3, e = x1 - x3;
+    x0 = a + c;
+    x2 = a - c;
+    x1 = pk_add_mi(b, e);
+    x3 = pk_sub_mi(b, e);
+}
+
+__device__ __forceinline__ void pk_dft5(v2f& x0, v2f& x1, v2f& x2, v2f& x3, v2f& x4) {
+    const float c1 = 0.30901699437494745f, c2 = -0.8090169943749475f;
+    const float s1 = 0.9510565162951535f, s2 = 0.5877852522924731f;
+    const v2f t1 = x1 + x4, t2 = x2 + x3, t3 = x1 - x4, t4 = x2 - x3;
+    const v2f a1 = __builtin_elementwise_fma(v2f(c2), t2, __builtin_elementwise_fma(v2f(c1), t1, x0));
+    const v2f a2 = __builtin_elementwise_fma(v2f(c1), t2, __builtin_elementwise_fma(v2f(c2), t1, x0));
+    const v2f p = __builtin_elementwise_fma(v2f(s2), t4, v2f(s1) * t3);
+    const v2f q = __builtin_elementwise_fma(v2f(-s1), t4, v2f(s2) * t3);
+    x0 = x0 + (t1 + t2);
+    x1 = pk_add_mi(a1, p);
+    x4 = pk_sub_mi(a1, p);
+    x2 = pk_add_mi(a2, q);
+    x3 = pk_sub_mi(a2, q);
+}
+
+// dft20 / dft16 above in packed form, twiddles as constants
+__device__ __forceinline__ void pk_dft20(v2f (&v)[20]) {
+#pragma unroll
+    for (int b = 0; b < 5; ++b) pk_dft4(v[b], v[5 + b], v[10 + b], v[15 + b]);
+#pragma unroll
+    for (int b = 1; b < 5; ++b)
+#pragma unroll
+        for (int c = 1; c < 4; ++c) v[5 * c + b] = pk_cmul_c(v[5 * c + b], kW20[b * c][0], kW20[b * c][1]);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) pk_dft5(v[5 * c], v[5 * c + 1], v[5 * c + 2], v[5 * c + 3], v[5 * c + 4]);
+}
+
+__device__ __forceinline__ void pk_dft16(v2f (&v)[16]) {
+#pragma unroll
+    for (int b = 0; b < 4; ++b) pk_dft4(v[b], v[4 + b], v[8 + b], v[12 + b]);
+#pragma unroll
+    for (int b = 1; b < 4; ++b)
+#pragma unroll
+        for (int c = 1; c < 4; ++c) v[4 * c + b] = pk_cmul_c(v[4 * c + b], kW16[b * c][0], kW16[b * c][1]);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) pk_dft4(v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3]);
+}
+
 }  // namespace avse

@@ -357,6 +357,240 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec640(SpecArgs a, in
     }
 }
 
+// The 200-ms segment case (configs[1]: every utterance is exactly one 3200-sample / 21-frame chunk, no complex output,
+// padded Slaney rows): a persistent kernel, 2 blocks per CU looping over utterances.
+//  - the tables are staged once per block instead of once per utterance (stamps, r03: about a third of k_spec640's
+//    block time was that prologue plus the sample-load latency);
+//  - a wave's 3 frames span 960 padded samples: the next utterance's span goes straight into the wave's own zbuf region
+//    by LDS-DMA (buffer loads with the LDS flag, no VGPRs; reflect padding resolved by the two edge waves) as soon as
+//    step 4 has read it, so the load runs under the store pass and the other block's work;
+//  - packed-fp32 FFT (fft_common.h pk_*): complex adds are one v_pk_add, products v_pk_mul + v_pk_fma against
+//    (w, i w) table pairs or constants, quarter turns in the op_sel / neg modifiers (1,524 -> ~1,000 VALU per wave
+//    and utterance);
+//  - the dB values stay in the wave's region (no dbuf), and the sliced output is written as float4.
+// Two block barriers per utterance (dB reuse, dB maximum).
+#ifndef AVSE_SEG_BPC
+#define AVSE_SEG_BPC 2
+#endif
+constexpr int SEG_L = 3200;
+constexpr int SEG_DB = 1024;   // float offset of a wave's dB values in its zbuf region (samples: [0, 960))
+
+__device__ __forceinline__ void seg_dma(float* sb, const float* __restrict__ sg, int wave, int lane, int pad_mode) {
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(sg), (short)0, SEG_L * 4, 0x00020000);
+    const int base = FPG * wave * 160 - 320;   // sample index of buffer slot 0
+    typedef __attribute__((address_space(3))) void* lds_ptr;
+    if (wave != 0 && wave != WAVES - 1) {      // (wave-uniform) interior: base .. base + 1023 inside the utterance
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr)(sb + 256 * j), 16, (base + 4 * lane) * 4, 1024 * j, 0, 0);
+    } else {   // one dword per lane; zero padding reads past the buffer's range (returns 0)
+#pragma unroll
+        for (int j = 0; j < 15; ++j) {
+            bool keep;
+            const int i = padded_index(base + 64 * j + lane, SEG_L, pad_mode, keep);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr)(sb + 64 * j), 4, keep ? i * 4 : 0x40000000, 0, 0, 0);
+        }
+    }
+}
+
+__global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec_seg(SpecArgs a) {
+    SPEC_STAMP_INIT
+    __shared__ v2f zbuf[WAVES * FPG * ZS];
+    __shared__ float4 tw4[320];    // W320^j, i W320^j (step 1)
+    __shared__ float4 ut4[161];    // U = -i W640^k / 2, i U (untangling)
+    __shared__ v2f winl[320];
+    __shared__ float4 melw4[80 * MW / 4];
+    __shared__ int mel_st[80];
+    __shared__ float wmax[WAVES];
+    static_assert(FPG * ZS * 2 >= SEG_DB + FPG * 80, "sample buffer and dB values live in the wave's zbuf region");
+
+    int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int n_mels = a.n_mels;
+    for (int i = tid; i < 320; i += 64 * WAVES) {
+        const float2 w = a.twiddle[2 * i];
+        tw4[i] = make_float4(w.x, w.y, -w.y, w.x);
+        winl[i] = reinterpret_cast<const v2f*>(a.window)[i];
+    }
+    for (int k = tid; k < 161; k += 64 * WAVES) {
+        const float2 w = a.twiddle[k];
+        ut4[k] = make_float4(0.5f * w.y, -0.5f * w.x, 0.5f * w.x, 0.5f * w.y);
+    }
+    for (int i = tid; i < n_mels * MW / 4; i += 64 * WAVES) melw4[i] = reinterpret_cast<const float4*>(a.mel_weight)[i];
+    for (int i = tid; i < n_mels; i += 64 * WAVES) mel_st[i] = a.mel_start[i];
+
+    v2f* zw = zbuf + wave * FPG * ZS;
+    float* zwf = reinterpret_cast<float*>(zw);
+    const long long n_utt = a.n_utt;
+    long long u = blockIdx.x;
+    if (u < n_utt) seg_dma(zwf, a.sig + u * SEG_L, wave, tid & 63, a.pad_mode);
+    for (; u < n_utt; u += gridDim.x) {
+        // the per-lane index math stays inside the loop: hoisted out of it, the loop-invariant addresses held more
+        // registers than the 128 of two blocks per CU (k_spec640's note)
+        asm volatile("" : "+v"(tid));
+        const int lane = tid & 63;
+        const int f1 = lane >> 4, n1 = lane & 15;
+        const long long nx = u + gridDim.x;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's samples have landed (wave-local buffer)
+        lds_barrier();                                        // the previous utterance's dB / wmax reads are done
+        SPEC_STAMP(0)
+        // ---- step 1: windowed 20-point DFTs over n2, lane = (f, n1) ----
+        v2f v[20];
+        {
+            const v2f* xs = zw + f1 * 80 + n1;   // padded samples 160 f1 + 2 (n1 + 16 n2) + {0, 1}
+#pragma unroll
+            for (int n2 = 0; n2 < 20; ++n2) v[n2] = xs[16 * n2];
+        }
+        wave_lds_sync();   // every lane's samples are read before the wave overwrites the buffer
+#pragma unroll
+        for (int n2 = 0; n2 < 20; ++n2) v[n2] *= winl[n1 + 16 * n2];
+        if (f1 < FPG) {
+            pk_dft20(v);
+            // v[5c + d] = Y[c + 4d]; twiddle W320^{n1 k2}
+            v2f* zf = zw + f1 * ZS;
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+#pragma unroll
+                for (int d = 0; d < 5; ++d) {
+                    const int k2 = c + 4 * d;
+                    v2f y = v[5 * c + d];
+                    if (k2) {
+                        const float4 t = tw4[n1 * k2];
+                        y = pk_cmul(y, v2f{t.x, t.y}, v2f{t.z, t.w});
+                    }
+                    zf[k2 * 17 + n1] = y;
+                }
+        }
+        wave_lds_sync();
+        SPEC_STAMP(1)
+        // ---- step 2: 16-point DFTs over n1, lane = (f, k2) -> Z[k2 + 20 k1] ----
+        {
+            const int f = lane / 20, k2 = lane - 20 * (lane / 20);
+            const bool act = f < FPG;
+            v2f w[16];
+            v2f* zf = zw + min(f, FPG - 1) * ZS;
+            if (act) {
+#pragma unroll
+                for (int n = 0; n < 16; ++n) w[n] = zf[k2 * 17 + n];
+            }
+            wave_lds_sync();
+            if (act) {
+                pk_dft16(w);
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+#pragma unroll
+                    for (int d = 0; d < 4; ++d) zf[k2 + 20 * (c + 4 * d)] = w[4 * c + d];
+            }
+        }
+        wave_lds_sync();
+        SPEC_STAMP(2)
+        // ---- step 3: real-FFT untangling + magnitudes, item = (f, k): |X[k]|, |X[320 - k]| ----
+        {
+            constexpr int IT3 = (FPG * 161 + 63) / 64;   // 8
+            float mk[IT3], mm[IT3];
+#pragma unroll
+            for (int j = 0; j < IT3; ++j) {
+                const int it = lane + 64 * j;
+                if (it >= FPG * 161) break;
+                const int f = it / 161, k = it - 161 * f;
+                const v2f* zf = zw + f * ZS;
+                const v2f zk = zf[k], zm = zf[k == 0 ? 0 : 320 - k];
+                const float4 U = ut4[k];
+                // X[k] = E + W^k O, conj X[320 - k] = E - W^k O;  E = (Zk + conj Zm) / 2, W^k O = U (Zk - conj Zm)
+                const v2f S = pk_add_conj(zk, zm);
+                const v2f WO = pk_cmul(pk_sub_conj(zk, zm), v2f{U.x, U.y}, v2f{U.z, U.w});
+                const v2f X = __builtin_elementwise_fma(v2f(0.5f), S, WO);
+                const v2f Y = __builtin_elementwise_fma(v2f(0.5f), S, -WO);
+                const v2f X2 = X * X, Y2 = Y * Y;
+                mk[j] = __builtin_amdgcn_sqrtf(X2.x + X2.y);
+                mm[j] = __builtin_amdgcn_sqrtf(Y2.x + Y2.y);
+            }
+            wave_lds_sync();
+#pragma unroll
+            for (int j = 0; j < IT3; ++j) {
+                const int it = lane + 64 * j;
+                if (it >= FPG * 161) break;
+                const int f = it / 161, k = it - 161 * f;
+                float* mf = zwf + f * (2 * ZS);
+                mf[k] = mk[j];
+                mf[320 - k] = mm[j];
+            }
+            for (int it = lane; it < FPG * MW; it += 64) {   // bins [321, 321 + MW) read by the padded band dots
+                const int f = it / MW, j = it - MW * f;
+                zwf[f * (2 * ZS) + 321 + j] = 0.f;
+            }
+            wave_lds_sync();
+        }
+        SPEC_STAMP(3)
+        // ---- step 4: Slaney mel + dB, item = (f, m) ----
+        float vmax = -INFINITY;
+        float db[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int it = lane + 64 * j;
+            db[j] = -INFINITY;
+            if (it >= FPG * n_mels) continue;
+            const int f = it >= n_mels ? (it >= 2 * n_mels ? 2 : 1) : 0, m = it - __mul24(n_mels, f);
+            const float* mf = zwf + f * (2 * ZS) + mel_st[m];
+            const float4* wm = melw4 + m * (MW / 4);
+            float acc = 0.f;
+#pragma unroll
+            for (int q = 0; q < MW / 4; ++q) {
+                const float4 w = wm[q];
+                acc = fmaf(mf[4 * q], w.x, acc);
+                acc = fmaf(mf[4 * q + 1], w.y, acc);
+                acc = fmaf(mf[4 * q + 2], w.z, acc);
+                acc = fmaf(mf[4 * q + 3], w.w, acc);
+            }
+            db[j] = acc > a.amin ? 6.0205999132796239f * __log2f(acc) : a.db_floor;
+            vmax = fmaxf(vmax, db[j]);
+        }
+        wave_lds_sync();   // the magnitude reads are done: the region takes the dB values and the next samples
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int it = lane + 64 * j;
+            if (it >= FPG * n_mels) continue;
+            const int f = it >= n_mels ? (it >= 2 * n_mels ? 2 : 1) : 0, m = it - __mul24(n_mels, f);
+            zwf[SEG_DB + f * 80 + m] = db[j];
+        }
+        if (nx < n_utt) seg_dma(zwf, a.sig + nx * SEG_L, wave, lane, a.pad_mode);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) vmax = fmaxf(vmax, __shfl_xor(vmax, o));
+        if (lane == 0) wmax[wave] = vmax;
+        lds_barrier();
+        SPEC_STAMP(4)
+        vmax = wmax[0];
+#pragma unroll
+        for (int w = 1; w < WAVES; ++w) vmax = fmaxf(vmax, wmax[w]);
+        const float floor_db = a.top_db >= 0.f ? vmax - a.top_db : -INFINITY;
+        // dB(m, t) of frame t = 3 w + f sits at zb[w 2 FPG ZS + f 80 + m] = zb[1800 w + 80 t + m]; w = t / 3 = (11 t) >> 5 and
+        // the other small divisions by 24-bit multiplies (the generic ones were 64-bit mul_lo / mul_hi sequences)
+        const float* zb = reinterpret_cast<const float*>(zbuf) + SEG_DB;
+        static_assert(2 * FPG * ZS - 3 * 80 == 1800, "dB layout");
+        if (a.spf == 20) {   // one 20-frame slice: out[u][0][m][t], t < 20 (frame 20 dropped), float4 over t
+            float4* o = reinterpret_cast<float4*>(a.mel_db + u * (long long)n_mels * 20);
+            for (int it = tid; it < n_mels * 5; it += 64 * WAVES) {
+                const int m = __umul24(it, 205) >> 10, t0 = 4 * (it - 5 * m);   // it < 400
+                float r[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int t = t0 + e;
+                    r[e] = fmaxf(zb[__umul24(__umul24(t, 11) >> 5, 1800) + 80 * t + m], floor_db);
+                }
+                o[it] = make_float4(r[0], r[1], r[2], r[3]);
+            }
+        } else {             // plain [n_mels][21]
+            float* o = a.mel_db + u * (long long)n_mels * CHUNK;
+            for (int it = tid; it < n_mels * CHUNK; it += 64 * WAVES) {
+                const int m = __umul24(it, 3121) >> 16, t = it - CHUNK * m;   // it < 1680
+                o[it] = fmaxf(zb[__umul24(__umul24(t, 11) >> 5, 1800) + 80 * t + m], floor_db);
+            }
+        }
+        SPEC_STAMP(5)
+    }
+}
+
 // Direct DFT fallback for n_fft != 640: one 256-thread block per (frame, utterance).
 __global__ __launch_bounds__(256) void k_spec_dft(SpecArgs a) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -436,6 +670,19 @@ int launch_spectrogram(const SpecArgs& a, hipStream_t s) {
         if (n_chunks > 1) AVSE_HIP_CHECK(hipMemsetAsync(a.umax, 0, sizeof(unsigned) * a.n_utt, s));
         const bool fast = a.n_mels <= 80 && a.mel_max_width == MW, ri = a.stft_ri != nullptr;
         const dim3 grid((unsigned)items), block(64 * WAVES);
+#ifndef AVSE_NO_SEG
+        if (fast && !ri && a.n_samples == SEG_L && a.n_frames == CHUNK && a.hop == 160 &&
+            ((reinterpret_cast<uintptr_t>(a.sig) | reinterpret_cast<uintptr_t>(a.mel_db)) & 15) == 0 &&
+            (a.spf == 0 || (a.spf == 20 && a.n_slices == 1))) {
+            int dev = 0, cus = 256;
+            AVSE_HIP_CHECK(hipGetDevice(&dev));
+            AVSE_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+            const unsigned g = (unsigned)std::min<long long>(a.n_utt, (long long)AVSE_SEG_BPC * cus);
+            hipLaunchKernelGGL(k_spec_seg, dim3(g), block, 0, s, a);
+            AVSE_HIP_CHECK(hipGetLastError());
+            return 0;
+        }
+#endif
         if (fast && ri) hipLaunchKernelGGL((k_spec640<true, true>), grid, block, 0, s, a, n_chunks);
         else if (fast) hipLaunchKernelGGL((k_spec640<true, false>), grid, block, 0, s, a, n_chunks);
         else if (ri) hipLaunchKernelGGL((k_spec640<false, true>), grid, block, 0, s, a, n_chunks);

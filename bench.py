@@ -123,7 +123,7 @@ def leg_stft(dev, reps=50, B=4096, sets=5):
     ms = e0.elapsed_time(e1) / reps
     gbs = STFT_BYTES_PER_CLIP * B / (ms * 1e-3) / 1e9
     return {"config": "BASELINE configs[1]: STFT only (n_fft 640, hop 160, 80 mel, dB, top_db), batch 4096 segments",
-            "kernel": "k_spec640", "ms_per_launch": round(ms, 4), "clips_per_s": round(B / (ms * 1e-3), 1),
+            "kernel": "k_spec_seg", "ms_per_launch": round(ms, 4), "clips_per_s": round(B / (ms * 1e-3), 1),
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": round(gbs / PEAK_HBM_GBS, 4), "bytes_per_launch": STFT_BYTES_PER_CLIP * B},
             "buffer_sets": sets, "working_set_mb": round(sets * B * STFT_BYTES_PER_CLIP / 1e6, 1), "reps": reps}

@@ -35,7 +35,7 @@ def test_library_is_gfx950_code_object():
     from avse_amd import _lib
     data = open(_lib.LIB_PATH, "rb").read()
     assert b"gfx950" in data
-    assert b"k_spec640" in data and b"k_conv" in data
+    assert b"k_spec640" in data and b"k_spec_seg" in data and b"k_conv" in data
 
 
 def test_abi_version_and_blob_size():
