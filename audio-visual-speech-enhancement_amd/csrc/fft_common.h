@@ -101,6 +101,14 @@ __device__ __forceinline__ v2f pk_cmul(v2f a, v2f w, v2f wq) {
     return __builtin_elementwise_fma(__builtin_shufflevector(a, a, 1, 1), wq, __builtin_shufflevector(a, a, 0, 0) * w);
 }
 __device__ __forceinline__ v2f pk_cmul_c(v2f a, float wr, float wi) { return pk_cmul(a, v2f{wr, wi}, v2f{-wi, wr}); }
+// a * w from w alone: (a.x w.x, a.x w.y) by v_pk_mul, then + (a.y (-w.y), a.y w.x) by one v_pk_fma whose op_sel swaps
+// w's halves and whose neg_lo negates the swapped-in w.y (twiddle tables stay float2: half the LDS bytes of (w, i w))
+__device__ __forceinline__ v2f pk_cmul_t(v2f a, v2f w) {
+    const v2f t = __builtin_shufflevector(a, a, 0, 0) * w;
+    v2f r;
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]" : "=v"(r) : "v"(a), "v"(w), "v"(t));
+    return r;
+}
 
 // W20^m, W16^m = e^{-2 pi i m / N} (double literals rounded to float)
 __device__ constexpr float kW20[13][2] = {

@@ -395,24 +395,26 @@ __global__ __launch_bounds__(64 * IWAVES) AVSE_ISTFT_ATTR void k_istft_fused(Ist
         {
             const int f = FPG * wave + (lane >> 4), n1 = lane & 15;
             const bool act = (lane >> 4) < FPG && f < nfr;
-            float2 v[20];
+            v2f v[20];   // packed-fp32 DFT (fft_common.h pk_*)
             if (act) {
+                const v2f* zv = reinterpret_cast<const v2f*>(zbuf) + f * ZS + n1;
 #pragma unroll
-                for (int n2 = 0; n2 < 20; ++n2) v[n2] = zbuf[f * ZS + n1 + 16 * n2];
+                for (int n2 = 0; n2 < 20; ++n2) v[n2] = zv[16 * n2];
             }
             ibarrier();
             IST_STAMP(3)
             if (more) issue_loads(item + gridDim.x, 1);
             if (act) {
-                dft20(v, tw);
-                float2* zf = zbuf + f * ZS;
+                pk_dft20(v);
+                v2f* zf = reinterpret_cast<v2f*>(zbuf) + f * ZS;
+                const v2f* twv = reinterpret_cast<const v2f*>(tw);
 #pragma unroll
                 for (int c = 0; c < 4; ++c)
 #pragma unroll
                     for (int d = 0; d < 5; ++d) {
                         const int k2 = c + 4 * d;
-                        float2 yv = v[5 * c + d];
-                        if (k2) yv = cmul(yv, tw[(2 * n1 * k2) % 640]);
+                        v2f yv = v[5 * c + d];
+                        if (k2) yv = pk_cmul_t(yv, twv[2 * n1 * k2]);   // W320^{n1 k2}, 2 n1 k2 <= 570
                         zf[k2 * 17 + n1] = yv;
                     }
             }
@@ -423,27 +425,27 @@ __global__ __launch_bounds__(64 * IWAVES) AVSE_ISTFT_ATTR void k_istft_fused(Ist
         {
             const int f = FPG * wave + lane / 20, k2 = lane - 20 * (lane / 20);
             const bool act = lane < 20 * FPG && f < nfr;
-            float2 v[16];
+            v2f v[16];
             float2* zf = zbuf + min(f, FW - 1) * ZS;
             if (act) {
+                const v2f* zv = reinterpret_cast<const v2f*>(zf) + k2 * 17;
 #pragma unroll
-                for (int n1 = 0; n1 < 16; ++n1) v[n1] = zf[k2 * 17 + n1];
+                for (int n1 = 0; n1 < 16; ++n1) v[n1] = zv[n1];
             }
             ibarrier();
             IST_STAMP(5)
             if (more) issue_loads(item + gridDim.x, 3);
             if (act) {
-                dft16(v, tw);
+                pk_dft16(v);
                 float* fr = reinterpret_cast<float*>(zf);
 #pragma unroll
                 for (int c = 0; c < 4; ++c)
 #pragma unroll
                     for (int d = 0; d < 4; ++d) {
                         const int n = k2 + 20 * (c + 4 * d);       // z[n] = conj(out[n]) / 320, then windowed
-                        const float2 o = v[4 * c + d];
-                        const float2 w = *reinterpret_cast<const float2*>(ws_l + 2 * n);
-                        fr[2 * n] = o.x * w.x;
-                        fr[2 * n + 1] = -o.y * w.y;
+                        const v2f o = v[4 * c + d];
+                        const v2f w = *reinterpret_cast<const v2f*>(ws_l + 2 * n);
+                        *reinterpret_cast<v2f*>(fr + 2 * n) = o * v2f{w.x, -w.y};
                     }
             }
         }

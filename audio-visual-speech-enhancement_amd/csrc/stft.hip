@@ -311,7 +311,8 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec640(SpecArgs a, in
             wave_lds_sync();
         }
         SPEC_STAMP(4)
-        // ---- step 4: Slaney mel + dB, item = (f, m) ----
+        // ---- step 4: Slaney mel + dB, item = (m, f), f fastest: the three lanes of a band read its weights at one LDS
+        // address (broadcast; 0.0983 -> 0.094 ms with the float2 twiddle tables) ----
         float vmax = -INFINITY;
         for (int it = lane; it < ng * n_mels; it += 64) {
             const int f = it >= n_mels ? (it >= 2 * n_mels ? 2 : 1) : 0, m = it - n_mels * f;
@@ -364,11 +365,15 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec640(SpecArgs a, in
 //  - a wave's 3 frames span 960 padded samples: the next utterance's span goes straight into the wave's own zbuf region
 //    by LDS-DMA (buffer loads with the LDS flag, no VGPRs; reflect padding resolved by the two edge waves) as soon as
 //    step 4 has read it, so the load runs under the store pass and the other block's work;
-//  - packed-fp32 FFT (fft_common.h pk_*): complex adds are one v_pk_add, products v_pk_mul + v_pk_fma against
-//    (w, i w) table pairs or constants, quarter turns in the op_sel / neg modifiers (1,524 -> ~1,000 VALU per wave
-//    and utterance);
+//  - packed-fp32 FFT (fft_common.h pk_*): complex adds are one v_pk_add, products v_pk_mul + v_pk_fma with the
+//    quarter turns and the (re, im) swap in the op_sel / neg modifiers, so twiddle tables stay float2 (1,524 -> ~800
+//    VALU per wave and utterance, PMC);
 //  - the dB values stay in the wave's region (no dbuf), and the sliced output is written as float4.
 // Two block barriers per utterance (dB reuse, dB maximum).
+// Tried (r03): the mel product on the matrix cores ([21 frames x bins] x [bins x 16-band tiles], v_mfma_f32_16x16x4f32,
+// B fragments evaluated from the triangle coefficients, one tile job per wave, a third barrier): 0.0941 vs 0.0928 ms.
+// f32 MFMA runs at the f32 VALU rate and the dense tiles carry ~2x the sparse band FMAs; the gain in LDS gathers
+// was eaten by the job imbalance (39-42 dependent MFMAs on the longest waves) at the extra barrier.
 #ifndef AVSE_SEG_BPC
 #define AVSE_SEG_BPC 2
 #endif
@@ -397,8 +402,8 @@ __device__ __forceinline__ void seg_dma(float* sb, const float* __restrict__ sg,
 __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec_seg(SpecArgs a) {
     SPEC_STAMP_INIT
     __shared__ v2f zbuf[WAVES * FPG * ZS];
-    __shared__ float4 tw4[320];    // W320^j, i W320^j (step 1)
-    __shared__ float4 ut4[161];    // U = -i W640^k / 2, i U (untangling)
+    __shared__ v2f tw2[320];       // W320^j (step 1)
+    __shared__ v2f ut2[161];       // U = -i W640^k / 2 (untangling)
     __shared__ v2f winl[320];
     __shared__ float4 melw4[80 * MW / 4];
     __shared__ int mel_st[80];
@@ -410,12 +415,12 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec_seg(SpecArgs a) {
     const int n_mels = a.n_mels;
     for (int i = tid; i < 320; i += 64 * WAVES) {
         const float2 w = a.twiddle[2 * i];
-        tw4[i] = make_float4(w.x, w.y, -w.y, w.x);
+        tw2[i] = v2f{w.x, w.y};
         winl[i] = reinterpret_cast<const v2f*>(a.window)[i];
     }
     for (int k = tid; k < 161; k += 64 * WAVES) {
         const float2 w = a.twiddle[k];
-        ut4[k] = make_float4(0.5f * w.y, -0.5f * w.x, 0.5f * w.x, 0.5f * w.y);
+        ut2[k] = v2f{0.5f * w.y, -0.5f * w.x};
     }
     for (int i = tid; i < n_mels * MW / 4; i += 64 * WAVES) melw4[i] = reinterpret_cast<const float4*>(a.mel_weight)[i];
     for (int i = tid; i < n_mels; i += 64 * WAVES) mel_st[i] = a.mel_start[i];
@@ -455,10 +460,7 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec_seg(SpecArgs a) {
                 for (int d = 0; d < 5; ++d) {
                     const int k2 = c + 4 * d;
                     v2f y = v[5 * c + d];
-                    if (k2) {
-                        const float4 t = tw4[n1 * k2];
-                        y = pk_cmul(y, v2f{t.x, t.y}, v2f{t.z, t.w});
-                    }
+                    if (k2) y = pk_cmul_t(y, tw2[n1 * k2]);
                     zf[k2 * 17 + n1] = y;
                 }
         }
@@ -496,10 +498,9 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec_seg(SpecArgs a) {
                 const int f = it / 161, k = it - 161 * f;
                 const v2f* zf = zw + f * ZS;
                 const v2f zk = zf[k], zm = zf[k == 0 ? 0 : 320 - k];
-                const float4 U = ut4[k];
                 // X[k] = E + W^k O, conj X[320 - k] = E - W^k O;  E = (Zk + conj Zm) / 2, W^k O = U (Zk - conj Zm)
                 const v2f S = pk_add_conj(zk, zm);
-                const v2f WO = pk_cmul(pk_sub_conj(zk, zm), v2f{U.x, U.y}, v2f{U.z, U.w});
+                const v2f WO = pk_cmul_t(pk_sub_conj(zk, zm), ut2[k]);
                 const v2f X = __builtin_elementwise_fma(v2f(0.5f), S, WO);
                 const v2f Y = __builtin_elementwise_fma(v2f(0.5f), S, -WO);
                 const v2f X2 = X * X, Y2 = Y * Y;
@@ -523,7 +524,8 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec_seg(SpecArgs a) {
             wave_lds_sync();
         }
         SPEC_STAMP(3)
-        // ---- step 4: Slaney mel + dB, item = (f, m) ----
+        // ---- step 4: Slaney mel + dB, item = (m, f), f fastest: the three lanes of a band read its weights at one LDS
+        // address (broadcast; 0.0983 -> 0.094 ms with the float2 twiddle tables) ----
         float vmax = -INFINITY;
         float db[4];
 #pragma unroll
@@ -531,7 +533,7 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec_seg(SpecArgs a) {
             const int it = lane + 64 * j;
             db[j] = -INFINITY;
             if (it >= FPG * n_mels) continue;
-            const int f = it >= n_mels ? (it >= 2 * n_mels ? 2 : 1) : 0, m = it - __mul24(n_mels, f);
+            const int m = __umul24(it, 43691) >> 17, f = it - 3 * m;   // m = it / 3 (it < 240)
             const float* mf = zwf + f * (2 * ZS) + mel_st[m];
             const float4* wm = melw4 + m * (MW / 4);
             float acc = 0.f;
@@ -551,7 +553,7 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec_seg(SpecArgs a) {
         for (int j = 0; j < 4; ++j) {
             const int it = lane + 64 * j;
             if (it >= FPG * n_mels) continue;
-            const int f = it >= n_mels ? (it >= 2 * n_mels ? 2 : 1) : 0, m = it - __mul24(n_mels, f);
+            const int m = __umul24(it, 43691) >> 17, f = it - 3 * m;
             zwf[SEG_DB + f * 80 + m] = db[j];
         }
         if (nx < n_utt) seg_dma(zwf, a.sig + nx * SEG_L, wave, lane, a.pad_mode);

@@ -137,3 +137,21 @@ def test_config2_batch_4096(gpu):
     np.testing.assert_array_equal(got[:, 0], full[:, :, :20])
     for u in sorted(set(np.linspace(0, 4095, 256).astype(int))):
         _check_db(got[u], R.preprocess_audio_signal(x[u], 16000, 200, 1, 25.0))
+
+
+@pytest.mark.parametrize("n_mels,fmin,fmax,sr,top_db", [(64, 0.0, 8000.0, 16000, 80.0), (80, 50.0, 7600.0, 16000, 80.0),
+                                                       (72, 0.0, 11025.0, 22050, None), (17, 0.0, 8000.0, 16000, 60.0)])
+def test_segment_kernel_other_banks(gpu, n_mels, fmin, fmax, sr, top_db):
+    """200-ms segments (3200 samples, n_fft 640, hop 160) with other Slaney banks against the restated librosa chain:
+    banks whose bands fit the padded 24-bin rows run the segment kernel k_spec_seg (80 bands from 50 Hz), wider ones
+    (17 / 64 bands, 72 at 22.05 kHz) k_spec640's generic band loop; top_db off and at 60 dB."""
+    ops = _ops()
+    rng = np.random.default_rng(11)
+    x = synth_audio(rng, 40, 3200)
+    got = ops.spectrogram(torch.from_numpy(x).to(gpu), sample_rate=sr, n_mels=n_mels, fmin=fmin, fmax=fmax,
+                          top_db=top_db).cpu().numpy()
+    assert got.shape == (40, n_mels, 21)
+    fb = R.mel_filterbank(sr, 640, n_mels, fmin, fmax)
+    for u in range(40):
+        mag, _ = R.magphase(R.stft(x[u], 640, 160))
+        _check_db(got[u], R.amplitude_to_db(fb @ mag, top_db=top_db))

@@ -112,4 +112,6 @@ def test_converted_keras_h5_runs_forward_against_oracle(tmp_path, gpu):
     dw = ops.DeviceWeights(loaded, "float32")
     got = ops.forward(dw, torch.from_numpy(mel).to(gpu), torch.from_numpy(video).to(gpu)).cpu().numpy()
     err = float(np.sqrt(np.mean((got.astype(np.float64) - ref) ** 2)))
-    assert err <= 1e-4 * max(1.0, float(np.sqrt(np.mean(ref ** 2)))), err
+    # the fp32 forward's bounds (tests/test_gpu_forward.py): absolute RMS 1e-4 (north star) and relative 1e-5
+    assert err <= 1e-4, err
+    assert err <= 1e-5 * float(np.sqrt(np.mean(ref ** 2))) + 1e-12, err

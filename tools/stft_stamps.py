@@ -1,7 +1,9 @@
-"""Per-step cycles of k_spec640 (stft.hip) on BASELINE configs[1] (4096 segments, no complex STFT output), from a
+"""Per-step cycles of k_spec_seg / k_spec640 (stft.hip) on BASELINE configs[1] (4096 segments, no complex STFT output), from a
 diagnostic variant library built with -DAVSE_STFT_STAMP (s_memtime stamps of thread 0 of every block):
     make -C audio-visual-speech-enhancement_amd/csrc_ab OUT=$PWD/tools/_libavse_sstamp.so EXTRA=-DAVSE_STFT_STAMP
-    python tools/stft_stamps.py tools/_libavse_sstamp.so"""
+    python tools/stft_stamps.py tools/_libavse_sstamp.so
+k_spec_seg (the configs[1] kernel since r03e) loops over utterances: the figures are per utterance.  k_spec640 runs
+for other geometries; its step names apply when the second argument is 640 (forced with -DAVSE_NO_SEG)."""
 import ctypes
 import os
 import sys
@@ -20,6 +22,9 @@ from avse_amd import _lib, ops  # noqa: E402
 
 STEPS = ["0 samples issue + barrier", "1 dft20 (wave 0)", "2a -> regs", "2b dft16", "3 untangle + |X|", "4 mel + dB + max",
          "5 clamp + store"]
+STEPS_SEG = ["0 DMA wait + barrier", "1 dft20 + twiddle", "2 dft16", "3 untangle + |X| + barrier", "4 mel MFMA + dB + barrier", "5 DMA issue + store"]
+if len(sys.argv) < 3 or sys.argv[2] != "640":
+    STEPS = STEPS_SEG
 
 
 def main():
@@ -40,9 +45,11 @@ def main():
     torch.cuda.synchronize()
     fn(buf.ctypes.data, 1)
     blocks = B * reps
-    print(f"cycles per block (thread 0, {blocks} blocks of one 21-frame segment):")
+    print(f"cycles per utterance (thread 0 of its block, {blocks} 21-frame segments):")
     tot = buf.sum(axis=0).astype(np.float64)
-    for name, v in zip(STEPS + ["7 table staging"], tot):
+    for name, v in zip(STEPS + [""] * (8 - len(STEPS)), tot):
+        if not name:
+            continue
         print(f"  {name:22s} {v / blocks:9.0f}")
     print(f"  {'total':22s} {tot.sum() / blocks:9.0f}")
 
