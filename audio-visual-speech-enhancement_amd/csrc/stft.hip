@@ -99,21 +99,22 @@ __device__ __forceinline__ int padded_index(int i, int L, int pad_mode, bool& ke
     return min(max(i, 0), L - 1);
 }
 
-// |X| by the hardware v_sqrt_f32 (1 ulp): sqrtf's correctly rounded sequence is ~12 instructions, 16 per lane
-// per chunk, and the magnitudes only feed the mel sums (dB tolerance 1e-3)
-__device__ __forceinline__ float cabs_fast(float2 x) { return __builtin_amdgcn_sqrtf(x.x * x.x + x.y * x.y); }
+// |X| by the hardware v_sqrt_f32 (1 ulp; sqrtf's correctly rounded sequence is ~12 instructions, 16 per lane per
+// chunk, and the magnitudes only feed the mel sums, dB tolerance 1e-3) of the packed square
+__device__ __forceinline__ float pk_abs(v2f x) {
+    const v2f x2 = x * x;
+    return __builtin_amdgcn_sqrtf(x2.x + x2.y);
+}
 
-// real-FFT untangling of the packed 320-point transform Z of one frame: X[k] and X[320 - k]
-__device__ __forceinline__ void untangle(const float2* __restrict__ zf, int k, const float2* __restrict__ twl, float2& X,
-                                         float2& Xm) {
-    const float2 zk = zf[k];
-    const float2 zm = zf[k == 0 ? 0 : 320 - k];
-    // E = (Zk + conj Zm)/2 ; O = -i/2 (Zk - conj Zm)
-    const float2 E = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y));
-    const float2 O = make_float2(0.5f * (zk.y + zm.y), -0.5f * (zk.x - zm.x));
-    const float2 WO = cmul(twl[k], O);
-    X = cadd(E, WO);
-    Xm = make_float2(E.x - WO.x, -(E.y - WO.y));   // X[320 - k] = conj(E - W^k O)
+// real-FFT untangling of the packed 320-point transform Z of one frame (z[n] = x[2n] + i x[2n+1]):
+// packed form: X = X[k], Y = conj X[320 - k] from Z[k], Z[320 - k]; U = -i W640^k / 2 (a float2 table):
+// E = (Zk + conj Zm) / 2, W^k O = U (Zk - conj Zm), X = E + W^k O, Y = E - W^k O
+__device__ __forceinline__ void pk_untangle(const v2f* __restrict__ zf, int k, const v2f* __restrict__ ut, v2f& X, v2f& Y) {
+    const v2f zk = zf[k], zm = zf[k == 0 ? 0 : 320 - k];
+    const v2f S = pk_add_conj(zk, zm);
+    const v2f WO = pk_cmul_t(pk_sub_conj(zk, zm), ut[k]);
+    X = __builtin_elementwise_fma(v2f(0.5f), S, WO);
+    Y = __builtin_elementwise_fma(v2f(0.5f), S, -WO);
 }
 
 // lane (f1, n1) of step 1 loads z[n1 + 16 n2] = (x[s0 + 2(n1 + 16 n2)], x[s0 + 2(n1 + 16 n2) + 1]), n2 < 20
@@ -160,6 +161,7 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec640(SpecArgs a, in
     __shared__ float2 zbuf[WAVES * FPG * ZS];
     __shared__ float dbuf[80 * CHUNK];
     __shared__ float2 twl[640];
+    __shared__ v2f ut2[161];       // U = -i W640^k / 2 (untangling)
     __shared__ float2 winl[320];
     __shared__ float4 melw4[FAST_MEL ? 80 * MW / 4 : 1];
     __shared__ int mel_st[80], mel_wd[80];
@@ -172,6 +174,10 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec640(SpecArgs a, in
     const int g = FPG * wave;                       // this wave's first frame in the chunk
 
     for (int i = tid; i < 640; i += 64 * WAVES) twl[i] = a.twiddle[i];
+    for (int k = tid; k < 161; k += 64 * WAVES) {
+        const float2 w = a.twiddle[k];
+        ut2[k] = v2f{0.5f * w.y, -0.5f * w.x};
+    }
     for (int i = tid; i < 320; i += 64 * WAVES) winl[i] = reinterpret_cast<const float2*>(a.window)[i];
     if (FAST_MEL)   // host rows are zero-padded to MW
         for (int i = tid; i < n_mels * MW / 4; i += 64 * WAVES) melw4[i] = reinterpret_cast<const float4*>(a.mel_weight)[i];
@@ -198,24 +204,25 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec640(SpecArgs a, in
         const int ng = max(0, min(FPG, nf - g));
         float2* zw = zbuf + wave * FPG * ZS;
 
-        // ---- step 1: 20-point DFTs over n2, lane = (f, n1) ----
-        float2 v[20];
+        // ---- step 1: 20-point DFTs over n2, lane = (f, n1) (packed fp32, fft_common.h pk_*) ----
+        v2f v[20];
 #pragma unroll
         for (int n2 = 0; n2 < 20; ++n2) {
             const float2 w = winl[n1 + 16 * n2];
-            v[n2] = make_float2(x[n2].x * w.x, x[n2].y * w.y);
+            v[n2] = v2f{x[n2].x, x[n2].y} * v2f{w.x, w.y};
         }
         if (f1 < ng) {
-            dft20(v, twl);
-            // v[5c + d] = Y[c + 4d]; twiddle W320^{n1 k2} = W640^{2 n1 k2}
-            float2* zf = zw + f1 * ZS;
+            pk_dft20(v);
+            // v[5c + d] = Y[c + 4d]; twiddle W320^{n1 k2} = W640^{2 n1 k2} (2 n1 k2 <= 570)
+            v2f* zf = reinterpret_cast<v2f*>(zw + f1 * ZS);
+            const v2f* twv = reinterpret_cast<const v2f*>(twl);
 #pragma unroll
             for (int c = 0; c < 4; ++c)
 #pragma unroll
                 for (int d = 0; d < 5; ++d) {
                     const int k2 = c + 4 * d;
-                    float2 y = v[5 * c + d];
-                    if (k2) y = cmul(y, twl[(2 * n1 * k2) % 640]);
+                    v2f y = v[5 * c + d];
+                    if (k2) y = pk_cmul_t(y, twv[2 * n1 * k2]);
                     zf[k2 * 17 + n1] = y;
                 }
         }
@@ -225,8 +232,8 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec640(SpecArgs a, in
         {
             const int f = lane / 20, k2 = lane - 20 * (lane / 20);
             const bool act = f < ng;
-            float2 w[16];
-            float2* zf = zw + min(f, FPG - 1) * ZS;
+            v2f w[16];
+            v2f* zf = reinterpret_cast<v2f*>(zw + min(f, FPG - 1) * ZS);
             if (act) {
 #pragma unroll
                 for (int n = 0; n < 16; ++n) w[n] = zf[k2 * 17 + n];
@@ -234,7 +241,7 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec640(SpecArgs a, in
             if constexpr (RI) lds_barrier(); else wave_lds_sync();
             SPEC_STAMP(2)
             if (act) {
-                dft16(w, twl);
+                pk_dft16(w);
 #pragma unroll
                 for (int c = 0; c < 4; ++c)
 #pragma unroll
@@ -252,14 +259,14 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec640(SpecArgs a, in
                 const int it = tid + 64 * WAVES * j;
                 const int k = it / CHUNK, f = it - CHUNK * k;
                 if (k > 160 || f >= nf) continue;
-                const float2* zf = zbuf + f * ZS;
-                float2 X, Xm;
-                untangle(zf, k, twl, X, Xm);
-                mk[j] = cabs_fast(X);
-                mm[j] = cabs_fast(Xm);
+                const v2f* zf = reinterpret_cast<const v2f*>(zbuf + f * ZS);
+                v2f X, Y;
+                pk_untangle(zf, k, ut2, X, Y);
+                mk[j] = pk_abs(X);
+                mm[j] = pk_abs(Y);
                 float2* o = reinterpret_cast<float2*>(a.stft_ri) + (long long)u * 321 * T + t0 + f;
-                o[(long long)k * T] = X;
-                if (k != 160) o[(long long)(320 - k) * T] = Xm;
+                o[(long long)k * T] = make_float2(X.x, X.y);
+                if (k != 160) o[(long long)(320 - k) * T] = make_float2(Y.x, -Y.y);   // X[320 - k] = conj(Y)
             }
             lds_barrier();
 #pragma unroll
@@ -288,10 +295,10 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec640(SpecArgs a, in
                 const int it = lane + 64 * j;
                 if (it >= ng * 161) break;
                 const int f = it / 161, k = it - 161 * f;
-                float2 X, Xm;
-                untangle(zw + f * ZS, k, twl, X, Xm);
-                mk[j] = cabs_fast(X);
-                mm[j] = cabs_fast(Xm);
+                v2f X, Y;
+                pk_untangle(reinterpret_cast<const v2f*>(zw + f * ZS), k, ut2, X, Y);
+                mk[j] = pk_abs(X);
+                mm[j] = pk_abs(Y);
             }
             wave_lds_sync();
 #pragma unroll
@@ -496,16 +503,10 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec_seg(SpecArgs a) {
                 const int it = lane + 64 * j;
                 if (it >= FPG * 161) break;
                 const int f = it / 161, k = it - 161 * f;
-                const v2f* zf = zw + f * ZS;
-                const v2f zk = zf[k], zm = zf[k == 0 ? 0 : 320 - k];
-                // X[k] = E + W^k O, conj X[320 - k] = E - W^k O;  E = (Zk + conj Zm) / 2, W^k O = U (Zk - conj Zm)
-                const v2f S = pk_add_conj(zk, zm);
-                const v2f WO = pk_cmul_t(pk_sub_conj(zk, zm), ut2[k]);
-                const v2f X = __builtin_elementwise_fma(v2f(0.5f), S, WO);
-                const v2f Y = __builtin_elementwise_fma(v2f(0.5f), S, -WO);
-                const v2f X2 = X * X, Y2 = Y * Y;
-                mk[j] = __builtin_amdgcn_sqrtf(X2.x + X2.y);
-                mm[j] = __builtin_amdgcn_sqrtf(Y2.x + Y2.y);
+                v2f X, Y;
+                pk_untangle(zw + f * ZS, k, ut2, X, Y);
+                mk[j] = pk_abs(X);
+                mm[j] = pk_abs(Y);
             }
             wave_lds_sync();
 #pragma unroll
