@@ -48,6 +48,14 @@ __device__ __forceinline__ float2 unit_phase(float2 d) {
     return r2 > 0.f ? make_float2(d.x * s, d.y * s) : make_float2(1.f, 0.f);
 }
 
+// a D / |D| (1 where D == 0) in packed form
+__device__ __forceinline__ v2f pk_unit_phase(v2f d, float a) {
+    const v2f d2 = d * d;
+    const float r2 = d2.x + d2.y;
+    const float s = a * __builtin_amdgcn_rsqf(r2);
+    return r2 > 0.f ? d * v2f(s) : v2f{a, 0.f};
+}
+
 // X[k] = (pinv(mel) @ 10^(dB/20))[k] * D[k]/|D[k]| for one frame, k in [0, nb)
 __device__ __forceinline__ float2 spectrum_bin(const IstftArgs& a, const float* amp, long long u, int k, int t) {
     float acc = 0.f;
@@ -364,7 +372,9 @@ __global__ __launch_bounds__(64 * IWAVES) AVSE_ISTFT_ATTR void k_istft_fused(Ist
                 const int km = k == 0 ? 320 : 320 - k;
                 const float4 bk = bins_l[k], bm = bins_l[km];
                 const int jk = __float_as_int(bk.z), jm = __float_as_int(bm.z);
-                const float2 twk = cconj(tw[k]);
+                // packed fp32 (fft_common.h): cw = conj(W640^k) / 2, so O = (xk - conj xm) cw and E = (xk + conj xm) / 2
+                const float2 twk = tw[k];
+                const v2f cw = v2f{0.5f * twk.x, -0.5f * twk.y};
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
                     const int f = f0 + h;
@@ -372,17 +382,16 @@ __global__ __launch_bounds__(64 * IWAVES) AVSE_ISTFT_ATTR void k_istft_fused(Ist
                     const float* y = amp[f];
                     const float ak = (jk >= 0 ? bk.x * y[jk] : 0.f) + (jk + 1 < n_mels && jk >= 0 ? bk.y * y[jk + 1] : 0.f);
                     const float am = (jm >= 0 ? bm.x * y[jm] : 0.f) + (jm + 1 < n_mels && jm >= 0 ? bm.y * y[jm + 1] : 0.f);
-                    const float2 pk = unit_phase(h ? make_float2(dk[j].z, dk[j].w) : make_float2(dk[j].x, dk[j].y));
-                    const float2 pm = unit_phase(h ? make_float2(dm[j].z, dm[j].w) : make_float2(dm[j].x, dm[j].y));
-                    float2 xk = make_float2(ak * pk.x, ak * pk.y);
-                    float2 xm = make_float2(am * pm.x, am * pm.y);
+                    const v2f dkh = h ? v2f{dk[j].z, dk[j].w} : v2f{dk[j].x, dk[j].y};
+                    const v2f dmh = h ? v2f{dm[j].z, dm[j].w} : v2f{dm[j].x, dm[j].y};
+                    v2f xk = pk_unit_phase(dkh, ak), xm = pk_unit_phase(dmh, am);
                     if (k == 0) { xk.y = 0.f; xm.y = 0.f; }       // irfft ignores the DC / Nyquist imaginary parts
-                    const float2 cxm = cconj(xm);
-                    const float2 E = make_float2(0.5f * (xk.x + cxm.x), 0.5f * (xk.y + cxm.y));
-                    const float2 O = cmul(make_float2(0.5f * (xk.x - cxm.x), 0.5f * (xk.y - cxm.y)), twk);
-                    float2* zf = zbuf + f * ZS;
-                    zf[k] = make_float2(E.x - O.y, -(E.y + O.x));          // conj(E + i O)
-                    if (k != 0 && k != 160) zf[320 - k] = make_float2(E.x + O.y, E.y - O.x);   // E - i O
+                    const v2f E = v2f(0.5f) * pk_add_conj(xk, xm);
+                    const v2f O = pk_cmul_t(pk_sub_conj(xk, xm), cw);
+                    v2f* zf = reinterpret_cast<v2f*>(zbuf + f * ZS);
+                    const v2f Zp = pk_sub_mi(E, O);                            // E + i O
+                    zf[k] = v2f{Zp.x, -Zp.y};                                  // conj(E + i O)
+                    if (k != 0 && k != 160) zf[320 - k] = pk_add_mi(E, O);     // E - i O
                 }
             }
         }

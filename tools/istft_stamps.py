@@ -17,7 +17,7 @@ avse_pkg.load()
 sys.modules["avse_amd"]._lib.LIB_PATH = os.path.abspath(sys.argv[1])
 from avse_amd import _lib, ops  # noqa: E402
 
-PHASES = ["1 amplitudes", "2 Thomas", "3 spectrum x phase", "4a Z' -> regs", "4b dft20 -> LDS", "4c -> regs",
+PHASES = ["1 amplitudes", "2 Gram MFMA solve", "3 spectrum x phase", "4a Z' -> regs", "4b dft20 -> LDS", "4c -> regs",
           "4d dft16 -> LDS", "5b overlap-add", "5a next item's loads"]
 
 
