@@ -301,6 +301,9 @@ int ensure_spec_tables(avse_ctx* c, int sr, int n_fft, int n_mels, double fmin, 
         int lo = -1, hi = -1;
         for (int k = 0; k < nb; ++k)
             if (fb[(size_t)m * nb + k] > 0) { if (lo < 0) lo = k; hi = k; }
+        // bands start at an even bin (a leading zero weight when the first non-zero bin is odd): the STFT kernels
+        // read a band's magnitudes as 8-B pairs (half the LDS instructions and bank-conflict cycles of 4-B reads)
+        lo = lo < 0 ? -1 : (lo & ~1);
         st[m] = lo < 0 ? 0 : lo;
         wd[m] = lo < 0 ? 0 : hi - lo + 1;
         if (wd[m] > maxw) maxw = wd[m];

@@ -327,13 +327,15 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec640(SpecArgs a, in
             float acc = 0.f;
             if (FAST_MEL) {
                 const float4* wm = melw4 + m * (MW / 4);
+                const v2f* mf2 = reinterpret_cast<const v2f*>(mf);   // even band starts (host)
 #pragma unroll
                 for (int q = 0; q < MW / 4; ++q) {
                     const float4 w = wm[q];
-                    acc = fmaf(mf[4 * q], w.x, acc);
-                    acc = fmaf(mf[4 * q + 1], w.y, acc);
-                    acc = fmaf(mf[4 * q + 2], w.z, acc);
-                    acc = fmaf(mf[4 * q + 3], w.w, acc);
+                    const v2f x0 = mf2[2 * q], x1 = mf2[2 * q + 1];
+                    acc = fmaf(x0.x, w.x, acc);
+                    acc = fmaf(x0.y, w.y, acc);
+                    acc = fmaf(x1.x, w.z, acc);
+                    acc = fmaf(x1.y, w.w, acc);
                 }
             } else {
                 const float* wm = a.mel_weight + m * mw;
@@ -535,16 +537,17 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec_seg(SpecArgs a) {
             db[j] = -INFINITY;
             if (it >= FPG * n_mels) continue;
             const int m = __umul24(it, 43691) >> 17, f = it - 3 * m;   // m = it / 3 (it < 240)
-            const float* mf = zwf + f * (2 * ZS) + mel_st[m];
+            const v2f* mf = reinterpret_cast<const v2f*>(zwf + f * (2 * ZS) + mel_st[m]);   // even band starts (host)
             const float4* wm = melw4 + m * (MW / 4);
             float acc = 0.f;
 #pragma unroll
             for (int q = 0; q < MW / 4; ++q) {
                 const float4 w = wm[q];
-                acc = fmaf(mf[4 * q], w.x, acc);
-                acc = fmaf(mf[4 * q + 1], w.y, acc);
-                acc = fmaf(mf[4 * q + 2], w.z, acc);
-                acc = fmaf(mf[4 * q + 3], w.w, acc);
+                const v2f x0 = mf[2 * q], x1 = mf[2 * q + 1];
+                acc = fmaf(x0.x, w.x, acc);
+                acc = fmaf(x0.y, w.y, acc);
+                acc = fmaf(x1.x, w.z, acc);
+                acc = fmaf(x1.y, w.w, acc);
             }
             db[j] = acc > a.amin ? 6.0205999132796239f * __log2f(acc) : a.db_floor;
             vmax = fmaxf(vmax, db[j]);
