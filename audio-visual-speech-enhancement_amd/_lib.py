@@ -12,7 +12,8 @@ import threading
 
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libavse.so")
+# AVSE_LIBRARY selects another build of the same ABI, e.g. the checked build (csrc/Makefile DEBUG=1 -> libavse_debug.so)
+LIB_PATH = os.environ.get("AVSE_LIBRARY") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libavse.so")
 HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "avse.h")
 
 AVSE_F32 = 0
@@ -32,6 +33,7 @@ _flt = ctypes.c_float
 # name -> (restype, argtypes); every function declared in include/avse.h
 SIGNATURES = {
     "avse_abi_version": (_int, []),
+    "avse_build_flags": (_int, []),
     "avse_last_error": (ctypes.c_char_p, []),
     "avse_ctx_create": (_int, [_int, ctypes.POINTER(_c_void_p)]),
     "avse_ctx_destroy": (None, [_c_void_p]),

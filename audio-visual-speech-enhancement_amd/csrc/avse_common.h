@@ -48,6 +48,62 @@ struct Options {
         }                                                                                      \
     } while (0)
 
+// ---- checked build (make DEBUG=1 -> libavse_debug.so, -DAVSE_DEBUG) -----------------------
+// Device-side protocol / bounds checks that a release build compiles out.  A failing check records the first hit
+// (kernel, check code, block, thread, observed and expected value) in its translation unit's record with one vector
+// compare-and-swap and the kernel carries on (no trap: a trapped wave can take the whole GPU down); the C-ABI entry
+// points synchronise their stream after launching and turn a hit into AVSE_ERR_CHECK with the record in
+// avse_last_error (debug_poll, capi.hip).
+struct DebugHit {
+    unsigned hit, kernel, code, block, thread;
+    int value, expect;
+};
+enum DebugKernel : unsigned {
+    DK_V1R = 1,      // k_conv_v1r: window-slot tags (the loader's window k in slot k % 3 when the compute waves read)
+    DK_SPEC = 3,     // k_spec_seg / k_spec640: output and LDS index bounds
+    DK_ISTFT = 4,    // k_istft_fused: frame range and output bounds
+};
+#ifdef AVSE_DEBUG
+inline constexpr bool kDebugBuild = true;
+__device__ __forceinline__ void debug_record(DebugHit* h, unsigned kern, unsigned code, int value, int expect) {
+    if (atomicCAS(&h->hit, 0u, 1u) == 0u) {
+        h->kernel = kern;
+        h->code = code;
+        h->block = blockIdx.x;
+        h->thread = threadIdx.x;
+        h->value = value;
+        h->expect = expect;
+        __threadfence();
+    }
+}
+// one record per translation unit (no relocatable device code): AVSE_DEBUG_RECORD(name) defines it and the host
+// reader `int name(DebugHit* out)` (copy + reset) that debug_poll calls
+#define AVSE_DEBUG_RECORD(reader)                                                                    \
+    static __device__ ::avse::DebugHit g_avse_dbg;                                                   \
+    int reader(::avse::DebugHit* out) {                                                              \
+        ::avse::DebugHit zero{};                                                                     \
+        if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_avse_dbg), sizeof(zero)) != hipSuccess) return 2;   \
+        return hipMemcpyToSymbol(HIP_SYMBOL(g_avse_dbg), &zero, sizeof(zero)) == hipSuccess ? 0 : 2; \
+    }
+#define AVSE_CHECK_DEV(cond, kern, code, value, expect)                                              \
+    do {                                                                                             \
+        if (!(cond)) ::avse::debug_record(&g_avse_dbg, (kern), (code), (int)(value), (int)(expect)); \
+    } while (0)
+#else
+inline constexpr bool kDebugBuild = false;
+#define AVSE_DEBUG_RECORD(reader)              \
+    int reader(::avse::DebugHit* out) {          \
+        *out = ::avse::DebugHit{};               \
+        return 0;                                \
+    }
+#define AVSE_CHECK_DEV(cond, kern, code, value, expect) \
+    do {                                                 \
+    } while (0)
+#endif
+int debug_read_v1r(DebugHit* out);
+int debug_read_stft(DebugHit* out);
+int debug_read_istft(DebugHit* out);
+
 // ---- STFT / mel front end ---------------------------------------------------------------
 struct MelTable {
     int n_mels = 0;

@@ -775,6 +775,8 @@ ConvArgs conv_args(const GpuLayer& G, const void* in, long long in_clip_stride, 
 extern "C" {
 
 int avse_abi_version(void) { return AVSE_ABI_VERSION; }
+
+int avse_build_flags(void) { return avse::kDebugBuild ? 1 : 0; }
 const char* avse_last_error(void) { return g_err.c_str(); }
 
 int avse_ctx_create(int device, avse_ctx** out) {
@@ -847,6 +849,29 @@ int avse_ctx_reserve(avse_ctx* c, int64_t max_clips, int dtype) {
     return ensure_arena(c, max_clips, dtype, kPlan25);   // the 25-fps network's scratch (other shapes grow it on use)
 }
 
+namespace avse {
+// checked build: wait for the stream, then report the first device-side check that fired (avse_common.h DebugHit)
+int debug_poll(void* stream) {
+    if constexpr (!kDebugBuild) return 0;
+    AVSE_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
+    static const struct {
+        int (*read)(DebugHit*);
+        const char* what;
+    } readers[] = {{debug_read_v1r, "k_conv_v1r"}, {debug_read_stft, "STFT"}, {debug_read_istft, "ISTFT"}};
+    for (const auto& r : readers) {
+        DebugHit h{};
+        if (r.read(&h)) return fail(AVSE_ERR_HIP, "checked build: reading the device check record failed");
+        if (h.hit)
+            return fail(AVSE_ERR_CHECK, std::string("checked build: ") + r.what + " check " + std::to_string(h.code) +
+                                            " failed (kernel id " + std::to_string(h.kernel) + ", block " +
+                                            std::to_string(h.block) + ", thread " + std::to_string(h.thread) +
+                                            ": value " + std::to_string(h.value) + ", expected " +
+                                            std::to_string(h.expect) + ")");
+    }
+    return 0;
+}
+}  // namespace avse
+
 int avse_spectrogram(avse_ctx* c, const float* sig, int64_t n_utt, int64_t n_samples, int sr, int n_fft, int hop,
                      int n_mels, float fmin, float fmax, float amin, float top_db, int pad_mode, int frames_per_slice,
                      float* mel_db, float* stft_ri, void* stream) {
@@ -891,7 +916,8 @@ int avse_spectrogram(avse_ctx* c, const float* sig, int64_t n_utt, int64_t n_sam
     a.mel_weight = c->spec.mel.weight;
     a.mel_max_width = c->spec.mel.max_width;
     a.umax = c->umax;
-    return launch_spectrogram(a, (hipStream_t)stream);
+    if (int lr = launch_spectrogram(a, (hipStream_t)stream)) return lr;
+    return debug_poll(stream);
 }
 
 int avse_istft(avse_ctx* c, const float* mel_db, const float* stft_ri, int64_t n_utt, int n_frames, int stft_frames,
@@ -936,7 +962,8 @@ int avse_istft(avse_ctx* c, const float* mel_db, const float* stft_ri, int64_t n
     a.sig = sig;
     a.bins = c->istft.bins;
     a.gram_inv = c->opt.dense_istft ? nullptr : c->istft.gram_inv;
-    return launch_istft(a, (hipStream_t)stream);
+    if (int lr = launch_istft(a, (hipStream_t)stream)) return lr;
+    return debug_poll(stream);
 }
 
 int64_t avse_weights_blob_floats(void) { return blob_floats(kPlan25); }
@@ -1293,8 +1320,17 @@ extern "C" {
 // are kept).  Opt-in (AVSE_GRAPH=1): a torch graph of the whole bench step (spectrogram + forward) measured 2.20 ->
 // 2.14 ms (tools/graph_probe.py), but replaying the forward alone inside the same step measured 2.234 vs 2.24-2.26 ms
 // direct (bench.py A/B, same box), so direct launches stay the default.
+static int forward_dispatch(avse_ctx* c, const avse_weights* W, const float* audio, const float* video,
+                            const float* vmean, const float* vstd, int64_t N, float* out, void* stream);
+
 int avse_forward(avse_ctx* c, const avse_weights* W, const float* audio, const float* video, const float* vmean,
                  const float* vstd, int64_t N, float* out, void* stream) {
+    if (int rc = forward_dispatch(c, W, audio, video, vmean, vstd, N, out, stream)) return rc;
+    return avse::debug_poll(stream);
+}
+
+static int forward_dispatch(avse_ctx* c, const avse_weights* W, const float* audio, const float* video,
+                            const float* vmean, const float* vstd, int64_t N, float* out, void* stream) {
     if (!c || !W || N <= 0 || !c->opt.graph)
         return forward_impl(c, W, audio, video, vmean, vstd, N, out, (hipStream_t)stream, nullptr);
     AVSE_HIP_CHECK(hipSetDevice(c->device));

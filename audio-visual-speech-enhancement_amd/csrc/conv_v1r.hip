@@ -21,6 +21,7 @@
 #include "avse_common.h"
 
 namespace avse {
+AVSE_DEBUG_RECORD(debug_read_v1r)
 namespace {
 
 constexpr float LRELU = 0.3f;
@@ -54,6 +55,7 @@ constexpr int NWS = 3;                                              // window sl
 constexpr int SPITCH = 576;
 constexpr int STG = 64 * SPITCH;
 constexpr int LDS_BYTES = WIMG + NWS * HSLOT + SSH + 2 * STG;
+constexpr int LDS_LAUNCH = LDS_BYTES + (kDebugBuild ? 16 : 0);      // checked build: + the window-slot tags
 constexpr int PPL = (HPIX + 255) / 256;                             // window pixels per loader lane (2)
 static_assert(HSLOT % 16 == 0 && LDS_BYTES <= 160 * 1024, "LDS");
 
@@ -66,6 +68,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_v1r(HaloArgs a) {
     char* const halo = lds + WIMG;                  // [NWS][HSLOT]
     float* const ssh = reinterpret_cast<float*>(halo + NWS * HSLOT);
     char* const stg = halo + NWS * HSLOT + SSH;     // [2][STG] pooled raw maxima, compute -> loader
+    int* const tags = reinterpret_cast<int*>(lds + LDS_BYTES);   // checked build: window index held by each slot
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -195,13 +198,20 @@ __global__ __launch_bounds__(512, 1) void k_conv_v1r(HaloArgs a) {
         };
         using Q0 = std::integral_constant<int, 0>;
         using Q1 = std::integral_constant<int, 1>;
+        // checked build: one loader lane tags the slot after the window's LDS stores (a wave's LDS operations
+        // complete in order); the compute waves compare the tags at both ends of a tile
+        auto tag = [&](int hs, int k) {
+            if (kDebugBuild && L == 0) tags[hs] = k;
+        };
         win_load(Q0{}, 0);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         win_store(Q0{}, 0);
+        tag(0, 0);
         if (nmine > 1) {
             win_load(Q1{}, 1);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             win_store(Q1{}, 1);
+            tag(1, 1);
         }
         if (nmine > 2) win_load(Q0{}, 2);
         if (nmine > 3) win_load(Q1{}, 3);
@@ -222,6 +232,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_v1r(HaloArgs a) {
                 // builtins, so the compiler's waitcnt pass waits for exactly the loads each store reads (with
                 // the stores and window k+3's loads issued after them still in flight; DESIGN.md §3 v_conv1)
                 win_store(set, (k + 2) % NWS);     // slot of window k-1, last read during tile k-1
+                tag((k + 2) % NWS, k + 2);
                 if (k + 4 < nmine) win_load(set, k + 4);
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -300,6 +311,10 @@ __global__ __launch_bounds__(512, 1) void k_conv_v1r(HaloArgs a) {
     // one tile: slice 0 in (xa, xb); tile k+1's slice 0 lands in (ya, yb) (parity flips per tile)
     auto tile = [&](int k, i32x4 (&xa)[4], i32x4 (&xb)[8], i32x4 (&ya)[4], i32x4 (&yb)[8]) {
         const int hs = k % NWS, hn = (k + 1) % NWS;
+        if (kDebugBuild && lane == 0) {   // after B_{k-1}: window k in slot hs (and k + 1 in hn, read in slice 4)
+            AVSE_CHECK_DEV(tags[hs] == k, DK_V1R, 1, tags[hs], k);
+            if (k + 1 < nmine) AVSE_CHECK_DEV(tags[hn] == k + 1, DK_V1R, 2, tags[hn], k + 1);
+        }
         slice(hs, 1, xa, xb, ya, yb, true);
         slice(hs, 2, ya, yb, xa, xb, false);
         slice(hs, 3, xa, xb, ya, yb, false);
@@ -307,6 +322,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_v1r(HaloArgs a) {
         // slice 4, with tile k+1's first fragments (window k+1 was stored before B_{k-1}; past the last tile
         // the read hits a stale slot and is never used)
         slice(hn, 0, xa, xb, ya, yb, false);
+        if (kDebugBuild && lane == 0) AVSE_CHECK_DEV(tags[hs] == k, DK_V1R, 3, tags[hs], k);   // not yet replaced
         epilogue(k);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if constexpr (!(ABL & 8)) barrier_raw();   // B_k: staging k is written; window k is no longer read
@@ -321,7 +337,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_v1r(HaloArgs a) {
 }  // namespace
 
 int launch_conv_v1r(const HaloArgs& a, hipStream_t s) {
-    if (int rc = ensure_lds_attr((const void*)k_conv_v1r<0>, LDS_BYTES)) return rc;
+    if (int rc = ensure_lds_attr((const void*)k_conv_v1r<0>, LDS_LAUNCH)) return rc;
     if (a.Hc % TH || a.Wc % TW || a.Co != 128 || a.Ci != NF || !a.w) {
         set_error("v_conv1 row-run kernel: unexpected layer shape or missing packing");
         return 3;
@@ -332,7 +348,7 @@ int launch_conv_v1r(const HaloArgs& a, hipStream_t s) {
     const int tiles = a.N * (a.Hc / TH) * (a.Wc / TW);
     int gx = ncu >= 8 ? ncu / 8 * 8 : ncu;
     if (gx > tiles) gx = tiles;
-    hipLaunchKernelGGL(k_conv_v1r<0>, dim3(gx), dim3(512), LDS_BYTES, s, a);
+    hipLaunchKernelGGL(k_conv_v1r<0>, dim3(gx), dim3(512), LDS_LAUNCH, s, a);
     AVSE_HIP_CHECK(hipGetLastError());
     return 0;
 }

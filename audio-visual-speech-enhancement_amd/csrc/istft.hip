@@ -25,6 +25,7 @@
 #endif
 
 namespace avse {
+AVSE_DEBUG_RECORD(debug_read_istft)
 namespace {
 
 constexpr int FPG = 3;
@@ -309,6 +310,10 @@ __global__ __launch_bounds__(64 * IWAVES) AVSE_ISTFT_ATTR void k_istft_fused(Ist
         const int t_lo = max(0, b * OF - 1);
         const int t_hi = min(T - 1, b * OF + OF + 1);
         const int nfr = t_hi - t_lo + 1;
+        if (kDebugBuild && tid == 0) {   // checked build: the chunk's frame window fits the block's frame slots
+            AVSE_CHECK_DEV(t_lo >= 0 && t_hi < T && nfr >= 1 && nfr <= FW, DK_ISTFT, 1, nfr, FW);
+            AVSE_CHECK_DEV(u < a.n_utt, DK_ISTFT, 2, u, (int)a.n_utt);
+        }
 
         // ---- 1. amplitudes (frame fastest: runs of consecutive frames of one band) ----
         {
@@ -472,8 +477,11 @@ __global__ __launch_bounds__(64 * IWAVES) AVSE_ISTFT_ATTR void k_istft_fused(Ist
                 float yv = 0.f;
                 if (hq >= 3 && hq <= T - 1) {                      // interior: four frames, constant sum-square
 #pragma unroll
-                    for (int q = 0; q < 4; ++q)                    // increasing t = hq - 3 + q
+                    for (int q = 0; q < 4; ++q) {                  // increasing t = hq - 3 + q
+                        AVSE_CHECK_DEV(hq - 3 + q - t_lo >= 0 && hq - 3 + q - t_lo < nfr, DK_ISTFT, 3,
+                                       hq - 3 + q - t_lo, nfr);
                         yv += reinterpret_cast<const float*>(zbuf + (hq - 3 + q - t_lo) * ZS)[o0 + 160 * (3 - q)];
+                    }
                     yv *= iwss_l[o0];
                 } else {                                           // the utterance's first / last hops
                     const int tlo = max(0, (p - 640 + 160) / 160); // first frame t with t*160 + 639 >= p

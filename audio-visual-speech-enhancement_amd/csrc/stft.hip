@@ -31,6 +31,7 @@
 #endif
 
 namespace avse {
+AVSE_DEBUG_RECORD(debug_read_stft)
 
 namespace {
 
@@ -360,6 +361,9 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec640(SpecArgs a, in
         for (int it = tid; it < n_mels * nf; it += 64 * WAVES) {
             const int m = it / nf, tl = it - nf * m;
             const long long oi = out_index(a.spf, a.n_slices, n_mels, T, u, m, t0 + tl);
+            AVSE_CHECK_DEV(t0 + tl < T && oi < (a.spf > 0 ? (long long)a.n_utt * a.n_slices * n_mels * a.spf
+                                                          : (long long)a.n_utt * n_mels * T),
+                           DK_SPEC, 2, t0 + tl, T);
             if (oi >= 0) a.mel_db[oi] = fmaxf(dbuf[m * CHUNK + tl], floor_db);
         }
         if (!single && tid == 0) atomicMax(a.umax + u, f2ord(vmax));
@@ -448,6 +452,11 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec_seg(SpecArgs a) {
         const long long nx = u + gridDim.x;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's samples have landed (wave-local buffer)
         lds_barrier();                                        // the previous utterance's dB / wmax reads are done
+        if (kDebugBuild && lane == 0) {   // checked build: the staged span is this utterance's (slot 320 + 7 wave)
+            [[maybe_unused]] const int sidx = 320 + 7 * wave, src = FPG * wave * 160 - 320 + sidx;   // in the utterance
+            [[maybe_unused]] const float* zv = reinterpret_cast<const float*>(zw);
+            AVSE_CHECK_DEV(zv[sidx] == a.sig[u * SEG_L + src], DK_SPEC, 1, (int)u, src);
+        }
         SPEC_STAMP(0)
         // ---- step 1: windowed 20-point DFTs over n2, lane = (f, n1) ----
         v2f v[20];

@@ -35,7 +35,8 @@ enum avse_status {
     AVSE_ERR_INVALID = 1,      /* bad argument / shape                                  */
     AVSE_ERR_HIP = 2,          /* HIP runtime error (message in avse_last_error)       */
     AVSE_ERR_UNSUPPORTED = 3,  /* configuration outside what the kernels implement      */
-    AVSE_ERR_OOM = 4           /* device allocation failed                             */
+    AVSE_ERR_OOM = 4,          /* device allocation failed                             */
+    AVSE_ERR_CHECK = 5         /* checked build only: a device-side protocol / bounds check fired */
 };
 
 enum avse_dtype { AVSE_F32 = 0, AVSE_BF16 = 1 };
@@ -231,6 +232,12 @@ int avse_trainer_read(avse_trainer* t, int what, float* host_blob, int64_t n_flo
 int avse_trainer_iterations(avse_trainer* t, int64_t* iterations);
 
 /* ---- diagnostics ----------------------------------------------------------------------- */
+
+/* Build flags of the loaded library: bit 0 = checked build (make DEBUG=1 -> libavse_debug.so, -DAVSE_DEBUG).  A checked
+ * build runs device-side protocol and bounds checks (v_conv1 window-slot tags, STFT sample staging and output bounds,
+ * ISTFT chunk frame ranges); avse_spectrogram / avse_istft / avse_forward then synchronise their stream and return
+ * AVSE_ERR_CHECK with the first failing check (kernel, check, block, thread, value, expected) in avse_last_error. */
+int avse_build_flags(void);
 
 /* Number of forward scratch buffers reported by avse_debug_scratch. */
 #define AVSE_DEBUG_NBUF 20

@@ -176,3 +176,28 @@ def test_other_frame_rate_networks_build_and_bad_shapes_are_refused():
         SpeechEnhancementNetwork.build((80, 22), (128, 128, 5))
     with pytest.raises(NotImplementedError):
         SpeechEnhancementNetwork.build((80, 20), (64, 64, 5))
+
+
+def _checked_harness():
+    """tests/native/abi_checked (csrc/Makefile `checked`: the checked build + host AddressSanitizer); built here when
+    missing (make is incremental; __graft_entry__.build() builds it too)."""
+    import subprocess
+    exe = os.path.join(ROOT, "tests", "native", "abi_checked")
+    csrc = os.path.join(ROOT, "audio-visual-speech-enhancement_amd", "csrc")
+    subprocess.check_call(["make", "-C", csrc, "-j8", "checked"], stdout=subprocess.DEVNULL)
+    return exe
+
+
+def test_checked_build_harness_host_part():
+    """The C-ABI's host paths (argument validation, blob sizes, shape refusals) under AddressSanitizer; without a
+    GPU the harness stops after them (tests/test_gpu_checked.py runs the device part)."""
+    import subprocess
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0", HIP_VISIBLE_DEVICES="")
+    r = subprocess.run([_checked_harness()], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "ok: 0 failure(s)" in r.stdout
+
+
+def test_release_and_checked_build_flags():
+    from avse_amd import _lib
+    assert _lib.load().avse_build_flags() == (1 if "debug" in os.path.basename(_lib.LIB_PATH) else 0)
