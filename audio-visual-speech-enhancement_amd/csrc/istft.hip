@@ -166,13 +166,13 @@ __global__ __launch_bounds__(64) void k_istft640(IstftArgs a) {
 //   5. overlap-add in increasing frame order x 1 / window sum-square (a per-position table in the interior)
 //      -> the trimmed signal, coalesced; first, the next chunk's global loads are issued (software pipeline)
 #ifndef AVSE_ISTFT_OF                         // A/B builds (tools/stft_time.py variant libraries)
-#define AVSE_ISTFT_OF 21
+#define AVSE_ISTFT_OF 30
 #endif
 #ifndef AVSE_ISTFT_ATTR
-#define AVSE_ISTFT_ATTR
+#define AVSE_ISTFT_ATTR __attribute__((amdgpu_waves_per_eu(3)))   // 11 waves: 3 per SIMD, <= 168 VGPRs
 #endif
 #ifndef AVSE_ISTFT_BPC
-#define AVSE_ISTFT_BPC 2
+#define AVSE_ISTFT_BPC 1
 #endif
 constexpr int OF = AVSE_ISTFT_OF;            // output hops per chunk
 constexpr int FW = OF + 3;                   // frames per chunk (n_fft / hop - 1 = 3 extra)
@@ -208,6 +208,7 @@ __global__ __launch_bounds__(64 * IWAVES) AVSE_ISTFT_ATTR void k_istft_fused(Ist
     // amplitudes, then y in place; odd row pitch (81 floats): the MFMA fragment reads (16 consecutive frames at one
     // band) are conflict-free and step 3's frame-pair lanes 2-way (a pitch of 80 put them on 2 banks)
     __shared__ float amp[FW][81];
+    __shared__ float yb[FW][81];                // y = (M M^T)^{-1} amp (step 2), read by step 3
     __shared__ float win_l[640];
     __shared__ float ws_l[640];                 // window / 320: applied as the DFT's samples are stored
     __shared__ float iwss_l[160];               // 1 / window sum-square of an interior sample, by position mod 160
@@ -243,7 +244,8 @@ __global__ __launch_bounds__(64 * IWAVES) AVSE_ISTFT_ATTR void k_istft_fused(Ist
     constexpr int IT1 = (FW * 80 + 64 * IWAVES - 1) / (64 * IWAVES);   // 4 (n_mels == 80, host-checked)
     // step 3 works on (bin k, frame pair): the pair's two STFT values are one 16-B load (the [bin][frame] layout keeps
     // a bin's frames adjacent); 8-B loads of single frames issued ~4.4K cycles per item (tools/istft_stamps.py)
-    constexpr int FP = FW / 2;                                          // frame pairs per chunk
+    constexpr int FP = (FW + 1) / 2;                                    // frame pairs per chunk (odd FW: the last
+                                                                        // pair's second frame is skipped)
     constexpr int IT3 = (161 * FP + 64 * IWAVES - 1) / (64 * IWAVES);  // 4
     float mv[IT1];
     float4 dk[IT3], dm[IT3];
@@ -329,39 +331,33 @@ __global__ __launch_bounds__(64 * IWAVES) AVSE_ISTFT_ATTR void k_istft_fused(Ist
         ibarrier();
         IST_STAMP(0)
         // ---- 2. y = (M M^T)^{-1} amp for the chunk's frames ----
-        // MFMA form: Y [32 frames (24 used) x 80] = A [32 x 80] x G [80 x 80], G = (M M^T)^{-1} (host, double ->
-        // float): v_mfma_f32_16x16x4_f32 (exact fp32 products) over 2 x 5 tiles, wave w < 5 owns the band tile w of
-        // both frame tiles; every operand is read into registers before the barrier, then y overwrites amp.  The
+        // MFMA form: Y [48 frames (FW used) x 80] = A [48 x 80] x G [80 x 80], G = (M M^T)^{-1} (host, double ->
+        // float): v_mfma_f32_16x16x4_f32 (exact fp32 products) over 3 x 5 output tiles of 16 frames x 16 bands, unit
+        // u = wave + IWAVES i (band tile u % 5, frame tile u / 5).  y has its own rows (yb), so each K-step's A and B
+        // fragments are read right before its MFMA (no pre-read into ~60 registers and no barrier between).  The
         // Thomas chain it replaces (one lane per frame, 159 dependent steps) took 8.5K of a 34K-cycle item.
         {
-            f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-            float fa[2][NMEL / 4], fb[NMEL / 4];
+            constexpr int NFT = (FW + 15) / 16, NU = NFT * (NMEL / 16);
             const int r16 = lane & 15, kq = lane >> 4;
-            if (wave < NMEL / 16) {
 #pragma unroll
-                for (int st = 0; st < NMEL / 4; ++st) {
-                    fb[st] = ginv_l[(4 * st + kq) * NMEL + 16 * wave + r16];
-#pragma unroll
-                    for (int r = 0; r < 2; ++r) {
-                        const int f = 16 * r + r16;
-                        fa[r][st] = f < nfr ? amp[f < FW ? f : 0][4 * st + kq] : 0.f;
-                    }
-                }
-            }
-            ibarrier();
-            if (wave < NMEL / 16) {
+            for (int i = 0; i < (NU + IWAVES - 1) / IWAVES; ++i) {
+                const int un = wave + IWAVES * i;
+                if (un >= NU) break;
+                const int bt = un % (NMEL / 16), ft = un / (NMEL / 16);
+                if (16 * ft >= nfr) continue;
+                const int f = 16 * ft + r16;
+                const float* ap = amp[min(f, FW - 1)] + kq;
+                const float* gp = ginv_l + kq * NMEL + 16 * bt + r16;
+                const bool va = f < nfr;
+                f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                 for (int st = 0; st < NMEL / 4; ++st)
+                    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(va ? ap[4 * st] : 0.f, gp[4 * st * NMEL], acc, 0, 0, 0);
 #pragma unroll
-                    for (int r = 0; r < 2; ++r)
-                        acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[r][st], fb[st], acc[r], 0, 0, 0);
-#pragma unroll
-                for (int r = 0; r < 2; ++r)
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const int f = 16 * r + 4 * kq + i;
-                        if (f < nfr) amp[f][16 * wave + r16] = acc[r][i];
-                    }
+                for (int e = 0; e < 4; ++e) {
+                    const int fo = 16 * ft + 4 * kq + e;
+                    if (fo < nfr) yb[fo][16 * bt + r16] = acc[e];
+                }
             }
         }
         ibarrier();
@@ -384,7 +380,7 @@ __global__ __launch_bounds__(64 * IWAVES) AVSE_ISTFT_ATTR void k_istft_fused(Ist
                 for (int h = 0; h < 2; ++h) {
                     const int f = f0 + h;
                     if (h == 1 && f >= nfr) break;
-                    const float* y = amp[f];
+                    const float* y = yb[f];
                     const float ak = (jk >= 0 ? bk.x * y[jk] : 0.f) + (jk + 1 < n_mels && jk >= 0 ? bk.y * y[jk + 1] : 0.f);
                     const float am = (jm >= 0 ? bm.x * y[jm] : 0.f) + (jm + 1 < n_mels && jm >= 0 ? bm.y * y[jm + 1] : 0.f);
                     const v2f dkh = h ? v2f{dk[j].z, dk[j].w} : v2f{dk[j].x, dk[j].y};
