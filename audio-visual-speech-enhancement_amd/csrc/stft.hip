@@ -381,8 +381,9 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec640(SpecArgs a, in
 //  - packed-fp32 FFT (fft_common.h pk_*): complex adds are one v_pk_add, products v_pk_mul + v_pk_fma with the
 //    quarter turns and the (re, im) swap in the op_sel / neg modifiers, so twiddle tables stay float2 (1,524 -> ~800
 //    VALU per wave and utterance, PMC);
-//  - the dB values stay in the wave's region (no dbuf), and the sliced output is written as float4.
-// Two block barriers per utterance (dB reuse, dB maximum).
+//  - one block barrier per utterance (the top_db maximum): every wave keeps its frames' dB values in registers and
+//    stores them itself once the maximum is known (no dB buffer, no store pass over the block; a variant that staged
+//    them in LDS for float4 stores needed a second barrier per utterance and measured 3 % slower).
 // Tried (r03): the mel product on the matrix cores ([21 frames x bins] x [bins x 16-band tiles], v_mfma_f32_16x16x4f32,
 // B fragments evaluated from the triangle coefficients, one tile job per wave, a third barrier): 0.0941 vs 0.0928 ms.
 // f32 MFMA runs at the f32 VALU rate and the dense tiles carry ~2x the sparse band FMAs; the gain in LDS gathers
@@ -391,7 +392,6 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec640(SpecArgs a, in
 #define AVSE_SEG_BPC 2
 #endif
 constexpr int SEG_L = 3200;
-constexpr int SEG_DB = 1024;   // float offset of a wave's dB values in its zbuf region (samples: [0, 960))
 
 __device__ __forceinline__ void seg_dma(float* sb, const float* __restrict__ sg, int wave, int lane, int pad_mode) {
     const __amdgpu_buffer_rsrc_t rs =
@@ -420,8 +420,8 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec_seg(SpecArgs a) {
     __shared__ v2f winl[320];
     __shared__ float4 melw4[80 * MW / 4];
     __shared__ int mel_st[80];
-    __shared__ float wmax[WAVES];
-    static_assert(FPG * ZS * 2 >= SEG_DB + FPG * 80, "sample buffer and dB values live in the wave's zbuf region");
+    __shared__ float wmax[2][WAVES];   // by utterance parity: a wave at most one utterance ahead writes the other row
+    static_assert(FPG * ZS * 2 >= 1024, "the sample buffer lives in the wave's zbuf region");
 
     int tid = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -443,7 +443,8 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec_seg(SpecArgs a) {
     const long long n_utt = a.n_utt;
     long long u = blockIdx.x;
     if (u < n_utt) seg_dma(zwf, a.sig + u * SEG_L, wave, tid & 63, a.pad_mode);
-    for (; u < n_utt; u += gridDim.x) {
+    int parity = 0;
+    for (; u < n_utt; u += gridDim.x, parity ^= 1) {
         // the per-lane index math stays inside the loop: hoisted out of it, the loop-invariant addresses held more
         // registers than the 128 of two blocks per CU (k_spec640's note)
         asm volatile("" : "+v"(tid));
@@ -451,7 +452,6 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec_seg(SpecArgs a) {
         const int f1 = lane >> 4, n1 = lane & 15;
         const long long nx = u + gridDim.x;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's samples have landed (wave-local buffer)
-        lds_barrier();                                        // the previous utterance's dB / wmax reads are done
         if (kDebugBuild && lane == 0) {   // checked build: the staged span is this utterance's (slot 320 + 7 wave)
             [[maybe_unused]] const int sidx = 320 + 7 * wave, src = FPG * wave * 160 - 320 + sidx;   // in the utterance
             [[maybe_unused]] const float* zv = reinterpret_cast<const float*>(zw);
@@ -561,46 +561,27 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec_seg(SpecArgs a) {
             db[j] = acc > a.amin ? 6.0205999132796239f * __log2f(acc) : a.db_floor;
             vmax = fmaxf(vmax, db[j]);
         }
-        wave_lds_sync();   // the magnitude reads are done: the region takes the dB values and the next samples
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int it = lane + 64 * j;
-            if (it >= FPG * n_mels) continue;
-            const int m = __umul24(it, 43691) >> 17, f = it - 3 * m;
-            zwf[SEG_DB + f * 80 + m] = db[j];
-        }
+        // one block barrier per utterance (the dB maximum): each wave keeps its frames' dB values in registers and
+        // stores them itself once the maximum is known, so no wave reads another wave's region and the next
+        // utterance's step 1 needs no barrier; the maxima alternate between two rows by utterance parity
+        wave_lds_sync();   // the magnitude reads are done: the region takes the next samples
         if (nx < n_utt) seg_dma(zwf, a.sig + nx * SEG_L, wave, lane, a.pad_mode);
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) vmax = fmaxf(vmax, __shfl_xor(vmax, o));
-        if (lane == 0) wmax[wave] = vmax;
+        if (lane == 0) wmax[parity][wave] = vmax;
         lds_barrier();
         SPEC_STAMP(4)
-        vmax = wmax[0];
+        vmax = wmax[parity][0];
 #pragma unroll
-        for (int w = 1; w < WAVES; ++w) vmax = fmaxf(vmax, wmax[w]);
+        for (int w = 1; w < WAVES; ++w) vmax = fmaxf(vmax, wmax[parity][w]);
         const float floor_db = a.top_db >= 0.f ? vmax - a.top_db : -INFINITY;
-        // dB(m, t) of frame t = 3 w + f sits at zb[w 2 FPG ZS + f 80 + m] = zb[1800 w + 80 t + m]; w = t / 3 = (11 t) >> 5 and
-        // the other small divisions by 24-bit multiplies (the generic ones were 64-bit mul_lo / mul_hi sequences)
-        const float* zb = reinterpret_cast<const float*>(zbuf) + SEG_DB;
-        static_assert(2 * FPG * ZS - 3 * 80 == 1800, "dB layout");
-        if (a.spf == 20) {   // one 20-frame slice: out[u][0][m][t], t < 20 (frame 20 dropped), float4 over t
-            float4* o = reinterpret_cast<float4*>(a.mel_db + u * (long long)n_mels * 20);
-            for (int it = tid; it < n_mels * 5; it += 64 * WAVES) {
-                const int m = __umul24(it, 205) >> 10, t0 = 4 * (it - 5 * m);   // it < 400
-                float r[4];
+        const int ts = a.spf == 20 ? 20 : CHUNK;   // frames stored per band (the 20-frame slice drops frame 20)
+        float* o = a.mel_db + u * (long long)n_mels * ts;
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int t = t0 + e;
-                    r[e] = fmaxf(zb[__umul24(__umul24(t, 11) >> 5, 1800) + 80 * t + m], floor_db);
-                }
-                o[it] = make_float4(r[0], r[1], r[2], r[3]);
-            }
-        } else {             // plain [n_mels][21]
-            float* o = a.mel_db + u * (long long)n_mels * CHUNK;
-            for (int it = tid; it < n_mels * CHUNK; it += 64 * WAVES) {
-                const int m = __umul24(it, 3121) >> 16, t = it - CHUNK * m;   // it < 1680
-                o[it] = fmaxf(zb[__umul24(__umul24(t, 11) >> 5, 1800) + 80 * t + m], floor_db);
-            }
+        for (int j = 0; j < 4; ++j) {
+            const int it = lane + 64 * j;
+            const int m = __umul24(it, 43691) >> 17, t = FPG * wave + it - 3 * m;   // item (m, f): frame 3 w + f
+            if (it < FPG * n_mels && t < ts) o[m * ts + t] = fmaxf(db[j], floor_db);
         }
         SPEC_STAMP(5)
     }
