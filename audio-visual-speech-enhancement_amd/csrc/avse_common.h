@@ -112,6 +112,7 @@ struct MelTable {
     int* start = nullptr;      // device [n_mels]
     int* width = nullptr;      // device [n_mels]
     float* weight = nullptr;   // device [n_mels][max_width]
+    int seg_nq[4] = {6, 6, 6, 6};   // k_spec_seg: 4-bin weight quads its mel pass j (bands 64 j / 3 ..) needs
 };
 
 struct SpecArgs {
@@ -132,6 +133,7 @@ struct SpecArgs {
     const int* mel_width;
     const float* mel_weight;
     int mel_max_width;
+    int mel_seg_nq[4];        // MelTable::seg_nq
     unsigned int* umax;       // [n_utt] ordered-float max scratch (chunked mode)
 };
 

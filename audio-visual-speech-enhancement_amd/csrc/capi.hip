@@ -323,6 +323,13 @@ int ensure_spec_tables(avse_ctx* c, int sr, int n_fft, int n_mels, double fmin, 
     AVSE_HIP_CHECK(hipMemcpy(t.mel.width, wd.data(), sizeof(int) * n_mels, hipMemcpyHostToDevice));
     AVSE_HIP_CHECK(hipMemcpy(t.mel.weight, wt.data(), sizeof(float) * wt.size(), hipMemcpyHostToDevice));
     t.sr = sr; t.n_fft = n_fft; t.n_mels = n_mels; t.fmin = fmin; t.fmax = fmax;
+    // k_spec_seg's mel pass j covers items 64 j .. 64 j + 63 = bands (item / 3): the widest of those bands (aligned
+    // start) in 4-bin quads; the rows stay padded to maxw, so a pass reads only the quads its bands can use
+    for (int j = 0; j < 4; ++j) {
+        int w = 0;
+        for (int it = 64 * j; it < 64 * j + 64 && it / 3 < n_mels; ++it) w = std::max(w, wd[it / 3]);
+        t.mel.seg_nq[j] = std::min((w + 3) / 4, maxw / 4);
+    }
     t.mel.n_mels = n_mels; t.mel.n_bins = nb; t.mel.max_width = maxw;
     return 0;
 }
@@ -915,6 +922,7 @@ int avse_spectrogram(avse_ctx* c, const float* sig, int64_t n_utt, int64_t n_sam
     a.mel_width = c->spec.mel.width;
     a.mel_weight = c->spec.mel.weight;
     a.mel_max_width = c->spec.mel.max_width;
+    std::memcpy(a.mel_seg_nq, c->spec.mel.seg_nq, sizeof(a.mel_seg_nq));
     a.umax = c->umax;
     if (int lr = launch_spectrogram(a, (hipStream_t)stream)) return lr;
     return debug_poll(stream);

@@ -322,15 +322,23 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec640(SpecArgs a, in
         // ---- step 4: Slaney mel + dB, item = (m, f), f fastest: the three lanes of a band read its weights at one LDS
         // address (broadcast; 0.0983 -> 0.094 ms with the float2 twiddle tables) ----
         float vmax = -INFINITY;
-        for (int it = lane; it < ng * n_mels; it += 64) {
-            const int f = it >= n_mels ? (it >= 2 * n_mels ? 2 : 1) : 0, m = it - n_mels * f;
+        // items (m, f) band-major, f fastest (as k_spec_seg): pass j covers bands 64 j / 3 .. and reads only the 4-bin
+        // weight quads those bands use (MelTable::seg_nq); the frames past a partial last chunk (f >= ng) idle
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+            const int it = lane + 64 * jj;
+            if (it >= FPG * n_mels) break;
+            const int m = __umul24(it, 43691) >> 17, f = it - 3 * m;   // m = it / 3 (it < 240)
+            if (f >= ng) continue;
             const float* mf = reinterpret_cast<const float*>(zw + f * ZS) + mel_st[m];
             float acc = 0.f;
             if (FAST_MEL) {
                 const float4* wm = melw4 + m * (MW / 4);
                 const v2f* mf2 = reinterpret_cast<const v2f*>(mf);   // even band starts (host)
+                const int nq = a.mel_seg_nq[jj];
 #pragma unroll
                 for (int q = 0; q < MW / 4; ++q) {
+                    if (q >= nq) break;
                     const float4 w = wm[q];
                     const v2f x0 = mf2[2 * q], x1 = mf2[2 * q + 1];
                     acc = fmaf(x0.x, w.x, acc);
@@ -548,9 +556,11 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec_seg(SpecArgs a) {
             const int m = __umul24(it, 43691) >> 17, f = it - 3 * m;   // m = it / 3 (it < 240)
             const v2f* mf = reinterpret_cast<const v2f*>(zwf + f * (2 * ZS) + mel_st[m]);   // even band starts (host)
             const float4* wm = melw4 + m * (MW / 4);
+            const int nq = a.mel_seg_nq[j];   // (uniform) quads the pass's bands use: 2-6 of 6 (Slaney widths 5-24)
             float acc = 0.f;
 #pragma unroll
             for (int q = 0; q < MW / 4; ++q) {
+                if (q >= nq) break;
                 const float4 w = wm[q];
                 const v2f x0 = mf[2 * q], x1 = mf[2 * q + 1];
                 acc = fmaf(x0.x, w.x, acc);
