@@ -410,12 +410,22 @@ __device__ __forceinline__ void seg_dma(float* sb, const float* __restrict__ sg,
 #pragma unroll
         for (int j = 0; j < 4; ++j)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr)(sb + 256 * j), 16, (base + 4 * lane) * 4, 1024 * j, 0, 0);
-    } else {   // one dword per lane; zero padding reads past the buffer's range (returns 0)
+    } else {
+        // edge waves: 640 samples inside the utterance as 16-B pieces (3 instructions, the last half used) and the 320
+        // padded ones one dword per lane with a reversed index (reflect) or an offset past the range (reads 0)
+        const bool first = wave == 0;
+        const int cslot = first ? 320 : 0, csmp = first ? 0 : SEG_L - 640;   // contiguous run: slots / samples
+        const int rslot = first ? 0 : 640, rbase = first ? 320 : 2 * (SEG_L - 1) - base;   // reflected run
 #pragma unroll
-        for (int j = 0; j < 15; ++j) {
-            bool keep;
-            const int i = padded_index(base + 64 * j + lane, SEG_L, pad_mode, keep);
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr)(sb + 64 * j), 4, keep ? i * 4 : 0x40000000, 0, 0, 0);
+        for (int j = 0; j < 3; ++j)
+            if (j < 2 || lane < 32)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr)(sb + cslot + 256 * j), 16, (csmp + 4 * lane) * 4,
+                                                         1024 * j, 0, 0);
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+            const int sl = rslot + 64 * j + lane;     // slot; reflected sample rbase - slot (reflect padding)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr)(sb + rslot + 64 * j), 4,
+                                                     pad_mode == 0 ? (rbase - sl) * 4 : 0x40000000, 0, 0, 0);
         }
     }
 }
