@@ -22,7 +22,7 @@ from avse_amd import _lib, ops  # noqa: E402
 
 STEPS = ["0 samples issue + barrier", "1 dft20 (wave 0)", "2a -> regs", "2b dft16", "3 untangle + |X|", "4 mel + dB + max",
          "5 clamp + store"]
-STEPS_SEG = ["0 DMA wait + barrier", "1 dft20 + twiddle", "2 dft16", "3 untangle + |X| + barrier", "4 mel MFMA + dB + barrier", "5 DMA issue + store"]
+STEPS_SEG = ["0 DMA wait", "1 dft20 + twiddle", "2 dft16", "3 untangle + |X|", "4 mel + dB + DMA + barrier", "5 dB stores"]
 if len(sys.argv) < 3 or sys.argv[2] != "640":
     STEPS = STEPS_SEG
 
