@@ -112,7 +112,8 @@ struct MelTable {
     int* start = nullptr;      // device [n_mels]
     int* width = nullptr;      // device [n_mels]
     float* weight = nullptr;   // device [n_mels][max_width]
-    int seg_nq[4] = {6, 6, 6, 6};   // k_spec_seg: 4-bin weight quads its mel pass j (bands 64 j / 3 ..) needs
+    int seg_nq[4] = {6, 6, 6, 6};   // k_spec640: 4-bin weight quads its mel pass j (bands 64 j / 3 ..) needs
+    int seg_nq4[4] = {7, 7, 7, 7};  // k_spec_seg: the same from the band start rounded down to a multiple of 4 bins
 };
 
 struct SpecArgs {
@@ -134,6 +135,7 @@ struct SpecArgs {
     const float* mel_weight;
     int mel_max_width;
     int mel_seg_nq[4];        // MelTable::seg_nq
+    int mel_seg_nq4[4];       // MelTable::seg_nq4
     unsigned int* umax;       // [n_utt] ordered-float max scratch (chunked mode)
 };
 

@@ -329,6 +329,10 @@ int ensure_spec_tables(avse_ctx* c, int sr, int n_fft, int n_mels, double fmin, 
         int w = 0;
         for (int it = 64 * j; it < 64 * j + 64 && it / 3 < n_mels; ++it) w = std::max(w, wd[it / 3]);
         t.mel.seg_nq[j] = std::min((w + 3) / 4, maxw / 4);
+        // k_spec_seg reads 16-B quads from 4-aligned band starts (st & ~3: a further 0 or 2 leading zero weights)
+        int w4 = 0;
+        for (int it = 64 * j; it < 64 * j + 64 && it / 3 < n_mels; ++it) w4 = std::max(w4, (st[it / 3] & 3) + wd[it / 3]);
+        t.mel.seg_nq4[j] = std::min((w4 + 3) / 4, (maxw + 4) / 4);
     }
     t.mel.n_mels = n_mels; t.mel.n_bins = nb; t.mel.max_width = maxw;
     return 0;
@@ -923,6 +927,7 @@ int avse_spectrogram(avse_ctx* c, const float* sig, int64_t n_utt, int64_t n_sam
     a.mel_weight = c->spec.mel.weight;
     a.mel_max_width = c->spec.mel.max_width;
     std::memcpy(a.mel_seg_nq, c->spec.mel.seg_nq, sizeof(a.mel_seg_nq));
+    std::memcpy(a.mel_seg_nq4, c->spec.mel.seg_nq4, sizeof(a.mel_seg_nq4));
     a.umax = c->umax;
     if (int lr = launch_spectrogram(a, (hipStream_t)stream)) return lr;
     return debug_poll(stream);

@@ -107,6 +107,48 @@ __device__ __forceinline__ float pk_abs(v2f x) {
     return __builtin_amdgcn_sqrtf(x2.x + x2.y);
 }
 
+// Slaney band dot of NQ weight quads against the band's magnitudes (k_spec_seg step 4, k_spec640): loads first,
+// then the FMAs (same summation order as the quad loop it replaced)
+template <int NQ>
+__device__ __forceinline__ float band_dot(const float4* wm, const v2f* mf) {
+    float4 w[NQ];
+    v2f x[2 * NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        w[q] = wm[q];
+        x[2 * q] = mf[2 * q];
+        x[2 * q + 1] = mf[2 * q + 1];
+    }
+    float acc = 0.f;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        acc = fmaf(x[2 * q].x, w[q].x, acc);
+        acc = fmaf(x[2 * q].y, w[q].y, acc);
+        acc = fmaf(x[2 * q + 1].x, w[q].z, acc);
+        acc = fmaf(x[2 * q + 1].y, w[q].w, acc);
+    }
+    return acc;
+}
+// the same over 16-B magnitude quads from a 4-aligned band start (k_spec_seg): ds_read_b128 for weights and magnitudes
+template <int NQ>
+__device__ __forceinline__ float band_dot4(const float4* wm, const float4* mf) {
+    float4 w[NQ], x[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        w[q] = wm[q];
+        x[q] = mf[q];
+    }
+    float acc = 0.f;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        acc = fmaf(x[q].x, w[q].x, acc);
+        acc = fmaf(x[q].y, w[q].y, acc);
+        acc = fmaf(x[q].z, w[q].z, acc);
+        acc = fmaf(x[q].w, w[q].w, acc);
+    }
+    return acc;
+}
+
 // real-FFT untangling of the packed 320-point transform Z of one frame (z[n] = x[2n] + i x[2n+1]):
 // packed form: X = X[k], Y = conj X[320 - k] from Z[k], Z[320 - k]; U = -i W640^k / 2 (a float2 table):
 // E = (Zk + conj Zm) / 2, W^k O = U (Zk - conj Zm), X = E + W^k O, Y = E - W^k O
@@ -335,16 +377,13 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec640(SpecArgs a, in
             if (FAST_MEL) {
                 const float4* wm = melw4 + m * (MW / 4);
                 const v2f* mf2 = reinterpret_cast<const v2f*>(mf);   // even band starts (host)
-                const int nq = a.mel_seg_nq[jj];
-#pragma unroll
-                for (int q = 0; q < MW / 4; ++q) {
-                    if (q >= nq) break;
-                    const float4 w = wm[q];
-                    const v2f x0 = mf2[2 * q], x1 = mf2[2 * q + 1];
-                    acc = fmaf(x0.x, w.x, acc);
-                    acc = fmaf(x0.y, w.y, acc);
-                    acc = fmaf(x1.x, w.z, acc);
-                    acc = fmaf(x1.y, w.w, acc);
+                switch (a.mel_seg_nq[jj]) {   // straight-line loads per quad count (k_spec_seg step 4)
+                    case 1: acc = band_dot<1>(wm, mf2); break;
+                    case 2: acc = band_dot<2>(wm, mf2); break;
+                    case 3: acc = band_dot<3>(wm, mf2); break;
+                    case 4: acc = band_dot<4>(wm, mf2); break;
+                    case 5: acc = band_dot<5>(wm, mf2); break;
+                    default: acc = band_dot<MW / 4>(wm, mf2); break;
                 }
             } else {
                 const float* wm = a.mel_weight + m * mw;
@@ -400,6 +439,11 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec640(SpecArgs a, in
 #define AVSE_SEG_BPC 2
 #endif
 constexpr int SEG_L = 3200;
+// step 4 layout (LDS bank model of MI355X_MICROARCH.md §LDS, one wave's mel reads per utterance): magnitudes of frame f
+// at f * SEG_FS floats, bands from a 4-aligned start with weight rows of SEG_MW floats, both read as 16-B quads
+// (ds_read_b128): 160 LDS cycles per wave and utterance against 418 for 8-B pairs at 680-float frames / 24-float rows
+constexpr int SEG_FS = 360, SEG_MW = MW + 4;
+static_assert(2 * SEG_FS + 321 + SEG_MW <= FPG * 2 * ZS && SEG_FS % 4 == 0, "magnitude frames inside the wave region");
 
 __device__ __forceinline__ void seg_dma(float* sb, const float* __restrict__ sg, int wave, int lane, int pad_mode) {
     const __amdgpu_buffer_rsrc_t rs =
@@ -432,12 +476,12 @@ __device__ __forceinline__ void seg_dma(float* sb, const float* __restrict__ sg,
 
 __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec_seg(SpecArgs a) {
     SPEC_STAMP_INIT
-    __shared__ v2f zbuf[WAVES * FPG * ZS];
-    __shared__ v2f tw2[320];       // W320^j (step 1)
+    __shared__ __attribute__((aligned(16))) v2f zbuf[WAVES * FPG * ZS];
+    __shared__ v2f twp[19 * 16];   // W320^(n1 k2) at (k2 - 1) * 16 + n1 (step 1: conflict-free rows per k2)
     __shared__ v2f ut2[161];       // U = -i W640^k / 2 (untangling)
     __shared__ v2f winl[320];
-    __shared__ float4 melw4[80 * MW / 4];
-    __shared__ int mel_st[80];
+    __shared__ float4 melw4[80 * SEG_MW / 4];
+    __shared__ int mel_st[80];     // 4-aligned band starts
     __shared__ float wmax[2][WAVES];   // by utterance parity: a wave at most one utterance ahead writes the other row
     static_assert(FPG * ZS * 2 >= 1024, "the sample buffer lives in the wave's zbuf region");
 
@@ -445,16 +489,22 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec_seg(SpecArgs a) {
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int n_mels = a.n_mels;
     for (int i = tid; i < 320; i += 64 * WAVES) {
-        const float2 w = a.twiddle[2 * i];
-        tw2[i] = v2f{w.x, w.y};
+        if (i < 19 * 16) {
+            const float2 w = a.twiddle[2 * (i & 15) * ((i >> 4) + 1)];
+            twp[i] = v2f{w.x, w.y};
+        }
         winl[i] = reinterpret_cast<const v2f*>(a.window)[i];
     }
     for (int k = tid; k < 161; k += 64 * WAVES) {
         const float2 w = a.twiddle[k];
         ut2[k] = v2f{0.5f * w.y, -0.5f * w.x};
     }
-    for (int i = tid; i < n_mels * MW / 4; i += 64 * WAVES) melw4[i] = reinterpret_cast<const float4*>(a.mel_weight)[i];
-    for (int i = tid; i < n_mels; i += 64 * WAVES) mel_st[i] = a.mel_start[i];
+    // weight rows re-based to the 4-aligned start: 0 or 2 leading zeros (host starts are even), zero tail
+    for (int i = tid; i < n_mels * SEG_MW; i += 64 * WAVES) {
+        const int m = i / SEG_MW, src = i - SEG_MW * m - (a.mel_start[m] & 3);
+        reinterpret_cast<float*>(melw4)[i] = src >= 0 && src < MW ? a.mel_weight[m * MW + src] : 0.f;
+    }
+    for (int i = tid; i < n_mels; i += 64 * WAVES) mel_st[i] = a.mel_start[i] & ~3;
 
     v2f* zw = zbuf + wave * FPG * ZS;
     float* zwf = reinterpret_cast<float*>(zw);
@@ -496,7 +546,7 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec_seg(SpecArgs a) {
                 for (int d = 0; d < 5; ++d) {
                     const int k2 = c + 4 * d;
                     v2f y = v[5 * c + d];
-                    if (k2) y = pk_cmul_t(y, tw2[n1 * k2]);
+                    if (k2) y = pk_cmul_t(y, twp[(k2 - 1) * 16 + n1]);
                     zf[k2 * 17 + n1] = y;
                 }
         }
@@ -543,13 +593,13 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec_seg(SpecArgs a) {
                 const int it = lane + 64 * j;
                 if (it >= FPG * 161) break;
                 const int f = it / 161, k = it - 161 * f;
-                float* mf = zwf + f * (2 * ZS);
+                float* mf = zwf + f * SEG_FS;
                 mf[k] = mk[j];
                 mf[320 - k] = mm[j];
             }
-            for (int it = lane; it < FPG * MW; it += 64) {   // bins [321, 321 + MW) read by the padded band dots
-                const int f = it / MW, j = it - MW * f;
-                zwf[f * (2 * ZS) + 321 + j] = 0.f;
+            for (int it = lane; it < FPG * SEG_MW; it += 64) {   // bins [321, 321 + SEG_MW) read by the padded band dots
+                const int f = it / SEG_MW, j = it - SEG_MW * f;
+                zwf[f * SEG_FS + 321 + j] = 0.f;
             }
             wave_lds_sync();
         }
@@ -564,19 +614,21 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec_seg(SpecArgs a) {
             db[j] = -INFINITY;
             if (it >= FPG * n_mels) continue;
             const int m = __umul24(it, 43691) >> 17, f = it - 3 * m;   // m = it / 3 (it < 240)
-            const v2f* mf = reinterpret_cast<const v2f*>(zwf + f * (2 * ZS) + mel_st[m]);   // even band starts (host)
-            const float4* wm = melw4 + m * (MW / 4);
-            const int nq = a.mel_seg_nq[j];   // (uniform) quads the pass's bands use: 2-6 of 6 (Slaney widths 5-24)
-            float acc = 0.f;
-#pragma unroll
-            for (int q = 0; q < MW / 4; ++q) {
-                if (q >= nq) break;
-                const float4 w = wm[q];
-                const v2f x0 = mf[2 * q], x1 = mf[2 * q + 1];
-                acc = fmaf(x0.x, w.x, acc);
-                acc = fmaf(x0.y, w.y, acc);
-                acc = fmaf(x1.x, w.z, acc);
-                acc = fmaf(x1.y, w.w, acc);
+            const float4* mf = reinterpret_cast<const float4*>(zwf + f * SEG_FS + mel_st[m]);
+            const float4* wm = melw4 + m * (SEG_MW / 4);
+            // (uniform) quads the pass's bands use: 1-7 of 7 (Slaney widths 5-24 from a 4-aligned start); one
+            // straight-line body per count so that all of a band's LDS reads issue back to back (a loop with a break
+            // waited for each quad in turn).  The extra leading / trailing terms are x * 0 added to an exact 0 or to
+            // the sum: the same value as the sum over the band's own bins.
+            float acc;
+            switch (a.mel_seg_nq4[j]) {
+                case 1: acc = band_dot4<1>(wm, mf); break;
+                case 2: acc = band_dot4<2>(wm, mf); break;
+                case 3: acc = band_dot4<3>(wm, mf); break;
+                case 4: acc = band_dot4<4>(wm, mf); break;
+                case 5: acc = band_dot4<5>(wm, mf); break;
+                case 6: acc = band_dot4<6>(wm, mf); break;
+                default: acc = band_dot4<SEG_MW / 4>(wm, mf); break;
             }
             db[j] = acc > a.amin ? 6.0205999132796239f * __log2f(acc) : a.db_floor;
             vmax = fmaxf(vmax, db[j]);

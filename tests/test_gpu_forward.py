@@ -345,6 +345,26 @@ def test_bf16_fused_per_clip_kernels_match_layer_path(gpu, N):
     assert rel_rms(out_f.reshape(ref.shape), ref) <= BF16_REL, rel_rms(out_f.reshape(ref.shape), ref)
 
 
+def test_serial_audio_branch_is_bitwise_equal(gpu):
+    """Option serial runs the per-layer audio branch (no_audenc) on the caller's stream instead of the side stream
+    that overlaps it with the video branch: the same kernels on the same inputs, so the outputs are bitwise equal,
+    in fp32 and bf16."""
+    from avse_amd import ops
+    from avse_amd.model import KerasModel
+    N = 7
+    model = KerasModel.init(seed=13, randomize=True)
+    mel, video = make_inputs(N, 33)
+    args = [ops.to_device(mel), ops.to_device(video)]
+    for dtype in ("float32", "bfloat16"):
+        dw = ops.DeviceWeights(model, dtype)
+        with dw.ctx.options(no_audenc=1):
+            side = ops.forward(dw, *args).cpu().numpy()
+        with dw.ctx.options(no_audenc=1, serial=1):
+            assert dw.ctx.get_option("serial") == 1
+            ser = ops.forward(dw, *args).cpu().numpy()
+        assert np.array_equal(side, ser), (dtype, float(np.abs(side - ser).max()))
+
+
 def test_gemm_ksplit1_small_batch(gpu):
     """k_gemm's unsplit epilogue (ksplit == 1, option gemm_ksplit_cap=1) at a small batch against the split
     path and the oracle: every dense layer and v_conv6 then run the non-split store."""
