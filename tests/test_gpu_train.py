@@ -136,8 +136,9 @@ def test_max_batch_1023_equals_repeated_small_batch(gpu):
     check_gradients(g1023, ref_g, tol=2e-2)
 
 
-def test_adam_steps_match_oracle(gpu):
-    """Three fit steps.  Adam normalises each gradient element by its own running RMS, so its first steps are
+@pytest.mark.parametrize("N", [4, 16])
+def test_adam_steps_match_oracle(gpu, N):
+    """Three fit steps, at N = 4 and at the reference's fit batch of 16 (network.py:203).  Adam normalises each gradient element by its own running RMS, so its first steps are
     ~lr * sign(g): elements whose gradient is within float32 noise of zero move by +-lr on either side.  The
     update arithmetic is therefore checked on the device's own gradients (Keras 2.0 Adam restated in float64,
     every tensor, relative 5e-4 of the update: the float32 parameter itself rounds at ~1e-7 of a unit-size gamma
@@ -147,8 +148,8 @@ def test_adam_steps_match_oracle(gpu):
     from avse_amd.model import KerasModel
     model = KerasModel.init(seed=3, randomize=True)
     rng = np.random.default_rng(77)
-    batches = [batch(rng, 4) + (100 + i,) for i in range(3)]
-    tr = ops.Trainer(model, max_batch=4, device=gpu)
+    batches = [batch(rng, N) + (100 + i,) for i in range(3)]
+    tr = ops.Trainer(model, max_batch=N, device=gpu)
     params = {n: a.astype(np.float64) for n, a in model.tensors.items()}
     m = {n: np.zeros_like(a) for n, a in params.items()}
     v = {n: np.zeros_like(a) for n, a in params.items()}
@@ -162,9 +163,16 @@ def test_adam_steps_match_oracle(gpu):
     for name, ref in params.items():
         if name.endswith(("moving_mean", "moving_variance")):
             continue
-        e = rel_rms(got[name].astype(np.float64) - model.tensors[name], ref - model.tensors[name])
-        if e > 5e-4:
-            bad[name] = e
+        p0 = model.tensors[name]
+        d_got, d_ref = got[name].astype(np.float64) - p0, ref - p0
+        # relative 5e-4 of the update, plus the rounding of the stored float32 parameter (half an ulp per step): the
+        # biases of the dense layers before BatchNormalization get gradients at float32 noise level (BN cancels a
+        # bias), so at N = 16 their updates are a few ulps of the bias and the rounding is most of the difference
+        ulp = np.spacing(np.abs(p0).astype(np.float32)).astype(np.float64)
+        err = float(np.sqrt(np.mean((d_got - d_ref) ** 2)))
+        bound = 5e-4 * float(np.sqrt(np.mean(d_ref ** 2))) + 1.5 * float(np.sqrt(np.mean(ulp ** 2)))
+        if err > bound:
+            bad[name] = (err, bound, rel_rms(d_got, d_ref))
     assert not bad, sorted(bad.items())
     _, ref_losses = KT.train_steps(model.tensors, batches, lr=5e-4, rate=0.25)
     np.testing.assert_allclose(losses, ref_losses, rtol=1e-3)
