@@ -4,13 +4,14 @@
 // Design (every choice measured with tools/halo_ablate.hip / tools/stream_ablate.hip at the v_conv2
 // bench shape; MFMA work alone runs at ~90% of the bf16 peak, so everything else must hide under it):
 //   * 512 threads = 4 compute waves + 4 loader waves, one of each per SIMD (244 VGPRs: two waves fit).
-//     Compute waves only read fragments from LDS, issue v_mfma_f32_32x32x16_bf16 (32-cycle MFMAs leave
-//     24 issue cycles each) and run the epilogue; they hold issue priority.  Loader waves do all address
-//     arithmetic, global loads and LDS stores.  With one wave per SIMD doing both, that work (~120
-//     instructions per step) did not fit in the MFMA shadow and cost +60%;
-//   * each compute wave owns 64 conv pixels x 128 output channels (2 x 4 blocks of 32 x 32): per
-//     32-channel K-slice it reads 4 A + 8 B fragments (12 KB for 16 MFMAs), 25% fewer LDS bytes per
-//     FLOP than 8 waves of 64 x 64, and keeps its 128 accumulators in place for the whole tile;
+//     Compute waves only read fragments from LDS, issue the MFMAs and run the epilogue; they hold issue
+//     priority.  Loader waves do all address arithmetic, global loads and LDS stores.  With one wave per
+//     SIMD doing both, that work (~120 instructions per step) did not fit in the MFMA shadow and cost +60%;
+//   * each compute wave owns 64 conv pixels x 128 output channels and keeps its 128 accumulators in place
+//     for the whole tile: per 32-channel K-slice it reads 4 A + 8 B fragments (12 KB), 25% fewer LDS bytes
+//     per FLOP than 8 waves of 64 x 64.  Default (M16): 32 v_mfma_f32_16x16x32_bf16 per slice over 4x4-pixel
+//     blocks (the chip holds a higher clock under this shape on random data); option mfma32: 16
+//     v_mfma_f32_32x32x16_bf16 over 2 x 4 blocks of 32 x 32 (measured slower);
 //   * the workgroup is persistent over tiles; one K-slice per step, one barrier per step;
 //   * per step each loader lane issues two 16-byte weight loads (the slice LAT+2 steps ahead) and, on
 //     the first HPW taps of a chunk, one 1-KB piece of the input window of the chunk after next, into a
