@@ -337,69 +337,131 @@ __device__ __forceinline__ void flush_partial(float (&acc)[A][B], float (&p)[A][
         }
 }
 
+// Block = 64 a x 64 b of one tap over one split of the rows: 4 waves of 32 a x 32 b, each 2 x 2 exact-fp32 MFMAs
+// (v_mfma_f32_16x16x4_f32: M = a, N = b, K = 4 rows) per 4-row step of a WG_CH-row chunk staged in LDS; the next chunk's
+// global loads are issued before the current chunk's MFMAs.  (Round 2's VALU form — 4 x 4 FMAs per thread — ran at
+// ~55 TFLOP/s: 0.97 ms of a 8.4-ms batch-16 step for v_conv2's gradient alone.)
+constexpr int WG_P = 80;   // LDS row pitch (floats): rows k and k + 1 of an operand read land 16 banks apart
+constexpr int WG_CH = 32;   // rows per LDS chunk (two barriers per chunk; 16 measured the same)
 __global__ __launch_bounds__(256) void k_wgrad(WgArgs w) {
-    __shared__ float gs[16][68], hs[16][68];
-    const int tid = threadIdx.x, ta = tid >> 4, tb = tid & 15;
+    __shared__ __attribute__((aligned(16))) float gs[WG_CH][WG_P], hs[WG_CH][WG_P];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int nbt = (w.B + 63) / 64;
     const int a0 = (blockIdx.x / nbt) * 64, b0 = (blockIdx.x % nbt) * 64;
     const int tap = blockIdx.y;
     const int2 t = w.taps[tap];
     const long long R = (long long)w.N * w.Hh * w.Wh;
     const long long r0 = blockIdx.z * w.rows_per_split, r1 = min(R, r0 + w.rows_per_split);
-    float acc[4][4] = {}, p[4][4] = {};
     const int lr = tid >> 4, lc = (tid & 15) * 4;   // loader: row lr of the chunk, 4 columns lc..lc+3
-    for (long long rc = r0; rc < r1; rc += 16) {
-        if (((rc - r0) & (kWgGroup - 1)) == 0) flush_partial(acc, p);
-        const long long r = rc + lr;
-        float4 gv = make_float4(0.f, 0.f, 0.f, 0.f), hv = gv;
-        if (r < r1) {
-            int n, y, x;
-            row_nyx(r, w.Hh, w.Wh, n, y, x);
-            const float* hp = w.H + n * w.h_clip + (long long)(y * w.Wh + x) * w.hcs + b0 + lc;
-            if (b0 + lc + 3 < w.B) hv = make_float4(hp[0], hp[1], hp[2], hp[3]);
+    // the tile's columns inside A / B: whole-float4 loads without per-lane edge tests (wave-uniform branch)
+    const bool full = a0 + 64 <= w.A && b0 + 64 <= w.B;
+    auto load = [&](long long r, int n, int y, int x, float4& gv, float4& hv) {
+        gv = make_float4(0.f, 0.f, 0.f, 0.f);
+        hv = gv;
+        if (r >= r1) return;
+        const float* hp = w.H + n * w.h_clip + (long long)(y * w.Wh + x) * w.hcs + b0 + lc;
+        const int gy = y * w.sy + t.x, gx = x * w.sx + t.y;
+        const bool gin = gy >= 0 && gy < w.Hg && gx >= 0 && gx < w.Wg;
+        const float* gp = w.G + n * w.g_clip + (long long)(gy * w.Wg + gx) * w.gcs + a0 + lc;
+        if (full) {
+            hv = *reinterpret_cast<const float4*>(hp);
+            if (gin) gv = *reinterpret_cast<const float4*>(gp);
+            return;
+        }
+        if (b0 + lc + 3 < w.B) hv = make_float4(hp[0], hp[1], hp[2], hp[3]);
+        else {
+            if (b0 + lc < w.B) hv.x = hp[0];
+            if (b0 + lc + 1 < w.B) hv.y = hp[1];
+            if (b0 + lc + 2 < w.B) hv.z = hp[2];
+        }
+        if (gin) {
+            if (a0 + lc + 3 < w.A) gv = make_float4(gp[0], gp[1], gp[2], gp[3]);
             else {
-                if (b0 + lc < w.B) hv.x = hp[0];
-                if (b0 + lc + 1 < w.B) hv.y = hp[1];
-                if (b0 + lc + 2 < w.B) hv.z = hp[2];
-            }
-            const int gy = y * w.sy + t.x, gx = x * w.sx + t.y;
-            if (gy >= 0 && gy < w.Hg && gx >= 0 && gx < w.Wg) {
-                const float* gp = w.G + n * w.g_clip + (long long)(gy * w.Wg + gx) * w.gcs + a0 + lc;
-                if (a0 + lc + 3 < w.A) gv = make_float4(gp[0], gp[1], gp[2], gp[3]);
-                else {
-                    if (a0 + lc < w.A) gv.x = gp[0];
-                    if (a0 + lc + 1 < w.A) gv.y = gp[1];
-                    if (a0 + lc + 2 < w.A) gv.z = gp[2];
-                }
+                if (a0 + lc < w.A) gv.x = gp[0];
+                if (a0 + lc + 1 < w.A) gv.y = gp[1];
+                if (a0 + lc + 2 < w.A) gv.z = gp[2];
             }
         }
+    };
+    // MFMA operands: lane l reads row 4 ks + (l >> 4) of the chunk, column (l & 15) of its 16-wide a / b block
+    const int wa = (wave >> 1) * 32, wb = (wave & 1) * 32, kr = lane >> 4, kc = lane & 15;
+    f32x4 acc[2][2], p[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = p[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    constexpr int LPT = WG_CH / 16;   // rows each thread stages per chunk
+    // a thread's rows advance by WG_CH per chunk: (n, y, x) stepped in place when a grid row holds >= WG_CH pixels
+    // (at most one wrap), else re-derived by division (the divisions were most of the loader's instructions)
+    const bool step_in_place = w.Wh >= WG_CH;
+    float4 gv[LPT], hv[LPT];
+    int cn[LPT], cy[LPT], cx[LPT];
+#pragma unroll
+    for (int u = 0; u < LPT; ++u) {
+        const long long r = r0 + lr + 16 * u;
+        if (r < r1) row_nyx(r, w.Hh, w.Wh, cn[u], cy[u], cx[u]);
+        else cn[u] = cy[u] = cx[u] = 0;
+        load(r, cn[u], cy[u], cx[u], gv[u], hv[u]);
+    }
+    for (long long rc = r0; rc < r1; rc += WG_CH) {
+        if (((rc - r0) & (kWgGroup - 1)) == 0 && rc != r0) {   // two-level row sums (see kWgGroup)
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    acc[i][j] += p[i][j];
+                    p[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+                }
+        }
+        __syncthreads();   // the previous chunk's operand reads are done
+#pragma unroll
+        for (int u = 0; u < LPT; ++u) {
+            *reinterpret_cast<float4*>(&gs[lr + 16 * u][lc]) = gv[u];
+            *reinterpret_cast<float4*>(&hs[lr + 16 * u][lc]) = hv[u];
+        }
         __syncthreads();
-        *reinterpret_cast<float4*>(&gs[lr][lc]) = gv;
-        *reinterpret_cast<float4*>(&hs[lr][lc]) = hv;
-        __syncthreads();
+        if (rc + WG_CH < r1)
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const float4 ga = *reinterpret_cast<const float4*>(&gs[k][ta * 4]);
-            const float4 hb = *reinterpret_cast<const float4*>(&hs[k][tb * 4]);
-            const float av[4] = {ga.x, ga.y, ga.z, ga.w}, bv[4] = {hb.x, hb.y, hb.z, hb.w};
+            for (int u = 0; u < LPT; ++u) {
+                const long long r = rc + WG_CH + lr + 16 * u;
+                if (step_in_place) {
+                    cx[u] += WG_CH;
+                    if (cx[u] >= w.Wh) {
+                        cx[u] -= w.Wh;
+                        if (++cy[u] == w.Hh) {
+                            cy[u] = 0;
+                            ++cn[u];
+                        }
+                    }
+                } else if (r < r1) {
+                    row_nyx(r, w.Hh, w.Wh, cn[u], cy[u], cx[u]);
+                }
+                load(r, cn[u], cy[u], cx[u], gv[u], hv[u]);
+            }
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+        for (int ks = 0; ks < WG_CH / 4; ++ks) {
+            const float* gr = &gs[4 * ks + kr][0];
+            const float* hr = &hs[4 * ks + kr][0];
+            const float av[2] = {gr[wa + kc], gr[wa + 16 + kc]}, bv[2] = {hr[wb + kc], hr[wb + 16 + kc]};
 #pragma unroll
-                for (int j = 0; j < 4; ++j) p[i][j] = fmaf(av[i], bv[j], p[i][j]);
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) p[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[j], p[i][j], 0, 0, 0);
         }
     }
-    flush_partial(acc, p);
     float* out = w.part + ((long long)blockIdx.z * w.ntaps + tap) * w.A * w.B;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int a = a0 + ta * 4 + i;
-        if (a >= w.A) continue;
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int b = b0 + tb * 4 + j;
-            if (b < w.B) out[(long long)a * w.B + b] = acc[i][j];
+        for (int j = 0; j < 2; ++j) {
+            const f32x4 v = acc[i][j] + p[i][j];
+            const int b = b0 + wb + 16 * j + kc;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int a = a0 + wa + 16 * i + 4 * kr + e;   // D row 4 (l >> 4) + e, column l & 15
+                if (a < w.A && b < w.B) out[(long long)a * w.B + b] = v[e];
+            }
         }
-    }
 }
 
 // Narrow-A variant (A <= 8: v_conv1's 5 input frames, d_deconv6's single output channel): block tile 8 a x 128 b,
@@ -646,6 +708,7 @@ struct avse_trainer {
     long long red_floats = 0;
     float* wpart = nullptr;   // wgrad split partials
     long long wpart_floats = 0;
+    float* kpart = nullptr;   // split-K partials of the short-grid input-gradient convolutions (train_split)
     float* loss = nullptr;
     std::vector<void*> allocs;
 };
@@ -867,6 +930,7 @@ bool wg_all_taps(const TLayer& T) {
 // wgrad work split over the reduction rows: ~2048 blocks in total, >= 256 rows per split (k_wgrad_nat: ~512
 // blocks of >= 256 rows, each covering every tap: its partials are 25 taps deep)
 constexpr long long kNatMaxRows = 2048;
+constexpr long long kSplitTiles = 1024;   // train_split: tiles x splits per launch (its workspace: 128 x 128 floats each)
 long long wg_splits(const TLayer& T, int64_t N) {
     const LayerDef& L = T.L;
     const int A = (L.kind == DECONV) ? L.cout : L.cin, B = (L.kind == DECONV) ? L.cin : L.cout;
@@ -920,6 +984,7 @@ int alloc_tensors(avse_trainer* t) {
     if (int rc = talloc(t, &t->ghat, zmax)) return rc;
     t->red_floats = std::max(red, 2LL * (2048 + 64) * 64 + 4096);   // colred's nblk * C <= (2048 + 64) * 64 (x2 MODE 2)
     if (int rc = talloc(t, &t->red, t->red_floats)) return rc;
+    if (int rc = talloc(t, &t->kpart, kSplitTiles * 128LL * 128)) return rc;
     t->wpart_floats = wmax;
     if (int rc = talloc(t, &t->wpart, wmax)) return rc;
     if (int rc = talloc(t, &t->loss, 1)) return rc;
@@ -1047,6 +1112,30 @@ int colred(avse_trainer* t, const float* x, int ld, const float* z, const float*
     hipLaunchKernelGGL(k_colfinish<STAGE>, dim3(C), dim3(256), 0, s, t->red, (int)nblk, C, M, fmean, finv, mm, mv, o0, o1);
     AVSE_HIP_CHECK(hipGetLastError());
     return 0;
+}
+
+// Split-K for the short grids of a training batch's input-gradient convolutions: at batch 16 the dgrad launches of
+// v_conv4..v_conv6 and the dense layers ran 11-64 workgroups (one 128-row tile of 16 clips for enc_dense) over K up to
+// 5,248 — 0.1-0.32 ms each.  Single-phase launches under 256 tiles double their split while the grid stays <= 1,024
+// workgroups and every split keeps >= 16 slabs (the inference planner's rule, capi.hip choose_ksplit);
+// k_splitk_reduce_tiles applies the same epilogue.  Batch-16 step 8.0 -> 6.55 ms.  The forward convolutions are not
+// split: that measured a further -0.22 ms, but its different fp32 summation order moves pre-activation values that
+// sit within rounding of a LeakyReLU kink or a max-pool tie to the other side on the reference-batch fixture of
+// tests/test_gpu_train.py (v_conv4's: 1.7e-2 on every upstream video gradient against the 1e-2 gate; other batches
+// 2e-5..1.5e-3), and the forward must keep the summation the parity gate was pinned on.
+void train_split(avse_trainer* t, ConvArgs& a) {
+    if (a.nphase != 1) return;
+    const long long M = (long long)a.N * a.Hq * a.Wq;
+    const int BN = a.Co <= 64 ? 64 : 128;
+    const long long tiles = ((M + 127) / 128) * ((a.Co + BN - 1) / BN);
+    if (tiles >= 256) return;
+    const int nslab = a.ph[0].kpad / 16;
+    int ks = 1;
+    while (tiles * ks * 2 <= kSplitTiles && nslab / (ks * 2) >= 16) ks *= 2;
+    if (ks > 1) {
+        a.ksplit = ks;
+        a.partial = t->kpart;
+    }
 }
 
 int wgrad(avse_trainer* t, const TLayer& T, const float* dz, int64_t N, hipStream_t s) {
@@ -1179,6 +1268,7 @@ int step_impl(avse_trainer* t, const float* audio, const float* video, const flo
         if (int rc = wgrad(t, T, dz, N, s)) return rc;
         if (T.dgrad) {
             ConvArgs a = dgrad_args(t, T, dz, N);
+            train_split(t, a);
             if (int rc = launch_conv(a, AVSE_F32, s)) return rc;
             if ((flags & AVSE_TRAIN_DEBUG_GIN) && (flags >> 8) == i) {   // debug: dL/d(input) of layer i in the scratch
                 AVSE_HIP_CHECK(hipMemcpyAsync(t->ghat, T.gin, sizeof(float) * N * T.in_clip, hipMemcpyDeviceToDevice, s));
