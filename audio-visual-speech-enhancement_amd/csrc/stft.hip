@@ -488,6 +488,12 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec_seg(SpecArgs a) {
     int tid = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int n_mels = a.n_mels;
+    // the first utterance's samples are requested before the tables, so both latencies overlap
+    v2f* zw = zbuf + wave * FPG * ZS;
+    float* zwf = reinterpret_cast<float*>(zw);
+    const long long n_utt = a.n_utt;
+    long long u = blockIdx.x;
+    if (u < n_utt) seg_dma(zwf, a.sig + u * SEG_L, wave, tid & 63, a.pad_mode);
     for (int i = tid; i < 320; i += 64 * WAVES) {
         if (i < 19 * 16) {
             const float2 w = a.twiddle[2 * (i & 15) * ((i >> 4) + 1)];
@@ -506,11 +512,7 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec_seg(SpecArgs a) {
     }
     for (int i = tid; i < n_mels; i += 64 * WAVES) mel_st[i] = a.mel_start[i] & ~3;
 
-    v2f* zw = zbuf + wave * FPG * ZS;
-    float* zwf = reinterpret_cast<float*>(zw);
-    const long long n_utt = a.n_utt;
-    long long u = blockIdx.x;
-    if (u < n_utt) seg_dma(zwf, a.sig + u * SEG_L, wave, tid & 63, a.pad_mode);
+    lds_barrier();   // the tables are complete before any wave's step 1 (the first utterance's samples stay in flight)
     int parity = 0;
     for (; u < n_utt; u += gridDim.x, parity ^= 1) {
         // the per-lane index math stays inside the loop: hoisted out of it, the loop-invariant addresses held more
