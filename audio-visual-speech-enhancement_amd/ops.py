@@ -53,6 +53,8 @@ def spectrogram(sig, sample_rate=16000, n_fft=640, hop_length=160, n_mels=80, fm
             raise ValueError(f"out must be {shape} on {sig.device}")
     stft = torch.empty((U, 1 + n_fft // 2, T, 2), dtype=torch.float32, device=sig.device) if return_stft else None
     pm = {"reflect": _lib.AVSE_PAD_REFLECT, "constant": _lib.AVSE_PAD_CONSTANT}[pad_mode]
+    if U == 0:   # empty batch: empty outputs (the C-ABI takes no NULL buffers, even for zero utterances)
+        return (out, torch.view_as_complex(stft)) if return_stft else out
     ctx = _lib.context(sig.device)
     with torch.cuda.device(sig.device):
         _lib.check(_lib.load().avse_spectrogram(
@@ -93,6 +95,8 @@ def istft(mel_db, stft, sample_rate=16000, n_fft=640, hop_length=160, n_mels=80,
         mel_db = mel_db[:, :, :T].contiguous()
         spf = 0
     out = torch.empty((U, hop_length * (T - 1)), dtype=torch.float32, device=mel_db.device)
+    if U == 0:
+        return out
     ctx = _lib.context(mel_db.device)
     with torch.cuda.device(mel_db.device):
         _lib.check(_lib.load().avse_istft(ctx.handle, _lib.ptr(mel_db), _lib.ptr(stft), U, int(T), int(T_stft), int(spf),
@@ -163,6 +167,8 @@ def forward(weights, audio, video, vnorm_mean=None, vnorm_std=None, out=None):
     _dev_f32(out, "out", (80, weights.T))
     if out.device != audio.device or out.shape[0] != N:
         raise ValueError(f"out must be [N, 80, {weights.T}] on the inputs' device")
+    if N == 0:
+        return out
     with torch.cuda.device(audio.device):
         _lib.check(_lib.load().avse_forward(weights.ctx.handle, weights.handle, _lib.ptr(audio), _lib.ptr(video),
                                             _lib.ptr(vnorm_mean), _lib.ptr(vnorm_std), N, _lib.ptr(out),
@@ -189,6 +195,8 @@ def video_normalize_(video, mean, std):
     _dev_f32(mean, "mean")
     _dev_f32(std, "std")
     S, H, W, F = video.shape
+    if S == 0:
+        return video
     ctx = _lib.context(video.device)
     with torch.cuda.device(video.device):
         _lib.check(_lib.load().avse_video_normalize(ctx.handle, _lib.ptr(video), S, H, W, F, _lib.ptr(mean),
