@@ -207,6 +207,10 @@ struct ConvArgs {
     ConvPhase ph[MAX_PHASES];
 };
 
+// k_conv's fp32 blocked summation: K-slabs (16 products each) summed FP32_BLOCK at a time into a zeroed partial that
+// is added to the running sum in slab order.  A split-K whose every split is exactly one such block, reduced in split
+// order, therefore reproduces the unsplit sums bit for bit (train.hip train_split).
+constexpr int kFp32Block = 8;
 int launch_conv(const ConvArgs& a, int dtype, hipStream_t s);
 
 // fused decoder tail d_deconv4 -> d_deconv5 -> d_deconv6, one workgroup per clip (conv_dec.hip, bf16)

@@ -70,7 +70,7 @@ template <typename T, int BN, bool FAST> constexpr int conv_occupancy() {
 // fp32 blocked summation: the K loop accumulates FP32_BLOCK slabs (FP32_BLOCK * 16 products per output) into a
 // zeroed partial that is then added to the running sum, so the running sum takes K / 128 roundings instead of
 // K / 4 (one per 16x16x4 MFMA).
-constexpr int FP32_BLOCK = 8;
+constexpr int FP32_BLOCK = kFp32Block;   // avse_common.h (train.hip's block-exact split-K plans on it)
 
 template <typename T, int BN, bool FAST>
 __global__ __launch_bounds__(256, (conv_occupancy<T, BN, FAST>())) void k_conv(ConvArgs a) {

@@ -708,7 +708,7 @@ struct avse_trainer {
     long long red_floats = 0;
     float* wpart = nullptr;   // wgrad split partials
     long long wpart_floats = 0;
-    float* kpart = nullptr;   // split-K partials of the short-grid input-gradient convolutions (train_split)
+    float* kpart = nullptr;   // split-K partials of the short-grid convolutions (train_split)
     float* loss = nullptr;
     std::vector<void*> allocs;
 };
@@ -930,7 +930,7 @@ bool wg_all_taps(const TLayer& T) {
 // wgrad work split over the reduction rows: ~2048 blocks in total, >= 256 rows per split (k_wgrad_nat: ~512
 // blocks of >= 256 rows, each covering every tap: its partials are 25 taps deep)
 constexpr long long kNatMaxRows = 2048;
-constexpr long long kSplitTiles = 1024;   // train_split: tiles x splits per launch (its workspace: 128 x 128 floats each)
+constexpr long long kSplitTiles = 2048;   // train_split: tiles x splits per launch (its workspace: 128 x 128 floats each)
 long long wg_splits(const TLayer& T, int64_t N) {
     const LayerDef& L = T.L;
     const int A = (L.kind == DECONV) ? L.cout : L.cin, B = (L.kind == DECONV) ? L.cin : L.cout;
@@ -1114,15 +1114,14 @@ int colred(avse_trainer* t, const float* x, int ld, const float* z, const float*
     return 0;
 }
 
-// Split-K for the short grids of a training batch's input-gradient convolutions: at batch 16 the dgrad launches of
+// Split-K for the short grids of a training batch (fp32): at batch 16 the forward and input-gradient launches of
 // v_conv4..v_conv6 and the dense layers ran 11-64 workgroups (one 128-row tile of 16 clips for enc_dense) over K up to
-// 5,248 — 0.1-0.32 ms each.  Single-phase launches under 256 tiles double their split while the grid stays <= 1,024
-// workgroups and every split keeps >= 16 slabs (the inference planner's rule, capi.hip choose_ksplit);
-// k_splitk_reduce_tiles applies the same epilogue.  Batch-16 step 8.0 -> 6.55 ms.  The forward convolutions are not
-// split: that measured a further -0.22 ms, but its different fp32 summation order moves pre-activation values that
-// sit within rounding of a LeakyReLU kink or a max-pool tie to the other side on the reference-batch fixture of
-// tests/test_gpu_train.py (v_conv4's: 1.7e-2 on every upstream video gradient against the 1e-2 gate; other batches
-// 2e-5..1.5e-3), and the forward must keep the summation the parity gate was pinned on.
+// 5,248.  Each split is exactly one block of k_conv's blocked fp32 summation (kFp32Block slabs) and
+// k_splitk_reduce_tiles adds the splits in order, so every sum is the unsplit kernel's bit for bit: ((0 + b0) + b1)
+// + ... either way.  (A split on the inference planner's rule — a few long splits — moved forward values within
+// rounding of a LeakyReLU kink or pool tie to the other side: 1.7e-2 on the upstream video gradients of the
+// test_gradients_match_oracle fixture)  Launches with >= 256 tiles, more than kSplitTiles
+// tile-splits, or a slab count whose even split is not exactly one block stay unsplit.
 void train_split(avse_trainer* t, ConvArgs& a) {
     if (a.nphase != 1) return;
     const long long M = (long long)a.N * a.Hq * a.Wq;
@@ -1130,12 +1129,10 @@ void train_split(avse_trainer* t, ConvArgs& a) {
     const long long tiles = ((M + 127) / 128) * ((a.Co + BN - 1) / BN);
     if (tiles >= 256) return;
     const int nslab = a.ph[0].kpad / 16;
-    int ks = 1;
-    while (tiles * ks * 2 <= kSplitTiles && nslab / (ks * 2) >= 16) ks *= 2;
-    if (ks > 1) {
-        a.ksplit = ks;
-        a.partial = t->kpart;
-    }
+    const int ks = (nslab + kFp32Block - 1) / kFp32Block;
+    if (ks < 2 || (nslab + ks - 1) / ks != kFp32Block || tiles * ks > kSplitTiles) return;
+    a.ksplit = ks;
+    a.partial = t->kpart;
 }
 
 int wgrad(avse_trainer* t, const TLayer& T, const float* dz, int64_t N, hipStream_t s) {
@@ -1196,6 +1193,7 @@ int step_impl(avse_trainer* t, const float* audio, const float* video, const flo
         TLayer& T = t->layers[i];
         const LayerDef& L = T.L;
         ConvArgs a = fwd_args(t, T, N);
+        train_split(t, a);
         if (int rc = launch_conv(a, AVSE_F32, s)) return rc;
         if (!L.bn) continue;
         const int C = L.bn_channels;
