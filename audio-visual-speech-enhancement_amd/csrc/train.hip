@@ -24,7 +24,8 @@
 //             convs, dense as a GEMM with the Keras (in, out) matrix)
 //   update    k_adam over the whole canonical parameter blob (moving statistics carry zero gradient: unchanged)
 // Parameters, gradients and Adam moments live in the canonical blob layout (include/avse.h avse_weights_load), so
-// export is a copy; forward / dgrad weight packings are gathered from it by index maps built once on the host.
+// export is a copy; forward / dgrad weight packings are written from it each step by k_pack, whose 64 x 64 tile
+// list is built once on the host and checked there against the element-wise index maps.
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -58,11 +59,31 @@ inline unsigned grid_for(long long n, int block = 256, long long cap = 8192) {
     return (unsigned)g;
 }
 
-__global__ void k_gather(float* __restrict__ dst, const int* __restrict__ map, const float* __restrict__ src, long long n) {
-    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
-        const int j = map[i];
-        dst[i] = j >= 0 ? src[j] : 0.f;
+// One <= 64 x 64 tile of a weight packing: dst[which][dst + r dld + c] = P[src + r sr + c sc].  Every (layer, phase,
+// tap) block of a packing is a strided 2-D view of the Keras kernel: a transpose (sr == 1: conv / dense forward,
+// deconv dgrad) or a row copy (sc == 1).  The tile is read along the unit-stride axis, turned in LDS and written
+// along dst rows, so both sides are coalesced (the index-map gather of round 2 read 4-byte words at a stride of
+// cout: ~0.2 ms per batch-16 step).
+struct PackTile {
+    long long dst, src;
+    int R, C, dld, sr, sc, which;
+};
+
+__global__ __launch_bounds__(256) void k_pack(float* __restrict__ wfwd, float* __restrict__ wdg, const float* __restrict__ P,
+                                              const PackTile* __restrict__ tiles) {
+    __shared__ float tile[64][65];
+    const PackTile T = tiles[blockIdx.x];
+    const int lo = threadIdx.x & 63, hi = threadIdx.x >> 6;
+    if (T.sr == 1) {
+        if (lo < T.R)
+            for (int c = hi; c < T.C; c += 4) tile[lo][c] = P[T.src + lo + (long long)c * T.sc];
+    } else if (lo < T.C) {
+        for (int r = hi; r < T.R; r += 4) tile[r][lo] = P[T.src + (long long)r * T.sr + (long long)lo * T.sc];
     }
+    __syncthreads();
+    float* __restrict__ dst = T.which ? wdg : wfwd;
+    if (lo < T.C)
+        for (int r = hi; r < T.R; r += 4) dst[T.dst + (long long)r * T.dld + lo] = tile[r][lo];
 }
 
 // video [N][128][128][F] -> (x - mean) / std (VideoNormalizer, data_processor.py:208-212) -> [N][128][128][8]
@@ -700,7 +721,8 @@ struct avse_trainer {
     std::vector<TLayer> layers;
     float *P = nullptr, *Gr = nullptr, *Mo = nullptr, *Vo = nullptr;
     float *wfwd = nullptr, *wdg = nullptr;
-    int *map_fwd = nullptr, *map_dg = nullptr;
+    PackTile* pack_tiles = nullptr;   // k_pack work list (forward + dgrad packings)
+    long long n_pack_tiles = 0;
     long long n_fwd = 0, n_dg = 0;
     float *ones = nullptr, *zeros = nullptr;
     float *in_audio = nullptr, *in_video = nullptr, *concat = nullptr, *g6 = nullptr, *ghat = nullptr;
@@ -739,10 +761,37 @@ long long kidx(const LayerDef& L, int ky, int kx, int ci, int co) {
     return (((long long)ky * L.kw + kx) * L.cout + co) * L.cin + ci;   // transposed conv (kh, kw, cout, cin)
 }
 
+// k_pack tiles of one (layer, phase, tap) block: rows x cols, dst row stride dld, source element (r, c) at
+// src + r sr + c sc (Keras kernel strides from kidx)
+void add_pack_tiles(std::vector<PackTile>& v, int which, long long dst, int dld, long long src, long long sr, long long sc,
+                    int rows, int cols) {
+    for (int r0 = 0; r0 < rows; r0 += 64)
+        for (int c0 = 0; c0 < cols; c0 += 64)
+            v.push_back(PackTile{dst + (long long)r0 * dld + c0, src + r0 * sr + c0 * sc, std::min(64, rows - r0),
+                                 std::min(64, cols - c0), dld, (int)sr, (int)sc, which});
+}
+
+// the packings the tiles write must be exactly the index maps (entries -1: padding, left at the allocation's zero)
+int check_pack_tiles(const std::vector<PackTile>& v, int which, const std::vector<int>& map) {
+    std::vector<int> got(map.size(), -1);
+    for (const PackTile& T : v) {
+        if (T.which != which) continue;
+        for (int r = 0; r < T.R; ++r)
+            for (int c = 0; c < T.C; ++c) {
+                const long long d = T.dst + (long long)r * T.dld + c;
+                if (d < 0 || d >= (long long)map.size() || got[d] != -1) return tfail(AVSE_ERR_INVALID, "pack tiles overlap");
+                got[d] = (int)(T.src + (long long)r * T.sr + (long long)c * T.sc);
+            }
+    }
+    if (got != map) return tfail(AVSE_ERR_INVALID, "pack tiles disagree with the packing map");
+    return 0;
+}
+
 int build_plan(avse_trainer* t, const float* host_blob) {
     t->layers.resize(kNumLayers);
     long long off = 0;
-    std::vector<int> mf, md;   // forward / dgrad gather maps
+    std::vector<int> mf, md;   // forward / dgrad gather maps (the reference the k_pack tiles are checked against)
+    std::vector<PackTile> tiles;
     for (int i = 0; i < kNumLayers; ++i) {
         TLayer& T = t->layers[i];
         const LayerDef& L = t->plan.L[i];
@@ -816,6 +865,12 @@ int build_plan(avse_trainer* t, const float* host_blob) {
                     for (int c = 0; c < L.cin; ++c)
                         mf[base + (size_t)n * kp + j * cp + c] =
                             (int)(T.o_k + kidx(L, ptaps[p][j].first, ptaps[p][j].second, c, n));
+            for (size_t j = 0; j < ptaps[p].size(); ++j) {
+                const int ky = ptaps[p][j].first, kx = ptaps[p][j].second;
+                const long long s0 = kidx(L, ky, kx, 0, 0);
+                add_pack_tiles(tiles, 0, (long long)base + (long long)j * cp, (int)kp, T.o_k + s0,
+                               kidx(L, ky, kx, 0, 1) - s0, kidx(L, ky, kx, 1, 0) - s0, L.cout, L.cin);
+            }
             woff += (long long)L.cout * kp;
         }
         // ---- weight-gradient taps: Keras tap order, offsets (ky - pt, kx - pl) on the strided grid ----
@@ -888,6 +943,12 @@ int build_plan(avse_trainer* t, const float* host_blob) {
                         for (int c = 0; c < L.cout; ++c)   // reduction channel = the layer's output channel
                             md[base + (size_t)n * kp + j * cp + c] =
                                 (int)(T.o_k + kidx(L, dtaps[p][j].first, dtaps[p][j].second, n, c));
+                for (size_t j = 0; j < dtaps[p].size(); ++j) {
+                    const int ky = dtaps[p][j].first, kx = dtaps[p][j].second;
+                    const long long s0 = kidx(L, ky, kx, 0, 0);
+                    add_pack_tiles(tiles, 1, (long long)base + (long long)j * cp, (int)kp, T.o_k + s0,
+                                   kidx(L, ky, kx, 1, 0) - s0, kidx(L, ky, kx, 0, 1) - s0, L.cin, L.cout);
+                }
                 doff += (long long)L.cin * kp;
             }
         }
@@ -896,12 +957,13 @@ int build_plan(avse_trainer* t, const float* host_blob) {
     t->nparams = off;
     t->n_fwd = (long long)mf.size();
     t->n_dg = (long long)md.size();
-    if (int rc = talloc(t, &t->map_fwd, mf.size())) return rc;
-    if (int rc = talloc(t, &t->map_dg, md.size())) return rc;
-    if (int rc = talloc(t, &t->wfwd, mf.size())) return rc;
+    if (int rc = check_pack_tiles(tiles, 0, mf)) return rc;
+    if (int rc = check_pack_tiles(tiles, 1, md)) return rc;
+    t->n_pack_tiles = (long long)tiles.size();
+    if (int rc = talloc(t, &t->pack_tiles, tiles.size())) return rc;
+    if (int rc = talloc(t, &t->wfwd, mf.size())) return rc;   // zeroed: the packings' padding is never written
     if (int rc = talloc(t, &t->wdg, md.size())) return rc;
-    AVSE_HIP_CHECK(hipMemcpy(t->map_fwd, mf.data(), mf.size() * sizeof(int), hipMemcpyHostToDevice));
-    AVSE_HIP_CHECK(hipMemcpy(t->map_dg, md.data(), md.size() * sizeof(int), hipMemcpyHostToDevice));
+    AVSE_HIP_CHECK(hipMemcpy(t->pack_tiles, tiles.data(), tiles.size() * sizeof(PackTile), hipMemcpyHostToDevice));
     for (auto& T : t->layers) {
         if (int rc = talloc(t, &T.d_taps, T.taps.size())) return rc;
         AVSE_HIP_CHECK(hipMemcpy(T.d_taps, T.taps.data(), T.taps.size() * sizeof(int2), hipMemcpyHostToDevice));
@@ -1178,8 +1240,8 @@ int wgrad(avse_trainer* t, const TLayer& T, const float* dz, int64_t N, hipStrea
 int step_impl(avse_trainer* t, const float* audio, const float* video, const float* target, const float* vmean,
               const float* vstd, int64_t N, float lr, float drop, uint32_t seed, int flags, float* loss, hipStream_t s) {
     // ---- weight packings from the current parameters ----
-    hipLaunchKernelGGL(k_gather, dim3(grid_for(t->n_fwd)), dim3(256), 0, s, t->wfwd, (const int*)t->map_fwd, (const float*)t->P, t->n_fwd);
-    hipLaunchKernelGGL(k_gather, dim3(grid_for(t->n_dg)), dim3(256), 0, s, t->wdg, (const int*)t->map_dg, (const float*)t->P, t->n_dg);
+    hipLaunchKernelGGL(k_pack, dim3((unsigned)t->n_pack_tiles), dim3(256), 0, s, t->wfwd, t->wdg, (const float*)t->P,
+                       (const PackTile*)t->pack_tiles);
     AVSE_HIP_CHECK(hipGetLastError());
     AVSE_HIP_CHECK(hipMemsetAsync(t->Gr, 0, sizeof(float) * t->nparams, s));
     // ---- inputs ----
