@@ -274,7 +274,14 @@ __global__ void k_act_bwd(ActArgs a, const float* __restrict__ gout, long long g
     }
 }
 
-// dz = gamma * inv * (g - dbeta / M - xhat * dgamma / M), in place over g
+// dz = gamma * inv * (g - dbeta / M - xhat * dgamma / M), rounded step by step (explicit fmas and _rn products) so
+// the compiler's contraction / hoisting choices cannot make k_bn_bwd and k_bn_bwd_colsum disagree
+__device__ __forceinline__ float bn_bwd_dz(float gv, float xh, float ga, float iv, float db, float dg, float rM) {
+    const float t = fmaf(-__fmul_rn(xh, dg), rM, fmaf(-db, rM, gv));
+    return __fmul_rn(__fmul_rn(ga, iv), t);
+}
+
+// in place over g
 __global__ void k_bn_bwd(const float* __restrict__ z, float* __restrict__ g, long long M, int C, const float* __restrict__ mean,
                          const float* __restrict__ inv, const float* __restrict__ gamma, const float* __restrict__ dbeta,
                          const float* __restrict__ dgamma) {
@@ -283,8 +290,42 @@ __global__ void k_bn_bwd(const float* __restrict__ z, float* __restrict__ g, lon
     for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
         const int c = (int)i % C;   // < 2^31 elements (trainer batch cap)
         const float xh = (z[i] - mean[c]) * inv[c];
-        g[i] = gamma[c] * inv[c] * (g[i] - dbeta[c] * rM - xh * dgamma[c] * rM);
+        g[i] = bn_bwd_dz(g[i], xh, gamma[c], inv[c], dbeta[c], dgamma[c], rM);
     }
+}
+
+// k_bn_bwd fused with the bias gradient's column sums (layers whose BN channels are the conv's output channels): the
+// grid, row partition and summation order of k_colreduce<0> over the dz it writes, so the partials (and, after
+// k_colfinish<3>, the bias gradient) are those of the two-pass path without dz's second read.
+__global__ __launch_bounds__(256) void k_bn_bwd_colsum(const float* __restrict__ z, float* __restrict__ g, long long M, int C,
+                                                       const float* __restrict__ mean, const float* __restrict__ inv,
+                                                       const float* __restrict__ gamma, const float* __restrict__ dbeta,
+                                                       const float* __restrict__ dgamma, long long rows_per_blk,
+                                                       float* __restrict__ part) {
+    __shared__ float s0[4][64];
+    const int tid = threadIdx.x, cl = tid & 63, rg = tid >> 6;
+    const int c = blockIdx.x * 64 + cl;
+    const long long r0 = blockIdx.y * rows_per_blk, r1 = min(M, r0 + rows_per_blk);
+    const float rM = 1.f / (float)M;
+    float a0 = 0.f;
+    if (c < C) {
+        const float mu = mean[c], iv = inv[c], ga = gamma[c], db = dbeta[c], dg = dgamma[c];
+        for (long long gr = r0 + rg; gr < r1; gr += 256) {
+            float p0 = 0.f;
+            const long long ge = min(r1, gr + 256);
+            for (long long r = gr; r < ge; r += 4) {
+                const long long i = r * C + c;
+                const float xh = (z[i] - mu) * iv;
+                const float v = bn_bwd_dz(g[i], xh, ga, iv, db, dg, rM);
+                g[i] = v;
+                p0 = __fadd_rn(p0, v);
+            }
+            a0 += p0;
+        }
+    }
+    s0[rg][cl] = a0;
+    __syncthreads();
+    if (rg == 0 && c < C) part[(long long)blockIdx.y * C + c] = s0[0][cl] + s0[1][cl] + s0[2][cl] + s0[3][cl];
 }
 
 // mean squared error (network.py:36, Keras mean over every element): per-block partial loss + dL/dy (channel stride gcs)
@@ -1159,15 +1200,22 @@ ConvArgs dgrad_args(avse_trainer* t, const TLayer& T, const float* dz, int64_t N
     return a;
 }
 
+// row blocks of a column reduction (k_colreduce, k_bn_bwd_colsum): ~2048 blocks of 64 columns x >= 64 rows
+// (v_conv1's 262k-row reductions ran on 128 blocks: 10 of 19.7 ms/step)
+void colred_grid(long long M, int C, long long* nblk_out, long long* rpb_out) {
+    const long long cblk = (C + 63) / 64;
+    long long nblk = std::min(std::max(1LL, 2048 / cblk), std::max(1LL, (M + 63) / 64));
+    const long long rpb = (M + nblk - 1) / nblk;
+    *nblk_out = (M + rpb - 1) / rpb;
+    *rpb_out = rpb;
+}
+
 // column reduction + finish; returns status
 template <int MODE, int STAGE>
 int colred(avse_trainer* t, const float* x, int ld, const float* z, const float* mean, const float* inv, long long M, int C,
            float* fmean, float* finv, float* mm, float* mv, float* o0, float* o1, hipStream_t s) {
-    // ~2048 blocks of 64 columns x >= 64 rows: v_conv1's 262k-row reductions ran on 128 blocks (10 of 19.7 ms/step)
-    const long long cblk = (C + 63) / 64;
-    long long nblk = std::min(std::max(1LL, 2048 / cblk), std::max(1LL, (M + 63) / 64));
-    const long long rpb = (M + nblk - 1) / nblk;
-    nblk = (M + rpb - 1) / rpb;
+    long long nblk, rpb;
+    colred_grid(M, C, &nblk, &rpb);
     if ((MODE == 2 ? 2 : 1) * nblk * (long long)C > t->red_floats) return tfail(AVSE_ERR_INVALID, "reduction workspace too small");
     hipLaunchKernelGGL(k_colreduce<MODE>, dim3((C + 63) / 64, (unsigned)nblk), dim3(256), 0, s, x, ld, z, mean, inv, M, C, rpb, t->red);
     AVSE_HIP_CHECK(hipGetLastError());
@@ -1292,6 +1340,7 @@ int step_impl(avse_trainer* t, const float* audio, const float* video, const flo
         const LayerDef& L = T.L;
         float* dz;
         const long long Mfull = N * (long long)T.hq * T.wq;
+        bool bias_fused = false;
         if (!L.bn) {
             dz = t->g6;   // dL/dy with the output's 8-channel stride
         } else {
@@ -1315,16 +1364,30 @@ int step_impl(avse_trainer* t, const float* audio, const float* video, const flo
             AVSE_HIP_CHECK(hipGetLastError());
             if (int rc = colred<2, 2>(t, t->ghat, C, T.z, T.mean, T.inv, M, C, nullptr, nullptr, nullptr, nullptr,
                                       t->Gr + T.o_be, t->Gr + T.o_g, s)) return rc;
-            hipLaunchKernelGGL(k_bn_bwd, dim3(grid_for(M * C)), dim3(256), 0, s, (const float*)T.z, t->ghat, M, C,
-                               (const float*)T.mean, (const float*)T.inv, (const float*)(t->P + T.o_g),
-                               (const float*)(t->Gr + T.o_be), (const float*)(t->Gr + T.o_g));
+            bias_fused = (L.cout == C && T.zc == C);
+            if (bias_fused) {   // dz and the bias gradient's column partials in one pass
+                long long nblk, rpb;
+                colred_grid(M, C, &nblk, &rpb);
+                if (nblk * (long long)C > t->red_floats) return tfail(AVSE_ERR_INVALID, "reduction workspace too small");
+                hipLaunchKernelGGL(k_bn_bwd_colsum, dim3((C + 63) / 64, (unsigned)nblk), dim3(256), 0, s, (const float*)T.z,
+                                   t->ghat, M, C, (const float*)T.mean, (const float*)T.inv, (const float*)(t->P + T.o_g),
+                                   (const float*)(t->Gr + T.o_be), (const float*)(t->Gr + T.o_g), rpb, t->red);
+                AVSE_HIP_CHECK(hipGetLastError());
+                hipLaunchKernelGGL(k_colfinish<3>, dim3(C), dim3(256), 0, s, (const float*)t->red, (int)nblk, C, M, nullptr,
+                                   nullptr, nullptr, nullptr, t->Gr + T.o_b, nullptr);
+            } else {
+                hipLaunchKernelGGL(k_bn_bwd, dim3(grid_for(M * C)), dim3(256), 0, s, (const float*)T.z, t->ghat, M, C,
+                                   (const float*)T.mean, (const float*)T.inv, (const float*)(t->P + T.o_g),
+                                   (const float*)(t->Gr + T.o_be), (const float*)(t->Gr + T.o_g));
+            }
             AVSE_HIP_CHECK(hipGetLastError());
             dz = t->ghat;
             if ((flags & AVSE_TRAIN_DEBUG_STOP) && (flags >> 8) == i) return 0;   // debug: dz of layer i in ghat
         }
         // bias: sum of dz over every pixel (per output channel)
-        if (int rc = colred<0, 3>(t, dz, T.zc, nullptr, nullptr, nullptr, Mfull, L.cout, nullptr, nullptr, nullptr, nullptr,
-                                  t->Gr + T.o_b, nullptr, s)) return rc;
+        if (!bias_fused)
+            if (int rc = colred<0, 3>(t, dz, T.zc, nullptr, nullptr, nullptr, Mfull, L.cout, nullptr, nullptr, nullptr, nullptr,
+                                      t->Gr + T.o_b, nullptr, s)) return rc;
         if (int rc = wgrad(t, T, dz, N, s)) return rc;
         if (T.dgrad) {
             ConvArgs a = dgrad_args(t, T, dz, N);
