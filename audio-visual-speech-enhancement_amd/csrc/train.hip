@@ -112,8 +112,8 @@ __global__ void k_prep_audio(const float* __restrict__ a, float* __restrict__ ou
 
 // Column reductions over the rows of a [M][ld] matrix (first C columns), one partial per row block:
 //   MODE 0: sum x                       (means, bias gradients)
-//   MODE 1: sum (x - mean)^2            (biased batch variance, second pass)
 //   MODE 2: sum g, sum g * xhat         (BN backward; xhat = (z - mean) * inv from z)
+//   MODE 3: per block: sum x (= MODE 0's partial) and sum (x - block mean)^2 (BN forward statistics in one launch)
 // grid (ceil(C / 64), nblk), 256 threads = 64 columns x 4 row groups.
 template <int MODE>
 __global__ __launch_bounds__(256) void k_colreduce(const float* __restrict__ x, int ld, const float* __restrict__ z,
@@ -124,8 +124,35 @@ __global__ __launch_bounds__(256) void k_colreduce(const float* __restrict__ x, 
     const int c = blockIdx.x * 64 + cl;
     const long long r0 = blockIdx.y * rows_per_blk, r1 = min(M, r0 + rows_per_blk);
     float a0 = 0.f, a1 = 0.f;
+    if (MODE == 3) {   // this block's sum (exactly MODE 0's partial), its mean, then the squared deviations about it
+        if (c < C)
+            for (long long g = r0 + rg; g < r1; g += 256) {
+                float p0 = 0.f;
+                const long long ge = min(r1, g + 256);
+                for (long long r = g; r < ge; r += 4) p0 += x[r * ld + c];
+                a0 += p0;
+            }
+        s0[rg][cl] = a0;
+        __syncthreads();
+        const float sb = s0[0][cl] + s0[1][cl] + s0[2][cl] + s0[3][cl];
+        const float mb = sb / (float)max(r1 - r0, 1LL);
+        if (c < C)
+            for (long long g = r0 + rg; g < r1; g += 256) {
+                float p1 = 0.f;
+                const long long ge = min(r1, g + 256);
+                for (long long r = g; r < ge; r += 4) { const float d = x[r * ld + c] - mb; p1 = fmaf(d, d, p1); }
+                a1 += p1;
+            }
+        s1[rg][cl] = a1;
+        __syncthreads();
+        if (rg == 0 && c < C) {
+            part[(long long)blockIdx.y * C + c] = sb;
+            part[(long long)(gridDim.y + blockIdx.y) * C + c] = s1[0][cl] + s1[1][cl] + s1[2][cl] + s1[3][cl];
+        }
+        return;
+    }
     if (c < C) {
-        const float mu = (MODE >= 1) ? mean[c] : 0.f;
+        const float mu = (MODE == 2) ? mean[c] : 0.f;
         const float iv = (MODE == 2) ? inv[c] : 0.f;
         // two-level sums (see kWgGroup): partials p0 / p1 over 64 rows per thread, then into a0 / a1
         for (long long g = r0 + rg; g < r1; g += 256) {
@@ -134,7 +161,6 @@ __global__ __launch_bounds__(256) void k_colreduce(const float* __restrict__ x, 
             for (long long r = g; r < ge; r += 4) {
                 const float v = x[r * ld + c];
                 if (MODE == 0) p0 += v;
-                if (MODE == 1) { const float d = v - mu; p0 = fmaf(d, d, p0); }
                 if (MODE == 2) { p0 += v; p1 = fmaf(v, (z[r * C + c] - mu) * iv, p1); }
             }
             a0 += p0;
@@ -153,8 +179,6 @@ __global__ __launch_bounds__(256) void k_colreduce(const float* __restrict__ x, 
 
 // Finish a column reduction in double: one 256-thread block per column, each thread summing a strided subset of the
 // row-block partials, then a fixed LDS tree (deterministic):
-//   STAGE 0: mean[c] = S / M
-//   STAGE 1: var = S / M (biased), inv = 1 / sqrt(var + eps), moving stats <- m * 0.99 + batch * 0.01
 //   STAGE 2: dbeta = S0, dgamma = S1 (into the gradient blob)
 //   STAGE 3: out[c] = S (bias gradient)
 template <int STAGE>
@@ -181,18 +205,50 @@ __global__ __launch_bounds__(256) void k_colfinish(const float* __restrict__ par
     if (tid != 0) return;
     s = rs[0];
     t = rt[0];
-    if (STAGE == 0) mean[c] = (float)(s / (double)M);
-    if (STAGE == 1) {
-        const double var = s / (double)M;
-        inv[c] = (float)(1.0 / std::sqrt(var + (double)kBnEps));
-        mm[c] = mm[c] * BN_MOMENTUM + mean[c] * (1.f - BN_MOMENTUM);
-        mv[c] = mv[c] * BN_MOMENTUM + (float)var * (1.f - BN_MOMENTUM);
-    }
     if (STAGE == 2) {
         out0[c] = (float)s;   // dbeta
         out1[c] = (float)t;   // dgamma
     }
     if (STAGE == 3) out0[c] = (float)s;
+}
+
+// BN forward statistics from MODE 3 partials (Chan et al. pairwise combination in double): mean = S / M (the sums of
+// the former two-pass path, same partials, same order: the same mean), M2 = sum_b M2_b + n_b (mean_b - mean)^2,
+// biased var = M2 / M (Keras 2.0.x), inv = 1 / sqrt(var + eps), moving stats <- m * 0.99 + batch * 0.01
+__global__ __launch_bounds__(256) void k_bnstat_finish(const float* __restrict__ part, int nblk, int C, long long M,
+                                                       long long rpb, float* __restrict__ mean, float* __restrict__ inv,
+                                                       float* __restrict__ mm, float* __restrict__ mv) {
+    __shared__ double rs[256], rt[256];
+    const int c = blockIdx.x, tid = threadIdx.x;
+    double s = 0;
+    for (int b = tid; b < nblk; b += 256) s += part[(long long)b * C + c];
+    rs[tid] = s;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (tid < o) rs[tid] += rs[tid + o];
+        __syncthreads();
+    }
+    const double mu = rs[0] / (double)M;
+    __syncthreads();
+    double t = 0;
+    for (int b = tid; b < nblk; b += 256) {
+        const double nb = (double)min(rpb, M - (long long)b * rpb);
+        const double d = (double)part[(long long)b * C + c] / nb - mu;
+        t += (double)part[(long long)(nblk + b) * C + c] + nb * d * d;
+    }
+    rt[tid] = t;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (tid < o) rt[tid] += rt[tid + o];
+        __syncthreads();
+    }
+    if (tid != 0) return;
+    const float m = (float)mu;
+    const double var = rt[0] / (double)M;
+    mean[c] = m;
+    inv[c] = (float)(1.0 / std::sqrt(var + (double)kBnEps));
+    mm[c] = mm[c] * BN_MOMENTUM + m * (1.f - BN_MOMENTUM);
+    mv[c] = mv[c] * BN_MOMENTUM + (float)var * (1.f - BN_MOMENTUM);
 }
 
 struct ActArgs {
@@ -1309,8 +1365,17 @@ int step_impl(avse_trainer* t, const float* audio, const float* video, const flo
         const int C = L.bn_channels;
         const long long M = N * (long long)T.hq * T.wq * (L.cout / C);
         float* P = t->P;
-        if (int rc = colred<0, 0>(t, T.z, C, nullptr, nullptr, nullptr, M, C, T.mean, nullptr, nullptr, nullptr, nullptr, nullptr, s)) return rc;
-        if (int rc = colred<1, 1>(t, T.z, C, nullptr, T.mean, nullptr, M, C, T.mean, T.inv, P + T.o_mm, P + T.o_mv, nullptr, nullptr, s)) return rc;
+        {   // batch statistics in one pass over z (per-block sums + deviations about the block mean) + one finish
+            long long nblk, rpb;
+            colred_grid(M, C, &nblk, &rpb);
+            if (2 * nblk * (long long)C > t->red_floats) return tfail(AVSE_ERR_INVALID, "reduction workspace too small");
+            hipLaunchKernelGGL(k_colreduce<3>, dim3((C + 63) / 64, (unsigned)nblk), dim3(256), 0, s, (const float*)T.z, C,
+                               nullptr, nullptr, nullptr, M, C, rpb, t->red);
+            AVSE_HIP_CHECK(hipGetLastError());
+            hipLaunchKernelGGL(k_bnstat_finish, dim3(C), dim3(256), 0, s, (const float*)t->red, (int)nblk, C, M, rpb, T.mean,
+                               T.inv, P + T.o_mm, P + T.o_mv);
+            AVSE_HIP_CHECK(hipGetLastError());
+        }
         ActArgs aa;
         std::memset(&aa, 0, sizeof(aa));
         aa.z = T.z; aa.N = (int)N; aa.C = C;
