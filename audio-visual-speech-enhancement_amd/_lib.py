@@ -16,8 +16,10 @@ import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 LIB_PATH = os.environ.get("AVSE_LIBRARY") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libavse.so")
 HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "avse.h")
 
+ABI_VERSION = 2
 AVSE_F32 = 0
 AVSE_BF16 = 1
+AVSE_F32_SPLIT = 2
 AVSE_PAD_REFLECT = 0
 AVSE_PAD_CONSTANT = 1
 AVSE_NUM_STAGES = 22
@@ -38,6 +40,7 @@ SIGNATURES = {
     "avse_ctx_create": (_int, [_int, ctypes.POINTER(_c_void_p)]),
     "avse_ctx_destroy": (None, [_c_void_p]),
     "avse_ctx_reserve": (_int, [_c_void_p, _i64, _int]),
+    "avse_ctx_reserve_weights": (_int, [_c_void_p, _c_void_p, _i64]),
     "avse_ctx_set_option": (_int, [_c_void_p, ctypes.c_char_p, _int]),
     "avse_ctx_get_option": (_int, [_c_void_p, ctypes.c_char_p, ctypes.POINTER(_int)]),
     "avse_spectrogram": (_int, [_c_void_p, _c_void_p, _i64, _i64, _int, _int, _int, _int, _flt, _flt, _flt, _flt,
@@ -108,6 +111,8 @@ def load():
                 fn = getattr(lib, name)
                 fn.restype = res
                 fn.argtypes = args
+            if lib.avse_abi_version() != ABI_VERSION:
+                raise AvseError(f"{LIB_PATH} implements ABI {lib.avse_abi_version()}, this binding ABI {ABI_VERSION}: rebuild it")
             _lib = lib
     return _lib
 
@@ -123,11 +128,16 @@ class Context:
 
     def __init__(self, device_index):
         self.device_index = device_index
+        self._cdll = load()   # held for __del__: module globals may be torn down first at interpreter exit
         self.handle = _c_void_p()
         check(load().avse_ctx_create(device_index, ctypes.byref(self.handle)), "avse_ctx_create")
 
     def reserve(self, max_clips, dtype):
         check(load().avse_ctx_reserve(self.handle, int(max_clips), int(dtype)), "avse_ctx_reserve")
+
+    def reserve_for(self, weights, max_clips):
+        """avse_ctx_reserve_weights: scratch for `weights`' network shape and dtype (ops.DeviceWeights)."""
+        check(load().avse_ctx_reserve_weights(self.handle, weights.handle, int(max_clips)), "avse_ctx_reserve_weights")
 
     def set_option(self, name, value):
         """avse_ctx_set_option: a kernel-path switch (include/avse.h), e.g. "no_gemm"."""
@@ -151,9 +161,9 @@ class Context:
                 self.set_option(k, v)
 
     def __del__(self):
-        h = getattr(self, "handle", None)
-        if h is not None and h.value and _lib is not None:
-            _lib.avse_ctx_destroy(h)
+        h, lib = getattr(self, "handle", None), getattr(self, "_cdll", None)
+        if h is not None and h.value and lib is not None:
+            lib.avse_ctx_destroy(h)
             self.handle = None
 
 

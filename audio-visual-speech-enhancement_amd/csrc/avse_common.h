@@ -6,6 +6,7 @@
 
 typedef __bf16 bf16_t;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 
@@ -292,6 +293,9 @@ int launch_dec_tail(const DecTailArgs& a, hipStream_t s);
 
 // ---- tiled bf16 video convolutions: conv_v1r.hip (v_conv1), conv_stream.hip (v_conv2..v_conv5) ----
 enum HaloVariant { HALO_NONE = -1, HALO_V1 = 0, HALO_K5 = 1, HALO_K3_16 = 2, HALO_K3_8 = 3 };
+// output element format of the tiled video convolutions: bf16; split f16 pairs (per pixel and 16 channels,
+// [h(16) | l(16)] with h = f16(x), l = f16(x - h): the next split layer's input); f32
+enum HaloOut { OUT_BF16 = 0, OUT_S16 = 1, OUT_F32 = 2 };
 
 struct HaloArgs {
     int variant;
@@ -308,6 +312,9 @@ struct HaloArgs {
     int out_pix_stride;
     int out_c_off;
     int mfma32;              // conv_stream.hip: 1 = v_mfma_f32_32x32x16_bf16 compute waves (A/B variant)
+    int split;               // 1 = split-f16 operands (AVSE_F32_SPLIT): in is the split-pair layout, Ci counts halves
+                             // (2 x channels), w holds [Bh | Bl] rows; out_mode OUT_S16 or OUT_F32
+    int out_mode;            // HaloOut
     unsigned long long* prof;   // ablation harness only (ABL & 128): per-wave cycle counters, else unused
 };
 

@@ -92,6 +92,18 @@ struct SpecTables {
 // ---------------------------------------------------------------------------------------------
 // network plan (network.py:17-175)
 // ---------------------------------------------------------------------------------------------
+uint16_t f2h(float f) {   // f32 -> f16 bits, round to nearest even (hipcc's host _Float16 conversion)
+    const _Float16 h = (_Float16)f;
+    uint16_t u;
+    std::memcpy(&u, &h, 2);
+    return u;
+}
+float h2f(uint16_t u) {
+    _Float16 h;
+    std::memcpy(&h, &u, 2);
+    return (float)h;
+}
+
 uint16_t f2bf(float f) {
     uint32_t u;
     std::memcpy(&u, &f, 4);
@@ -270,9 +282,19 @@ size_t arena_bytes(int64_t clips, int dtype, const Options& o, size_t* offs, con
     return off;
 }
 
-int ensure_arena(avse_ctx* c, int64_t clips, int dtype, const NetPlan& p) {
+bool valid_dtype(int dtype) { return dtype == AVSE_F32 || dtype == AVSE_BF16 || dtype == AVSE_F32_SPLIT; }
+
+// grows the forward scratch; never while `s` (nullable) is being captured into a graph: the caller must reserve first
+int ensure_arena(avse_ctx* c, int64_t clips, int dtype, const NetPlan& p, hipStream_t s) {
     const size_t need = arena_bytes(clips, dtype, c->opt, nullptr, p);
     if (need <= c->arena_bytes) return 0;
+    if (s) {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        AVSE_HIP_CHECK(hipStreamIsCapturing(s, &cs));
+        if (cs != hipStreamCaptureStatusNone)
+            return fail(AVSE_ERR_INVALID, "the forward scratch would grow while the stream is being captured: call "
+                                          "avse_ctx_reserve_weights(ctx, weights, max_clips) before the capture");
+    }
     if (c->arena) (void)hipFree(c->arena);
     c->arena = nullptr;
     c->arena_bytes = 0;
@@ -580,6 +602,7 @@ int build_layer(avse_weights* W, int li, const float* kernel, const float* bias,
         }
     }
     int rc;
+    const bool split = W->dtype == AVSE_F32_SPLIT;   // generic layers of the split dtype run the fp32 packing
     if (W->dtype == AVSE_BF16) {
         std::vector<uint16_t> pb(packed.size());
         for (size_t i = 0; i < packed.size(); ++i) pb[i] = f2bf(packed[i]);
@@ -607,7 +630,8 @@ int build_layer(avse_weights* W, int li, const float* kernel, const float* bias,
 
     // packing for the bf16 video conv kernels: conv_stream.hip [slice][Cout][32], slice = (cg*4 + cc)*KS^2
     // + tap; conv_v1r.hip (v_conv1) [kernel row][Cout][32].  Options::no_halo keeps the generic k_conv.
-    if (W->dtype == AVSE_BF16 && L.kind == CONV && L.pool && L.hin >= 8 && !opt.no_halo) {
+    // Split dtype: the same kernels on split-f16 operands (see below).
+    if ((W->dtype == AVSE_BF16 || split) && L.kind == CONV && L.pool && L.hin >= 8 && !opt.no_halo) {
         const int ntap = L.kh * L.kw;
         if (L.cin == 5 && L.kh == 5) G.halo = HALO_V1;   // conv_v1r.hip: 5 frames (25 / 29.97 fps)
         else if (L.cin % 128) G.halo = HALO_NONE;         // 6 frames (30 fps): generic k_conv
@@ -623,6 +647,57 @@ int build_layer(avse_weights* W, int li, const float* kernel, const float* bias,
             scale_h[n] = std::fabs(scale[n]);
         }
         if (G.halo == HALO_NONE) return 0;
+        if (split) {
+            // split-f16 operands: output channel n's (sign-folded) weights scaled by 2^e_n, e_n = 14 - ceil(log2 max|w|),
+            // so that hi = f16(w 2^e) stays below 2^15 and lo = f16(w 2^e - hi) keeps full precision for every weight
+            // above 2^-10 of the channel's largest; the BN scale takes 2^-e_n back (powers of two: exact)
+            const int ntap = L.kh * L.kw;
+            std::vector<int> ex(L.cout, 0);
+            for (int n = 0; n < L.cout; ++n) {
+                float mx = 0.f;
+                for (int t = 0; t < ntap; ++t)
+                    for (int c = 0; c < L.cin; ++c) mx = std::max(mx, std::fabs(kernel[((size_t)t * L.cin + c) * L.cout + n]));
+                int e2 = 0;
+                if (mx > 0.f) (void)std::frexp(mx, &e2);   // mx = f 2^e2, f in [0.5, 1)
+                ex[n] = mx > 0.f ? 15 - e2 : 0;              // max|w| 2^e in [2^14, 2^15)
+                scale_h[n] = std::ldexp(scale_h[n], -ex[n]);
+            }
+            auto wsc = [&](int n, float v) { return std::ldexp(sgn[n] * v, ex[n]); };
+            std::vector<uint16_t> sp;
+            if (G.halo == HALO_V1) {
+                // conv_v1r.hip k_conv_v1s: [piece h / l][kernel row ky][Cout][32], k = kx * 6 + frame
+                const size_t img = (size_t)L.kh * L.cout * 32;
+                sp.assign(2 * img, 0);
+                for (int ky = 0; ky < L.kh; ++ky)
+                    for (int n = 0; n < L.cout; ++n)
+                        for (int kx = 0; kx < L.kw; ++kx)
+                            for (int f = 0; f < L.cin; ++f) {
+                                const float v = wsc(n, kernel[((size_t)(ky * L.kw + kx) * L.cin + f) * L.cout + n]);
+                                const uint16_t h = f2h(v);
+                                const size_t o = ((size_t)ky * L.cout + n) * 32 + kx * 6 + f;
+                                sp[o] = h;
+                                sp[img + o] = f2h(v - h2f(h));
+                            }
+            } else {
+                // conv_stream.hip (S16): slice = chunk * KS^2 + tap over 16-channel chunks; row n = [Bh(16) | Bl(16)]
+                const int nsteps = (L.cin / 16) * ntap;
+                sp.assign((size_t)nsteps * L.cout * 32, 0);
+                for (int st = 0; st < nsteps; ++st)
+                    for (int n = 0; n < L.cout; ++n)
+                        for (int kk = 0; kk < 16; ++kk) {
+                            const int tap = st % ntap, c = (st / ntap) * 16 + kk;
+                            const float v = wsc(n, kernel[((size_t)tap * L.cin + c) * L.cout + n]);
+                            const uint16_t h = f2h(v);
+                            sp[((size_t)st * L.cout + n) * 32 + kk] = h;
+                            sp[((size_t)st * L.cout + n) * 32 + 16 + kk] = f2h(v - h2f(h));
+                        }
+            }
+            if ((rc = upload(W, scale_h, &G.scale_h))) return rc;
+            uint16_t* d;
+            if ((rc = upload(W, sp, &d))) return rc;
+            G.w_halo = d;
+            return 0;
+        }
         if ((rc = upload(W, scale_h, &G.scale_h))) return rc;
         std::vector<uint16_t> hp;
         if (G.halo == HALO_V1) {
@@ -855,15 +930,25 @@ int avse_ctx_get_option(avse_ctx* c, const char* name, int* value) {
 }
 
 int avse_ctx_reserve(avse_ctx* c, int64_t max_clips, int dtype) {
-    if (!c || max_clips < 0 || (dtype != AVSE_F32 && dtype != AVSE_BF16)) return fail(AVSE_ERR_INVALID, "bad reserve args");
+    if (!c || max_clips < 0 || !valid_dtype(dtype)) return fail(AVSE_ERR_INVALID, "bad reserve args");
     AVSE_HIP_CHECK(hipSetDevice(c->device));
-    return ensure_arena(c, max_clips, dtype, kPlan25);   // the 25-fps network's scratch (other shapes grow it on use)
+    return ensure_arena(c, max_clips, dtype, kPlan25, nullptr);   // the 25-fps network's scratch
+}
+
+int avse_ctx_reserve_weights(avse_ctx* c, const avse_weights* w, int64_t max_clips) {
+    if (!c || !w || max_clips < 0) return fail(AVSE_ERR_INVALID, "bad reserve args");
+    if (w->device != c->device) return fail(AVSE_ERR_INVALID, "weights and context are on different devices");
+    AVSE_HIP_CHECK(hipSetDevice(c->device));
+    return ensure_arena(c, max_clips, w->dtype, w->plan, nullptr);   // the network shape these weights were built for
 }
 
 namespace avse {
 // checked build: wait for the stream, then report the first device-side check that fired (avse_common.h DebugHit)
 int debug_poll(void* stream) {
     if constexpr (!kDebugBuild) return 0;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    AVSE_HIP_CHECK(hipStreamIsCapturing((hipStream_t)stream, &cs));
+    if (cs != hipStreamCaptureStatusNone) return 0;   // no synchronisation inside a capture: checked on a later call
     AVSE_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
     static const struct {
         int (*read)(DebugHit*);
@@ -1000,7 +1085,7 @@ int avse_weights_shape(const avse_weights* w, int* spec_frames, int* video_frame
 int avse_weights_load_shape(avse_ctx* c, const float* blob, int64_t n_floats, int dtype, int spec_frames,
                             int video_frames, avse_weights** out) {
     if (!c || !blob || !out) return fail(AVSE_ERR_INVALID, "NULL argument");
-    if (dtype != AVSE_F32 && dtype != AVSE_BF16) return fail(AVSE_ERR_INVALID, "bad compute dtype");
+    if (!valid_dtype(dtype)) return fail(AVSE_ERR_INVALID, "bad compute dtype");
     if (!plan_valid(spec_frames, video_frames))
         return fail(AVSE_ERR_UNSUPPORTED, "network shape [80, " + std::to_string(spec_frames) + "] x [128, 128, " +
                                               std::to_string(video_frames) + "]: the decoder reproduces 80 x T only for "
@@ -1038,6 +1123,15 @@ int avse_weights_load_shape(avse_ctx* c, const float* blob, int64_t n_floats, in
         int rc = build_layer(W, i, kernel, bias, bn, c->opt);
         if (rc) { delete W; return rc; }
     }
+    if (dtype == AVSE_F32_SPLIT) {
+        // the split layers pass split-pair activations to each other: they must be a prefix v_conv1 .. of the video
+        // encoder (a 6-frame v_conv1 runs generic: then every video layer does)
+        bool prefix = true;
+        for (int i = 5; i < 11; ++i) {
+            if (W->layers[i].halo == HALO_NONE) prefix = false;
+            if (!prefix) W->layers[i].halo = HALO_NONE;
+        }
+    }
     *out = W;
     return 0;
 }
@@ -1062,10 +1156,12 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
     if (W->device != c->device) return fail(AVSE_ERR_INVALID, "weights and context are on different devices");
     AVSE_HIP_CHECK(hipSetDevice(c->device));
     const NetPlan& P = W->plan;
-    int rc = ensure_arena(c, N, W->dtype, P);
+    int rc = ensure_arena(c, N, W->dtype, P, s);
     if (rc) return rc;
     c->last_plan = P;
     const int dt = W->dtype;
+    const bool split = dt == AVSE_F32_SPLIT;               // video convs on split-f16 operands, the rest fp32
+    const int gdt = dt == AVSE_BF16 ? AVSE_BF16 : AVSE_F32;   // dtype of the generic kernels' buffers
     size_t off[B_COUNT + 1];
     arena_bytes(N, dt, c->opt, off, P);
     const long long CAT = P.cat, AEMB = P.aemb, EMB = P.emb;
@@ -1094,7 +1190,7 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
         g.counters = c->gemm_counters;
         return launch_gemm(g, mode, s);
     };
-    auto split = [&](ConvArgs& a) {   // dense layers / v_conv6: split-K when the grid is small
+    auto ksplit = [&](ConvArgs& a) {   // dense layers / v_conv6: split-K when the grid is small
         if (a.nphase != 1) return;
         const int64_t M = (int64_t)a.N * a.Hq * a.Wq;
         a.ksplit = choose_ksplit(M, a.Co, a.ph[0].kpad, dt);
@@ -1114,13 +1210,25 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
                              void* cat) -> int {
         auto vb = [&](int b) { return (void*)(c->arena + o[b]); };
         const int v_in[6] = {B_VIN, B_V1, B_V2, B_V3, B_V4, B_V5};
-        if (L(5).halo == HALO_NONE && (rc = launch_video_prep(vid, vm, vs, vb(B_VIN), n, P.F, dt, s))) return rc;
+        if (L(5).halo == HALO_NONE && (rc = launch_video_prep(vid, vm, vs, vb(B_VIN), n, P.F, gdt, s))) return rc;
         for (int i = 0; i < 6; ++i) {
             const GpuLayer& G = L(5 + i);
             if (G.halo != HALO_NONE) {
                 HaloArgs h = (i < 5) ? halo_args(G, vb(v_in[i]), vid, vm, vs, vb(v_in[i + 1]),
                                                  (long long)G.ho * G.wo * G.def.cout, G.def.cout, 0, n, opt)
                                      : halo_args(G, vb(v_in[i]), vid, vm, vs, cat, CAT, G.def.cout, AEMB, n, opt);
+                if (split) {
+                    // split-pair input (2 halves per channel) from the previous split layer; output split pairs for
+                    // a next split layer, fp32 for a generic one (weights_load keeps the split layers a prefix)
+                    h.split = 1;
+                    if (G.halo != HALO_V1) h.Ci = 2 * G.def.cin;
+                    const bool next_split = i < 5 && L(6 + i).halo != HALO_NONE;
+                    h.out_mode = next_split ? OUT_S16 : OUT_F32;
+                    if (next_split) {
+                        h.out_clip_stride *= 2;
+                        h.out_pix_stride *= 2;
+                    }
+                }
                 rc = G.halo == HALO_V1 ? launch_conv_v1r(h, s) : launch_conv_stream(h, s);
                 if (rc || (rc = mark())) return rc;
                 continue;
@@ -1133,8 +1241,8 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
             }
             ConvArgs a = (i < 5) ? conv_args(G, vb(v_in[i]), in_cs, vb(v_in[i + 1]), (long long)G.ho * G.wo * G.def.cout, G.def.cout, 0, n)
                                  : conv_args(G, vb(v_in[i]), in_cs, cat, CAT, G.def.cout, AEMB, n);  // concat[aemb:]
-            if (i == 5) split(a);
-            if ((rc = launch_conv(a, dt, s)) || (rc = mark())) return rc;
+            if (i == 5) ksplit(a);
+            if ((rc = launch_conv(a, gdt, s)) || (rc = mark())) return rc;
         }
         return 0;
     };
@@ -1220,14 +1328,14 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
         for (int k = 0; k < 6; ++k)
             if ((rc = mark())) return rc;   // audio_prep (= the fused kernel), a_conv1..a_conv5
     }
-    if (!aud_fused && ((rc = launch_audio_prep(audio, buf(B_AIN), N * kMels * P.T, dt, sa)) || (rc = mark()))) return rc;
+    if (!aud_fused && ((rc = launch_audio_prep(audio, buf(B_AIN), N * kMels * P.T, gdt, sa)) || (rc = mark()))) return rc;
     const int a_in[5] = {B_AIN, B_A1, B_A2, B_A3, B_A4};
     for (int i = 0; i < 5 && !aud_fused; ++i) {
         const GpuLayer& G = L(i);
         const long long in_cs = (long long)G.def.hin * G.def.win * (i == 0 ? G.cin_pad : G.def.cin);
         ConvArgs a = (i < 4) ? conv_args(G, buf(a_in[i]), in_cs, buf(a_in[i + 1]), (long long)G.ho * G.wo * G.def.cout, G.def.cout, 0, N)
                              : conv_args(G, buf(a_in[i]), in_cs, buf(B_CAT), CAT, G.def.cout, 0, N);   // Flatten -> concat[0:aemb]
-        if ((rc = launch_conv(a, dt, sa)) || (rc = mark())) return rc;
+        if ((rc = launch_conv(a, gdt, sa)) || (rc = mark())) return rc;
     }
     if (concurrent) AVSE_HIP_CHECK(hipEventRecord(c->join, sa));
     if (video) {
@@ -1247,14 +1355,14 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
         if ((rc = gemm(L(13), buf(B_E2), EMB, buf(B_E3), AEMB, 0, 0, N)) || (rc = mark())) return rc;
     } else {
         ConvArgs a = conv_args(L(11), buf(B_CAT), CAT, buf(B_E1), EMB, EMB, 0, N);
-        split(a);
-        if ((rc = launch_conv(a, dt, s)) || (rc = mark())) return rc;
+        ksplit(a);
+        if ((rc = launch_conv(a, gdt, s)) || (rc = mark())) return rc;
         a = conv_args(L(12), buf(B_E1), EMB, buf(B_E2), EMB, EMB, 0, N);
-        split(a);
-        if ((rc = launch_conv(a, dt, s)) || (rc = mark())) return rc;
+        ksplit(a);
+        if ((rc = launch_conv(a, gdt, s)) || (rc = mark())) return rc;
         a = conv_args(L(13), buf(B_E2), EMB, buf(B_E3), AEMB, AEMB, 0, N);
-        split(a);
-        if ((rc = launch_conv(a, dt, s)) || (rc = mark())) return rc;
+        ksplit(a);
+        if ((rc = launch_conv(a, gdt, s)) || (rc = mark())) return rc;
     }
     // audio decoder (network.py:112-135)
     const int d_in[6] = {B_E3, B_D1, B_D2, B_D3, B_D4, B_D5};
@@ -1309,14 +1417,14 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
             a.fuse_w = W->d6_w;
             a.fuse_bias = W->d6_bias;
             a.fuse_out = out;
-            if ((rc = launch_conv(a, dt, s)) || (rc = mark())) return rc;
+            if ((rc = launch_conv(a, gdt, s)) || (rc = mark())) return rc;
             continue;
         }
         ConvArgs a = conv_args(G, buf(d_in[i]), in_cs, buf(d_in[i + 1]), (long long)G.ho * G.wo * G.def.cout, G.def.cout, 0, N);
-        if ((rc = launch_conv(a, dt, s)) || (rc = mark())) return rc;
+        if ((rc = launch_conv(a, gdt, s)) || (rc = mark())) return rc;
     }
     if (opt.unfused_tail) {
-        if ((rc = launch_out_conv(buf(B_D5), W->d6_w, W->d6_bias, out, N * kMels * P.T, dt, s)) || (rc = mark())) return rc;
+        if ((rc = launch_out_conv(buf(B_D5), W->d6_w, W->d6_bias, out, N * kMels * P.T, gdt, s)) || (rc = mark())) return rc;
     } else if ((rc = mark())) {   // d_deconv6: fused into d_deconv5 above
         return rc;
     }
@@ -1348,7 +1456,7 @@ static int forward_dispatch(avse_ctx* c, const avse_weights* W, const float* aud
         return forward_impl(c, W, audio, video, vmean, vstd, N, out, (hipStream_t)stream, nullptr);
     AVSE_HIP_CHECK(hipSetDevice(c->device));
     if (W->device != c->device) return fail(AVSE_ERR_INVALID, "weights and context are on different devices");
-    int rc = ensure_arena(c, N, W->dtype, W->plan);   // no allocation inside the capture
+    int rc = ensure_arena(c, N, W->dtype, W->plan, (hipStream_t)stream);   // no allocation inside the capture
     if (rc) return rc;
     const void* key[8] = {(const void*)W->serial, audio, video, vmean, vstd, out, c->arena, (const void*)c->arena_bytes};
     avse_ctx::Graph* hit = nullptr;

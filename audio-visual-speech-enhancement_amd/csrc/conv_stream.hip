@@ -80,7 +80,7 @@ __device__ __forceinline__ void barrier_raw() { asm volatile("s_barrier" ::: "me
 // LAT (load -> LDS store distance, steps): 10 for 5x5, 6 for 3x3; it divides the unrolled chunk pair
 // (2 KS^2 steps).  Measured on v_conv2 (runtime-tap loader): LAT 4 / 5 / 10 / 20 = 1.14 / 1.04-1.13 / 1.00 /
 // 1.27 ms (20 spills).
-template <int KS, int TH, int TW, int NCLIP, int LAT_ = (KS == 5 ? 10 : 6), int BP_ = 1>
+template <int KS, int TH, int TW, int NCLIP, int LAT_ = (KS == 5 ? 10 : 6), int BP_ = 1, bool S16_ = false>
 struct StreamGeom {
     static constexpr int HH = TH + KS - 1, HW = TW + KS - 1;
     static constexpr int HPIX = NCLIP * HH * HW;              // halo pixels per chunk
@@ -93,8 +93,11 @@ struct StreamGeom {
     // during step j (loaded WD = LAT + BP + 1 steps ahead) into a ring of NWS = 2 BP weight slots: the slot
     // it overwrites held slice j + 1 - BP, whose fragments the compute waves read during step j - BP, before
     // the previous barrier; 3 halo chunk slots
-    static constexpr int LAT = LAT_, BP = BP_, NWS = 2 * BP, WD = LAT + BP + 1, NHS = 3, PAIR = 2 * NTAP;
+    // S16 (split-f16 operands): the compute waves read slice t's lo weights during step t as well, so the ring
+    // has a third slot (the loader's slot (j + 2) % 3 was last read during step j - 1)
+    static constexpr int LAT = LAT_, BP = BP_, NWS = S16_ ? 3 : 2 * BP, WD = LAT + BP + 1, NHS = 3, PAIR = 2 * NTAP;
     static_assert(BP == 1 || BP == 2, "barrier period");
+    static_assert(!S16_ || BP == 1, "split-f16 operands: one step per barrier");
     static constexpr int LDS = NHS * CSLOT + NWS * WSLOT;
     static_assert(LDS + 1024 <= 160 * 1024, "LDS");   // one workgroup per CU: ~250 VGPRs x 8 waves fill the register file
     static_assert(NCLIP * TH * TW == 256, "tile = 256 conv pixels (4 waves x 4 fragments)");
@@ -121,10 +124,20 @@ struct StreamGeom {
 // loop, 2 = no weight streaming in the loop, 4 = no barrier/wait, 8 = no fragment reads, 16 = no MFMAs,
 // 64 = every tile reads clip 0's window (L2-resident input), 128 = s_memtime per step: cycles working /
 // waiting (vmcnt, lgkmcnt) / in the barrier, per wave, into a.prof[(block * 8 + wave) * 4 + {0,1,2, 3=steps}]
+//
+// S16: fp32-accurate split-f16 operands (DESIGN.md §3 "split-f16").  Every fp32 value x is carried as the f16 pair
+// (h, l) = (f16(x), f16(x - h)); the input activation holds, per pixel and per 16 channels, 32 f16 = [h(16) | l(16)]
+// (a "chunk" of 32 halves is then 16 real channels), the weight row of output channel co per slice 32 f16 =
+// [Bh(16) | Bl(16)] of the same 16 channels (scaled by a per-channel power of two folded into the BN scale).  A step
+// issues two groups of 32 v_mfma_f32_16x16x32_f16: lanes of k-groups 0, 1 hold Ah, of 2, 3 Al; the B fragment of
+// group 1 reads the Bh half for every lane (k-group kg & 1), of group 2 the Bl half (2 + (kg & 1)), so the two
+// groups sum Ah Bh + Al Bh and Ah Bl + Al Bl: all four products of (Ah + Al)(Bh + Bl), each 32-product MFMA rounded
+// once into the fp32 accumulator (tools/split_probe.hip: more accurate than exact-fp32 MFMA at K = 3200).
 template <int KS, int TH, int TW, int NCLIP, bool M16 = true, int LAT_ = StreamGeom<KS, TH, TW, NCLIP>::LAT, int ABL = 0,
-          int BP_ = 1>
+          int BP_ = 1, bool S16 = false>
 __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
-    using G = StreamGeom<KS, TH, TW, NCLIP, LAT_, BP_>;
+    static_assert(!S16 || M16, "split-f16 operands: 16x16x32 compute waves only");
+    using G = StreamGeom<KS, TH, TW, NCLIP, LAT_, BP_, S16>;
     constexpr int HH = G::HH, HW = G::HW, HPIX = G::HPIX, HPW = G::HPW, NTAP = G::NTAP;
     constexpr int CSLOT = G::CSLOT, WSLOT = G::WSLOT, LAT = G::LAT, WD = G::WD, PAIR = G::PAIR;
     constexpr int BP = G::BP, NWS = G::NWS;
@@ -292,7 +305,9 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
             // 1. LDS stores of set S: weights of slice j+BP+1 (slot (j+BP+1) % NWS) and the piece loaded
             //    with them
             if constexpr (!(ABL & 2)) {
-                char* const wd = wdst + (((j + BP + 1) + (kRot ? wrot : 0)) & (NWS - 1)) * WSLOT;
+                int wsl = (j + BP + 1) % NWS + (kRot ? wrot : 0);
+                if (wsl >= NWS) wsl -= NWS;
+                char* const wd = wdst + wsl * WSLOT;
                 st16(wd, rw[S][0]);
                 st16(wd + 1024, rw[S][1]);
             }
@@ -327,7 +342,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
             [&]<int... J>(std::integer_sequence<int, J...>) {
                 (lstep(std::integral_constant<int, J>{}), ...);
             }(std::make_integer_sequence<int, PAIR>{});
-            if constexpr (kRot) wrot = (wrot + PAIR) & (NWS - 1);
+            if constexpr (kRot) wrot = (wrot + PAIR) % NWS;
         }
         wait_vm_lgkm0<0>();   // loads still in flight target registers and rows nobody reads
         if constexpr ((ABL & 128) != 0)
@@ -339,6 +354,15 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
     }
 
     // =============================== compute waves ===============================
+    // S16 read spacing (MFMAs per fragment read): group 1's 8 Bl reads, group 2's 12 next-slice reads
+#ifndef AVSE_S16_SG1
+#define AVSE_S16_SG1 4
+#endif
+#ifndef AVSE_S16_SG2
+#define AVSE_S16_SG2 2
+#endif
+    constexpr int SG1 = AVSE_S16_SG1, SG2 = AVSE_S16_SG2;
+    static_assert(8 * SG1 <= 32 && 12 * SG2 <= 32, "read spacing");
     // the MFMA stream gets issue priority over the co-resident loader wave of its SIMD (-2% time)
     __builtin_amdgcn_s_setprio(2);
     if constexpr (M16) {
@@ -357,7 +381,15 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
         const int ab = ((cl0 * HH + 4 * by0 + 2 * (q >> 1) + dy) * HW + 4 * bx0 + 2 * (q & 1) + dx) * 64;
         // block i of the wave relative to block 0 (bx0 % SBX == 0 or SBX == 2 with bx0 == 0)
         auto boff_of = [](int i) { return ((i / SBX) * 4 * HW + (i % SBX) * 4) * 64; };
-        const int bo16 = r16 * 64 + ((kg ^ wswz<true>(r16)) << 4);   // + 1024 j for column block j
+        // + 1024 j for column block j.  S16: bo16 reads the Bh half of the row for every lane (k-group kg & 1), bo16l
+        // the Bl half (2 + (kg & 1)); the per-16-lane address pattern is the bf16 one (same conflict-free image)
+        const int bo16 = r16 * 64 + (((S16 ? (kg & 1) : kg) ^ wswz<true>(r16)) << 4);
+        const int bo16l = r16 * 64 + (((2 + (kg & 1)) ^ wswz<true>(r16)) << 4);
+        auto frags_lo = [&](int ws, i32x4 (&fb)[8]) {
+            const char* wp = wring + ws * WSLOT + bo16l;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) fb[j] = *reinterpret_cast<const i32x4*>(wp + 1024 * j);
+        };
         auto frags = [&](int hs, int tap, int ws, i32x4 (&fa)[4], i32x4 (&fb)[8]) {
             const int ky = tap / KS, kx = tap % KS;
             const int pos = (kg ^ hsw<true>(dy + ky)) << 4;
@@ -386,11 +418,16 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) acc[i][j] = (f32x4){};
         const int Wp = a.Wc / 2;
-        auto epilogue = [&](int clip0, int oy0, int ox0) {
-            const long long cbytes = a.out_clip_stride * 2;
+        // output element (pooled pixel p, channel co): OUT_BF16 / OUT_F32 at p * out_pix_stride + out_c_off + co;
+        // OUT_S16 (the next stream layer's split input, out_pix_stride = 2 Co) h at p * out_pix_stride + out_c_off +
+        // 32 (co / 16) + co % 16 and l 16 halves further
+        auto epilogue_m = [&](auto modec, int clip0, int oy0, int ox0) {
+            constexpr int OM = decltype(modec)::value;
+            constexpr int ES = OM == OUT_F32 ? 4 : 2;
+            const long long cbytes = a.out_clip_stride * ES;
             const __amdgpu_buffer_rsrc_t ors = make_rsrc(reinterpret_cast<const char*>(a.out) + (long long)clip0 * cbytes,
                                                          (long long)(a.N - clip0) * cbytes);
-            const int cbase = cl0 * (int)a.out_clip_stride + a.out_c_off + co0 + r16;
+            const int cbase = cl0 * (int)a.out_clip_stride + a.out_c_off + (OM == OUT_S16 ? 2 * co0 : co0) + r16;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int py = (oy0 + 4 * (by0 + i / SBX)) / 2 + (kg >> 1);
@@ -401,12 +438,32 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
                     const float mx = fmaxf(fmaxf(acc[i][j][0], acc[i][j][1]), fmaxf(acc[i][j][2], acc[i][j][3]));
                     float x = fmaf(mx, ssh[16 * j + r16], ssh[128 + 16 * j + r16]);
                     x = fmaxf(x, LRELU * x);
-                    __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (bf16_t)x), ors,
-                                                          (pbase + 16 * j) * 2, 0, 0);
+                    if constexpr (OM == OUT_BF16) {
+                        __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (bf16_t)x), ors,
+                                                              (pbase + 16 * j) * 2, 0, 0);
+                    } else if constexpr (OM == OUT_S16) {
+                        const _Float16 h = (_Float16)x;
+                        const _Float16 l = (_Float16)(x - (float)h);
+                        __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, h), ors,
+                                                              (pbase + 32 * j) * 2, 0, 0);
+                        __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, l), ors,
+                                                              (pbase + 32 * j + 16) * 2, 0, 0);
+                    } else {
+                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, x), ors, (pbase + 16 * j) * 4, 0, 0);
+                    }
                     // restart the chain in place: x * 0 (not a constant, which the register allocator would
                     // materialise elsewhere and then shuffle — that spilled the 256-register budget)
                     acc[i][j] *= 0.f;
                 }
+            }
+        };
+        auto epilogue = [&](int clip0, int oy0, int ox0) {
+            if constexpr (!S16) {
+                epilogue_m(std::integral_constant<int, OUT_BF16>{}, clip0, oy0, ox0);
+            } else if (a.out_mode == OUT_S16) {
+                epilogue_m(std::integral_constant<int, OUT_S16>{}, clip0, oy0, ox0);
+            } else {
+                epilogue_m(std::integral_constant<int, OUT_F32>{}, clip0, oy0, ox0);
             }
         };
 
@@ -421,26 +478,66 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
 
         // bar: the step closes a BP-step group (t % BP == BP - 1; t is even on the first call of each pair)
         auto cstep = [&](auto bar, int t, i32x4 (&ca)[4], i32x4 (&cb)[8], i32x4 (&xa)[4], i32x4 (&xb)[8]) {
-            if constexpr (!(ABL & 8)) frags(hs1, tap1, (t + 1) & (NWS - 1), xa, xb);
-            if constexpr (!(ABL & 16))
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
+            if constexpr (S16) {
+                // column-block-outer MFMA order: B fragment j is dead after its 4 MFMAs, so the fragment read
+                // issued behind them can take its registers (the step holds ~24 live fragments, as bf16 does)
+                // group 1: Ah Bh + Al Bh, while this slice's Bl fragments (weight slot t % 3) are read
+                i32x4 cl[8];
+                if constexpr (!(ABL & 8)) frags_lo(t % NWS, cl);
+                if constexpr (!(ABL & 16))
 #pragma unroll
                     for (int j = 0; j < 8; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                            __builtin_bit_cast(bf16x8, ca[i]), __builtin_bit_cast(bf16x8, cb[j]), acc[i][j], 0, 0, 0);
+#pragma unroll
+                        for (int i = 0; i < 4; ++i)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
+                                __builtin_bit_cast(f16x8, ca[i]), __builtin_bit_cast(f16x8, cb[j]), acc[i][j], 0, 0, 0);
+#pragma unroll
+                for (int r = 0; r < 8; ++r) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, SG1, 0);   // MFMA
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);     // DS read
+                }
+                __builtin_amdgcn_sched_group_barrier(0x008, 32 - 8 * SG1, 0);
+                __builtin_amdgcn_sched_barrier(0);
+                // group 2: Ah Bl + Al Bl, while the next slice's A and Bh fragments are read
+                if constexpr (!(ABL & 8)) frags(hs1, tap1, (t + 1) % NWS, xa, xb);
+                if constexpr (!(ABL & 16))
+#pragma unroll
+                    for (int j = 0; j < 8; ++j)
+#pragma unroll
+                        for (int i = 0; i < 4; ++i)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
+                                __builtin_bit_cast(f16x8, ca[i]), __builtin_bit_cast(f16x8, cl[j]), acc[i][j], 0, 0, 0);
+#pragma unroll
+                for (int r = 0; r < 12; ++r) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, SG2, 0);   // MFMA
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);     // DS read
+                }
+                __builtin_amdgcn_sched_group_barrier(0x008, 32 - 12 * SG2, 0);
+                __builtin_amdgcn_sched_barrier(0);
+            } else {
+                if constexpr (!(ABL & 8)) frags(hs1, tap1, (t + 1) & (NWS - 1), xa, xb);
+                if constexpr (!(ABL & 16))
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+#pragma unroll
+                        for (int j = 0; j < 8; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                                __builtin_bit_cast(bf16x8, ca[i]), __builtin_bit_cast(bf16x8, cb[j]), acc[i][j], 0, 0, 0);
+            }
             // the next slice's 12 fragment reads one per MFMA from the start of the step (measured against two
             // MFMAs per read over 24 MFMAs, 3:2, 1:2 and all reads first: -1 to -2 % on v_conv2 / v_conv4, the
             // bunched forms +2 to +17 %).  A 3-slot weight ring that lets the compute waves skip the lgkmcnt(0)
             // drain before each barrier was slower (+2-4 %): the drain overlaps the barrier wait, the deferred
             // wait stalls the next step's first MFMAs
+            if constexpr (!S16) {
 #pragma unroll
-            for (int r = 0; r < 12; ++r) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
-                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
+                for (int r = 0; r < 12; ++r) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
+                }
+                __builtin_amdgcn_sched_group_barrier(0x008, 20, 0);
+                __builtin_amdgcn_sched_barrier(0);
             }
-            __builtin_amdgcn_sched_group_barrier(0x008, 20, 0);
-            __builtin_amdgcn_sched_barrier(0);
             if constexpr (!(ABL & 4) && decltype(bar)::value) {
                 if constexpr ((ABL & 128) != 0) pt0 = __builtin_amdgcn_s_memtime();
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -625,10 +722,11 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
         }
 }
 
-template <int KS, int TH, int TW, int NCLIP, bool M16>
+template <int KS, int TH, int TW, int NCLIP, bool M16, bool S16 = false>
 int launch_stream(const HaloArgs& a, hipStream_t s) {
-    using G = StreamGeom<KS, TH, TW, NCLIP>;
-    if (int rc = ensure_lds_attr((const void*)k_conv_stream<KS, TH, TW, NCLIP, M16>, G::LDS + 1024)) return rc;
+    using G = StreamGeom<KS, TH, TW, NCLIP, StreamGeom<KS, TH, TW, NCLIP>::LAT, 1, S16>;
+    constexpr auto kern = k_conv_stream<KS, TH, TW, NCLIP, M16, G::LAT, 0, 1, S16>;
+    if (int rc = ensure_lds_attr((const void*)kern, G::LDS + 1024)) return rc;
     if (a.Hc % TH || a.Wc % TW || a.Co % 128 || a.Ci % 64) {   // an even number of 32-channel chunks
         set_error("stream conv: tile does not divide the layer");
         return 3;
@@ -642,7 +740,11 @@ int launch_stream(const HaloArgs& a, hipStream_t s) {
     int gx = ncu / cob;
     gx = gx >= 8 ? gx / 8 * 8 : (gx < 1 ? 1 : gx);
     if (gx > tiles) gx = tiles;
-    hipLaunchKernelGGL((k_conv_stream<KS, TH, TW, NCLIP, M16>), dim3(gx, cob), dim3(512), G::LDS + 1024, s, a);
+    if (S16 && a.out_mode != OUT_S16 && a.out_mode != OUT_F32) {
+        set_error("stream conv: split-f16 operands write split or f32 outputs");
+        return 3;
+    }
+    hipLaunchKernelGGL(kern, dim3(gx, cob), dim3(512), G::LDS + 1024, s, a);
     AVSE_HIP_CHECK(hipGetLastError());
     return 0;
 }
@@ -651,6 +753,15 @@ int launch_stream(const HaloArgs& a, hipStream_t s) {
 
 int launch_conv_stream(const HaloArgs& a, hipStream_t s) {
     const bool m32 = a.mfma32 != 0;   // v_mfma_f32_32x32x16_bf16 compute waves (A/B variant, Options::mfma32)
+    if (a.split) {   // split-f16 operands (a.Ci counts halves: 2 x the layer's channels)
+        switch (a.variant) {
+            case HALO_K5: return launch_stream<5, 16, 16, 1, true, true>(a, s);
+            case HALO_K3_16: return launch_stream<3, 16, 16, 1, true, true>(a, s);
+            case HALO_K3_8: return launch_stream<3, 8, 8, 4, true, true>(a, s);
+        }
+        set_error("stream conv: unsupported variant");
+        return 3;
+    }
     switch (a.variant) {
         case HALO_K5: return m32 ? launch_stream<5, 16, 16, 1, false>(a, s) : launch_stream<5, 16, 16, 1, true>(a, s);
         case HALO_K3_16: return m32 ? launch_stream<3, 16, 16, 1, false>(a, s) : launch_stream<3, 16, 16, 1, true>(a, s);

@@ -334,9 +334,278 @@ __global__ __launch_bounds__(512, 1) void k_conv_v1r(HaloArgs a) {
     }
 }
 
+// ------------------------------------------------------------------------------------------------------------
+// k_conv_v1s: v_conv1 with split-f16 operands (AVSE_F32_SPLIT, DESIGN.md §3 "split-f16"), the same row-run K
+// layout.  The normalised window is stored twice — h = f16(x) and l = f16(x - h), 12-byte pixels each — and the
+// weights as Bh / Bl images [piece][kernel row][Co][32] f16 (80 KB, resident; scaled by a per-channel power of two
+// that the BN scale undoes).  A K-slice is four groups of 32 v_mfma_f32_16x16x32_f16 (Ah Bh, Ah Bl, Al Bl, Al Bh: all
+// four products, each MFMA rounding its 32 products once into fp32), ordered so that at most 24 fragments are live:
+//   Ah Bh (reading Bl) -> Ah Bl (reading Al) -> Al Bl (reading the next slice's Ah) -> Al Bh (reading its Bh).
+// With four times the MFMAs per window the compute waves run the epilogue themselves (BN + LeakyReLU on the pooled
+// maxima, split, stores into the next layer's split-pair layout: per pixel and 16 channels [h(16) | l(16)]); the
+// loader waves only stage windows.  Window / barrier protocol as k_conv_v1r (3 slots, window k+2 stored while
+// tile k computes).
+constexpr int HIMG = HSLOT;                                    // one window image (h or l)
+constexpr int SSLOT = 2 * HIMG;                                // window slot: h image, l image
+constexpr int WIMG_S = 2 * NSL * 128 * 64;                     // Bh, Bl: 80 KB
+constexpr int LDS_S = WIMG_S + NWS * SSLOT + SSH;
+static_assert(LDS_S <= 160 * 1024, "LDS (split v_conv1)");
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+
+__global__ __launch_bounds__(512, 1) void k_conv_v1s(HaloArgs a) {
+    extern __shared__ __attribute__((aligned(1024))) char lds[];
+    char* const wimg = lds;                          // [2 pieces][5 rows][128 co][64 B]
+    char* const halo = lds + WIMG_S;                 // [NWS][h image | l image]
+    float* const ssh = reinterpret_cast<float*>(halo + NWS * SSLOT);
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int w = wave & 3;
+
+    const int tiles_x = a.Wc / TW, tiles_per_clip = tiles_x * (a.Hc / TH);
+    const int ntiles = a.N * tiles_per_clip;
+    const int gxs = (int)gridDim.x;
+    const int slot = (gxs % 8 == 0) ? ((int)blockIdx.x % 8) * (gxs / 8) + (int)blockIdx.x / 8 : (int)blockIdx.x;
+    const int nmine = (ntiles - slot + gxs - 1) / gxs;
+    if (nmine <= 0) return;
+    auto tile_origin = [&](int k, int& clip, int& oy0, int& ox0) {
+        const int t = slot + k * gxs;
+        clip = t / tiles_per_clip;
+        const int tt = t - clip * tiles_per_clip;
+        oy0 = (tt / tiles_x) * TH;
+        ox0 = (tt % tiles_x) * TW;
+    };
+
+    if (wave >= 4) {
+        // =============================== loader waves ===============================
+        const int L = w * 64 + lane;
+        {
+            const __amdgpu_buffer_rsrc_t wrs = make_rsrc(a.w, (long long)WIMG_S);
+#pragma unroll
+            for (int i = 0; i < WIMG_S / 16 / 256; ++i) {
+                const int C = L + 256 * i, row = C >> 2, sl = C & 3;
+                const i32x4 v = __builtin_amdgcn_raw_buffer_load_b128(wrs, C * 16, 0, 0);
+                *reinterpret_cast<i32x4*>(wimg + row * 64 + ((sl ^ wsw(row & 127)) << 4)) = v;
+            }
+            if (L < 128) {
+                ssh[L] = a.scale[L];
+                ssh[128 + L] = a.shift[L];
+            }
+            for (int i = L; i < NWS * SSLOT / 4; i += 256) {   // pitch padding and tails of every image
+                const int off = (i * 4) % HIMG;
+                if (off >= HH * HWP * PB || (off / PB) % HWP >= HW) reinterpret_cast<int*>(halo)[i] = 0;
+            }
+        }
+        const long long clip_bytes = (long long)a.Hc * a.Wc * NF * 4;
+        const bool norm = a.vmean != nullptr;
+        const __amdgpu_buffer_rsrc_t mrs = make_rsrc(norm ? a.vmean : a.video, (long long)a.Hc * a.Wc * 4);
+        const __amdgpu_buffer_rsrc_t srs = make_rsrc(norm ? a.vstd : a.video, (long long)a.Hc * a.Wc * 4);
+        f32x4 v4[2][PPL];
+        float v1[2][PPL], pm[2][PPL], ps[2][PPL];
+        int pok[2][PPL];
+        auto win_load = [&](auto set, int k) {
+            constexpr int Q = decltype(set)::value;
+            int clip, oy0, ox0;
+            tile_origin(k, clip, oy0, ox0);
+            const __amdgpu_buffer_rsrc_t vrs =
+                make_rsrc(reinterpret_cast<const char*>(a.video) + (long long)clip * clip_bytes, clip_bytes);
+#pragma unroll
+            for (int e = 0; e < PPL; ++e) {
+                const int P = L + 256 * e;
+                const int wy = P / HW, wx = P - wy * HW;
+                const int iy = oy0 + wy - PAD, ix = ox0 + wx - PAD;
+                const int ok = (int)(P < HPIX) & (int)((unsigned)iy < (unsigned)a.Hc) & (int)((unsigned)ix < (unsigned)a.Wc);
+                const int pix = iy * a.Wc + ix;
+                const int voff = ok ? pix * NF * 4 : kOOB, moff = ok ? pix * 4 : kOOB;
+                v4[Q][e] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(vrs, voff, 0, 0));
+                v1[Q][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(vrs, voff, 16, 0));
+                pm[Q][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(mrs, moff, 0, 0));
+                ps[Q][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(srs, moff, 0, 0));
+                pok[Q][e] = ok;
+            }
+        };
+        // VideoNormalizer ((v - mean) / std: an IEEE division, the reference's numpy op), 'same' zero padding, split
+        auto win_store = [&](auto set, int hs) {
+            constexpr int Q = decltype(set)::value;
+#pragma unroll
+            for (int e = 0; e < PPL; ++e) {
+                const int P = L + 256 * e;
+                if (P >= HPIX) continue;
+                float f[6] = {v4[Q][e][0], v4[Q][e][1], v4[Q][e][2], v4[Q][e][3], v1[Q][e], 0.f};
+#pragma unroll
+                for (int i = 0; i < NF; ++i) {
+                    const float n = norm ? (f[i] - pm[Q][e]) / ps[Q][e] : f[i];
+                    f[i] = pok[Q][e] ? n : 0.f;
+                }
+                _Float16 h[6], l[6];
+#pragma unroll
+                for (int i = 0; i < 6; ++i) {
+                    h[i] = (_Float16)f[i];
+                    l[i] = (_Float16)(f[i] - (float)h[i]);
+                }
+                const int wy = P / HW, wx = P - wy * HW;
+                unsigned* dh = reinterpret_cast<unsigned*>(halo + hs * SSLOT + (wy * HWP + wx) * PB);
+                unsigned* dl = reinterpret_cast<unsigned*>(halo + hs * SSLOT + HIMG + (wy * HWP + wx) * PB);
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    dh[i] = __builtin_bit_cast(unsigned, (f16x2){h[2 * i], h[2 * i + 1]});
+                    dl[i] = __builtin_bit_cast(unsigned, (f16x2){l[2 * i], l[2 * i + 1]});
+                }
+            }
+        };
+        using Q0 = std::integral_constant<int, 0>;
+        using Q1 = std::integral_constant<int, 1>;
+        win_load(Q0{}, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        win_store(Q0{}, 0);
+        if (nmine > 1) {
+            win_load(Q1{}, 1);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            win_store(Q1{}, 1);
+        }
+        if (nmine > 2) win_load(Q0{}, 2);
+        if (nmine > 3) win_load(Q1{}, 3);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        barrier_raw();   // B_-1: weights, BN tail, windows 0 and 1
+        auto iter = [&](auto set, int k) {
+            if (k + 2 < nmine) {
+                win_store(set, (k + 2) % NWS);   // slot of window k-1, last read during tile k-1
+                if (k + 4 < nmine) win_load(set, k + 4);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            barrier_raw();   // B_k: window k+2 stored; window k is no longer read
+        };
+        for (int k = 0; k < nmine; k += 2) {
+            iter(Q0{}, k);
+            if (k + 1 < nmine) iter(Q1{}, k + 1);
+        }
+        return;
+    }
+
+    // =============================== compute waves ===============================
+    __builtin_amdgcn_s_setprio(2);
+    const int r16 = lane & 15, kg = lane >> 4;
+    const int q = r16 >> 2, dy = (r16 >> 1) & 1, dx = r16 & 1;
+    const int abase = ((4 * w + 2 * (q >> 1) + dy) * HWP + 2 * (q & 1) + dx) * PB + 16 * kg;
+    const int bbase = r16 * 64 + ((kg ^ wsw(r16)) << 4);   // + piece * 40960 + slice * 8192 + 1024 j
+    auto fragA = [&](int hs, int piece, int ky, i32x4 (&fa)[4]) {
+        const char* hp = halo + hs * SSLOT + piece * HIMG + abase + ky * HWP * PB;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const unsigned* p = reinterpret_cast<const unsigned*>(hp + 4 * i * PB);
+            fa[i] = (i32x4){(int)p[0], (int)p[1], (int)p[2], (int)p[3]};
+        }
+    };
+    auto fragB = [&](int piece, int ky, i32x4 (&fb)[8]) {
+        const char* wp = wimg + piece * (NSL * 8192) + ky * 8192 + bbase;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) fb[j] = *reinterpret_cast<const i32x4*>(wp + 1024 * j);
+    };
+    barrier_raw();   // B_-1
+
+    f32x4 acc[4][8];
+    auto mfmas = [&](const i32x4 (&ca)[4], const i32x4 (&cb)[8], bool first) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, ca[i]),
+                                                                    __builtin_bit_cast(f16x8, cb[j]),
+                                                                    first ? (f32x4){0.f, 0.f, 0.f, 0.f} : acc[i][j], 0, 0, 0);
+    };
+    auto sched = [](auto nds) {
+        constexpr int ND = decltype(nds)::value;
+#pragma unroll
+        for (int r = 0; r < ND; ++r) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 32 - ND, 0);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    // K-slice ky of window slot hs, with (ah, bh) = its Ah / Bh fragments in registers; reads the next slice's
+    // (hsn, kyn) Ah / Bh into (nah, nbh)
+    auto slice = [&](int hs, int ky, int hsn, int kyn, i32x4 (&ah)[4], i32x4 (&bh)[8], i32x4 (&nah)[4],
+                     i32x4 (&nbh)[8], bool first) {
+        i32x4 bl[8], al[4];
+        fragB(1, ky, bl);
+        mfmas(ah, bh, first);
+        sched(std::integral_constant<int, 8>{});
+        fragA(hs, 1, ky, al);
+        mfmas(ah, bl, false);
+        sched(std::integral_constant<int, 16>{});
+        fragA(hsn, 0, kyn, nah);
+        mfmas(al, bl, false);
+        sched(std::integral_constant<int, 16>{});
+        fragB(0, kyn, nbh);
+        mfmas(al, bh, false);
+        sched(std::integral_constant<int, 8>{});
+    };
+    const int Wp = a.Wc / 2;
+    const long long cbytes = a.out_clip_stride * 2;
+    auto epilogue = [&](int k) {
+        int clip, oy0, ox0;
+        tile_origin(k, clip, oy0, ox0);
+        const __amdgpu_buffer_rsrc_t ors = make_rsrc(reinterpret_cast<const char*>(a.out) + (long long)clip * cbytes, cbytes);
+        const int py = (oy0 >> 1) + 2 * w + (kg >> 1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int px = (ox0 >> 1) + 2 * i + (kg & 1);
+            const int pbase = (py * Wp + px) * a.out_pix_stride + a.out_c_off + r16;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float mx = fmaxf(fmaxf(acc[i][j][0], acc[i][j][1]), fmaxf(acc[i][j][2], acc[i][j][3]));
+                float x = fmaf(mx, ssh[16 * j + r16], ssh[128 + 16 * j + r16]);
+                x = fmaxf(x, LRELU * x);
+                const _Float16 h = (_Float16)x;
+                const _Float16 l = (_Float16)(x - (float)h);
+                __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, h), ors, (pbase + 32 * j) * 2, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, l), ors, (pbase + 32 * j + 16) * 2, 0, 0);
+            }
+        }
+    };
+    i32x4 fa[4], fb[8], na[4], nb[8];
+    auto tile = [&](int k, i32x4 (&xa)[4], i32x4 (&xb)[8], i32x4 (&ya)[4], i32x4 (&yb)[8]) {
+        const int hs = k % NWS, hn = (k + 1) % NWS;
+        slice(hs, 0, hs, 1, xa, xb, ya, yb, true);
+        slice(hs, 1, hs, 2, ya, yb, xa, xb, false);
+        slice(hs, 2, hs, 3, xa, xb, ya, yb, false);
+        slice(hs, 3, hs, 4, ya, yb, xa, xb, false);
+        // slice 4 reads tile k+1's first fragments (window k+1 was stored before B_{k-1}; past the last tile the
+        // read hits a stale slot and is never used)
+        slice(hs, 4, hn, 0, xa, xb, ya, yb, false);
+        epilogue(k);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        barrier_raw();   // B_k: window k is no longer read
+    };
+    fragA(0, 0, 0, fa);
+    fragB(0, 0, fb);
+    for (int k = 0; k < nmine; k += 2) {
+        tile(k, fa, fb, na, nb);
+        if (k + 1 < nmine) tile(k + 1, na, nb, fa, fb);
+    }
+}
+
 }  // namespace
 
 int launch_conv_v1r(const HaloArgs& a, hipStream_t s) {
+    if (a.split) {
+        if (int rc = ensure_lds_attr((const void*)k_conv_v1s, LDS_S)) return rc;
+        if (a.Hc % TH || a.Wc % TW || a.Co != 128 || a.Ci != NF || !a.w || a.out_mode != OUT_S16) {
+            set_error("v_conv1 split kernel: unexpected layer shape, packing or output format");
+            return 3;
+        }
+        int dev = 0, ncu = 256;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+        const int tiles = a.N * (a.Hc / TH) * (a.Wc / TW);
+        int gx = ncu >= 8 ? ncu / 8 * 8 : ncu;
+        if (gx > tiles) gx = tiles;
+        hipLaunchKernelGGL(k_conv_v1s, dim3(gx), dim3(512), LDS_S, s, a);
+        AVSE_HIP_CHECK(hipGetLastError());
+        return 0;
+    }
     if (int rc = ensure_lds_attr((const void*)k_conv_v1r<0>, LDS_LAUNCH)) return rc;
     if (a.Hc % TH || a.Wc % TW || a.Co != 128 || a.Ci != NF || !a.w) {
         set_error("v_conv1 row-run kernel: unexpected layer shape or missing packing");

@@ -82,7 +82,9 @@ constexpr NetPlan make_plan(int T, int F) {
     return p;
 }
 
-constexpr bool plan_valid(int T, int F) { return T >= 4 && T % 4 == 0 && T <= 4096 && F >= 1 && F <= 8; }
+// T <= 64: the range the kernels' 32-bit activation / gather-map indexing is validated for (T = 20 at 25 fps, 24 at
+// 29.97 / 30 fps; a 1023-clip training batch keeps every tensor far below 2^31 elements there)
+constexpr bool plan_valid(int T, int F) { return T >= 4 && T % 4 == 0 && T <= 64 && F >= 1 && F <= 8; }
 
 // audio 80x20x1, video 128x128x5 (data_processor.py:12, :47-55 at 16 kHz / 25 fps): the benchmarked network
 inline constexpr NetPlan kPlan25 = make_plan(20, 5);

@@ -35,7 +35,7 @@ def embedding(T):
 def shape_supported(T, F):
     """The shapes libavse implements (include/avse.h avse_weights_blob_floats_shape): the decoder reproduces 80 x T
     only for T a multiple of 4 (else Keras' own fit / evaluate would fail on the shape mismatch too)."""
-    return T >= 4 and T % 4 == 0 and T <= 4096 and 1 <= F <= 8
+    return T >= 4 and T % 4 == 0 and T <= 64 and 1 <= F <= 8   # csrc/netplan.h plan_valid
 
 
 def layers(T=20, F=5):

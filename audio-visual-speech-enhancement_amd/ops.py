@@ -11,7 +11,9 @@ import torch
 from . import _lib
 from .model import KerasModel, blob_floats
 
-DTYPES = {"float32": _lib.AVSE_F32, "fp32": _lib.AVSE_F32, "bfloat16": _lib.AVSE_BF16, "bf16": _lib.AVSE_BF16}
+DTYPES = {"float32": _lib.AVSE_F32, "fp32": _lib.AVSE_F32, "bfloat16": _lib.AVSE_BF16, "bf16": _lib.AVSE_BF16,
+          # float32 accuracy from split-f16 matrix-core products (include/avse.h AVSE_F32_SPLIT)
+          "float32_split": _lib.AVSE_F32_SPLIT, "fp32_split": _lib.AVSE_F32_SPLIT}
 
 
 def _dev_f32(t, name, shape=None):
@@ -115,7 +117,9 @@ class DeviceWeights:
         self.ctx = _lib.context(device)
         self.T, self.F = model.T, model.F
         blob = model.to_blob()
-        assert blob.size == blob_floats(self.T, self.F) == _lib.load().avse_weights_blob_floats_shape(self.T, self.F)
+        # the CDLL is held here: at interpreter exit the module globals may be gone before this object
+        self._cdll = _lib.load()
+        assert blob.size == blob_floats(self.T, self.F) == self._cdll.avse_weights_blob_floats_shape(self.T, self.F)
         self.handle = ctypes.c_void_p()
         with torch.cuda.device(self.ctx.device_index):
             _lib.check(_lib.load().avse_weights_load_shape(self.ctx.handle, blob.ctypes.data_as(ctypes.c_void_p),
@@ -127,9 +131,9 @@ class DeviceWeights:
         return (80, self.T)
 
     def __del__(self):
-        h = getattr(self, "handle", None)
-        if h is not None and h.value and _lib._lib is not None:
-            _lib._lib.avse_weights_destroy(h)
+        h, lib = getattr(self, "handle", None), getattr(self, "_cdll", None)
+        if h is not None and h.value and lib is not None:
+            lib.avse_weights_destroy(h)
             self.handle = None
 
 
@@ -239,6 +243,7 @@ class Trainer:
         self.max_batch = int(max_batch)
         self.T, self.F = model.T, model.F
         blob = model.to_blob()
+        self._cdll = _lib.load()   # held for __del__ (see DeviceWeights)
         self.handle = ctypes.c_void_p()
         with torch.cuda.device(self.ctx.device_index):
             _lib.check(_lib.load().avse_trainer_create_shape(self.ctx.handle, blob.ctypes.data_as(ctypes.c_void_p),
@@ -292,7 +297,7 @@ class Trainer:
         return v.value
 
     def __del__(self):
-        h = getattr(self, "handle", None)
-        if h is not None and h.value and _lib._lib is not None:
-            _lib._lib.avse_trainer_destroy(h)
+        h, lib = getattr(self, "handle", None), getattr(self, "_cdll", None)
+        if h is not None and h.value and lib is not None:
+            lib.avse_trainer_destroy(h)
             self.handle = None

@@ -28,7 +28,9 @@
 extern "C" {
 #endif
 
-#define AVSE_ABI_VERSION 1
+/* 2: compute dtype AVSE_F32_SPLIT, avse_ctx_reserve_weights; option names tile_alt / aud_side removed (round 3);
+ *    status AVSE_ERR_CHECK (checked build) */
+#define AVSE_ABI_VERSION 2
 
 enum avse_status {
     AVSE_OK = 0,
@@ -39,7 +41,17 @@ enum avse_status {
     AVSE_ERR_CHECK = 5         /* checked build only: a device-side protocol / bounds check fired */
 };
 
-enum avse_dtype { AVSE_F32 = 0, AVSE_BF16 = 1 };
+/* Compute dtypes of avse_weights_load (inputs, outputs and accumulation are float32 in all three):
+ *   AVSE_F32        every layer on exact-fp32 MFMA (v_mfma_f32_16x16x4_f32: a k-ordered fmaf chain)
+ *   AVSE_BF16       activations and weights rounded to bf16 (the fast path; ~2e-3 relative output error)
+ *   AVSE_F32_SPLIT  float32 accuracy on the 16-bit matrix cores: the video convolutions v_conv1..v_conv5 carry every
+ *                   fp32 operand as an f16 pair x = h + l (h = f16(x), l = f16(x - h); weights scaled per output
+ *                   channel by a power of two) and form all four products h h, h l, l h, l l with
+ *                   v_mfma_f32_16x16x32_f16, each MFMA rounding its 32 exact products once into the fp32 accumulator —
+ *                   measured MORE accurate than AVSE_F32 (tools/split_probe.hip); the other layers run as AVSE_F32.
+ *                   Activations of these layers must stay below 65504 in magnitude (f16 range; BatchNormalization
+ *                   keeps a trained network's far below). */
+enum avse_dtype { AVSE_F32 = 0, AVSE_BF16 = 1, AVSE_F32_SPLIT = 2 };
 enum avse_pad_mode { AVSE_PAD_REFLECT = 0, AVSE_PAD_CONSTANT = 1 };
 
 typedef struct avse_ctx avse_ctx;
@@ -71,9 +83,13 @@ void avse_ctx_destroy(avse_ctx* ctx);
 int avse_ctx_set_option(avse_ctx* ctx, const char* name, int value);
 int avse_ctx_get_option(avse_ctx* ctx, const char* name, int* value);
 
-/* Pre-size the forward scratch for up to max_clips clips so that later avse_forward calls never
- * allocate (required before capturing avse_forward into a hipGraph). */
+/* Pre-size the forward scratch for up to max_clips clips of the 25-fps network so that later avse_forward calls
+ * never allocate (required before capturing avse_forward into a hipGraph). */
 int avse_ctx_reserve(avse_ctx* ctx, int64_t max_clips, int compute_dtype);
+/* The same for the network shape and compute dtype `weights` were loaded for (avse_weights_load_shape: e.g. the
+ * 29.97 / 30-fps networks need a larger scratch).  avse_forward fails with AVSE_ERR_INVALID, instead of growing the
+ * scratch, while its stream is being captured. */
+int avse_ctx_reserve_weights(avse_ctx* ctx, const avse_weights* weights, int64_t max_clips);
 
 /* ---- audio front end ------------------------------------------------------------------- */
 
@@ -137,7 +153,7 @@ int64_t avse_weights_blob_floats_shape(int spec_frames, int video_frames);
  *   order: a_conv1..5, v_conv1..6, enc_dense, dec_dense1, dec_dense2, d_deconv1..6
  *   (d_deconv6 has no BatchNormalization).
  * BN (eps 1e-3) is folded into per-channel scale/shift; kernels are repacked for the implicit
- * GEMM and uploaded in compute_dtype (AVSE_F32 or AVSE_BF16).  Synchronous. */
+ * GEMM and uploaded in compute_dtype (avse_dtype).  Synchronous. */
 int avse_weights_load(avse_ctx* ctx, const float* host_blob, int64_t n_floats, int compute_dtype,
                       avse_weights** out);
 /* avse_weights_load for the network of build((80, spec_frames), (128, 128, video_frames)); the weights remember

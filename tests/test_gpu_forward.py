@@ -36,6 +36,10 @@ BUF_SHAPES = {"video_in": (128, 128, 8), "audio_in": (80, 20, 8), "a_conv1": (40
               "d_deconv5": (80, 20, 64)}
 
 
+# AVSE_F32_SPLIT: buffers written by one split video layer for the next (v_conv5 feeds the generic v_conv6 in fp32)
+SPLIT_PAIR_BUFS = ("v_conv1", "v_conv2", "v_conv3", "v_conv4")
+
+
 def make_inputs(N, seed):
     rng = np.random.default_rng(seed)
     from conftest import synth_audio
@@ -74,7 +78,13 @@ def scratch(dw, N, clips=None, names=None):
             rc = hip.hipMemcpy(ctypes.c_void_p(t.data_ptr() + j * per * es),
                                ctypes.c_void_p(base.value + offs[i] + c * per * es), per * es, 3)
             assert rc == 0
-        out[name] = t.float().cpu().numpy().reshape((len(clips),) + BUF_SHAPES[name])
+        if dw.dtype == _lib.AVSE_F32_SPLIT and name in SPLIT_PAIR_BUFS:
+            # split-pair layout (include/avse.h AVSE_F32_SPLIT): per pixel and 16 channels [h(16) | l(16)] f16
+            shp = BUF_SHAPES[name]
+            hl = t.view(torch.float16).float().cpu().numpy().reshape((len(clips),) + shp[:-1] + (shp[-1] // 16, 2, 16))
+            out[name] = (hl[..., 0, :].astype(np.float64) + hl[..., 1, :]).reshape((len(clips),) + shp)
+        else:
+            out[name] = t.float().cpu().numpy().reshape((len(clips),) + BUF_SHAPES[name])
     return out
 
 

@@ -1,0 +1,122 @@
+"""AVSE_F32_SPLIT parity: the video convolutions on split-f16 operands (conv_v1r.hip k_conv_v1s, conv_stream.hip
+k_conv_stream<..., S16>: every fp32 operand as the f16 pair h + l, all four products on the 16-bit matrix cores,
+fp32 accumulation) against the float64 Keras-semantics oracle, under the SAME bounds as the exact-fp32 path
+(test_gpu_forward.py FP32_ABS / FP32_REL: the north star's 1e-4 absolute RMS on dB-scale outputs, 1e-5 relative),
+every materialised layer included; and against the exact-fp32 path's own error (measured: no worse).
+"""
+import numpy as np
+import pytest
+
+from oracle import keras_ref as K
+from oracle import librosa_ref as R
+from test_gpu_forward import (FP32_ABS, FP32_REL, abs_rms, db_scale, make_inputs, rel_rms, run_case, scratch,
+                              spread_clips)
+
+pytestmark = pytest.mark.gpu
+
+SPLIT = "float32_split"
+
+
+@pytest.mark.parametrize("N,db", [(1, False), (3, True), (37, False), (37, True)])
+def test_split_forward_matches_oracle(gpu, N, db):
+    got, ref, inter, dw = run_case(gpu, N, SPLIT, seed=N, db=db)
+    err, ae = rel_rms(got, ref), abs_rms(got, ref)
+    got32, _, _, _ = run_case(gpu, N, "float32", seed=N, db=db)
+    ae32 = abs_rms(got32, ref)
+    print(f"split N={N} db={db}: output RMS {np.sqrt(np.mean(ref ** 2)):.3g}, abs RMS err {ae:.3e} (exact fp32 "
+          f"{ae32:.3e}), rel {err:.3e}")
+    if err > FP32_REL:
+        sc = scratch(dw, N)
+        report = {k: rel_rms(sc[k], inter[k]) for k in inter if k in sc}
+        pytest.fail(f"rel RMS {err:.3e}; per-layer rel RMS: {report}")
+    assert ae <= FP32_ABS, ae
+    assert ae <= 1.5 * ae32 + 1e-6, (ae, ae32)
+
+
+def test_split_intermediates(gpu):
+    """Every layer (the split-pair buffers decoded h + l) against the oracle; the fused d_deconv6 is unfused here."""
+    from avse_amd import _lib
+    with _lib.context().options(unfused_tail=1):
+        got, ref, inter, dw = run_case(gpu, 2, SPLIT, seed=21, normalize=True)
+        sc = scratch(dw, 2)
+    for k in inter:
+        if k in sc:
+            print(f"{k:12s} rel {rel_rms(sc[k], inter[k]):.2e}")
+            assert rel_rms(sc[k], inter[k]) <= FP32_REL, (k, rel_rms(sc[k], inter[k]))
+
+
+@pytest.mark.parametrize("N", [5, 301, 512])
+def test_split_bench_batch_matches_oracle(gpu, N):
+    """The launch bench.py times in the split dtype (its inputs, normaliser, 512 clips; N = 301 and 5 leave ragged
+    4-clip v_conv5 tiles): output and every materialised layer of spread clips against the float64 oracle."""
+    import bench
+    from avse_amd import ops
+    from avse_amd.model import KerasModel
+    rng = np.random.default_rng(1234)
+    audio_np, video_np = bench.synth(rng, N)
+    mean_np = video_np.mean(axis=(0, 3)).astype(np.float32)
+    std_np = video_np.std(axis=(0, 3)).astype(np.float32)
+    model = db_scale(KerasModel.init(seed=0, randomize=True))
+    dw = ops.DeviceWeights(model, SPLIT)
+    mel = ops.spectrogram(ops.to_device(audio_np), frames_per_slice=20).view(N, 80, 20)
+    out = ops.forward(dw, mel, ops.to_device(video_np), ops.to_device(mean_np), ops.to_device(std_np)).cpu().numpy()
+    clips = spread_clips(N, k=12)
+    mel_np = mel.cpu().numpy()[clips]
+    inter = {}
+    vn = R.video_normalize(video_np[clips], mean_np, std_np).astype(np.float32)
+    ref = K.forward(model.layer_dict(), mel_np, vn, intermediates=inter)
+    names = ["v_conv1", "v_conv2", "v_conv3", "v_conv4", "v_conv5", "concat"]
+    sc = scratch(dw, N, clips, names)
+    layers = {k: rel_rms(sc[k], inter[k]) for k in names}
+    ae = abs_rms(out[clips], ref)
+    print(f"split N={N}: output abs RMS {ae:.3e} rel {rel_rms(out[clips], ref):.3e}; per layer {layers}")
+    assert np.isfinite(out).all()
+    assert ae <= FP32_ABS
+    assert rel_rms(out[clips], ref) <= FP32_REL
+    for k, e in layers.items():
+        assert e <= FP32_REL, (k, e)
+
+
+def test_split_zero_video(gpu):
+    """video = None (BASELINE configs[2]): the N = 1 split video encoder on the all-zero clip, broadcast."""
+    from avse_amd import ops
+    from avse_amd.model import KerasModel
+    model = db_scale(KerasModel.init(seed=5, randomize=True))
+    mel, _ = make_inputs(6, 44)
+    ref = K.forward(model.layer_dict(), mel, None)
+    dw = ops.DeviceWeights(model, SPLIT)
+    got = ops.forward(dw, ops.to_device(mel), None).cpu().numpy()
+    assert abs_rms(got, ref) <= FP32_ABS and rel_rms(got, ref) <= FP32_REL
+
+
+@pytest.mark.parametrize("T,F", [(24, 5), (24, 6)])
+def test_split_other_frame_rates(gpu, T, F):
+    """29.97 fps (5 frames: the split video kernels) and 30 fps (6 frames: v_conv1 has no split kernel, so every video
+    layer runs the generic fp32 one) networks in the split dtype."""
+    from avse_amd import ops
+    from avse_amd.model import KerasModel
+    from conftest import synth_video
+    model = db_scale(KerasModel.init(seed=2, randomize=True, audio_shape=(80, T), video_shape=(128, 128, F)))
+    rng = np.random.default_rng(3)
+    mel = rng.normal(-40, 15, (3, 80, T)).astype(np.float32)
+    video = synth_video(rng, 3, f=F)
+    ref = K.forward(model.layer_dict(), mel, video)
+    dw = ops.DeviceWeights(model, SPLIT)
+    got = ops.forward(dw, ops.to_device(mel), ops.to_device(video)).cpu().numpy()
+    print(f"split T={T} F={F}: abs {abs_rms(got, ref):.3e} rel {rel_rms(got, ref):.3e}")
+    assert abs_rms(got, ref) <= FP32_ABS and rel_rms(got, ref) <= FP32_REL
+
+
+def test_split_small_activations(gpu):
+    """Tiny inputs (video x 1e-4, no normaliser): activations whose lo pieces are f16 subnormals; the error stays
+    within the fp32 bounds relative to the output."""
+    from avse_amd import ops
+    from avse_amd.model import KerasModel
+    model = KerasModel.init(seed=8, randomize=True)
+    mel, video = make_inputs(3, 12)
+    video = (video * 1e-4).astype(np.float32)
+    ref = K.forward(model.layer_dict(), mel, video)
+    dw = ops.DeviceWeights(model, SPLIT)
+    got = ops.forward(dw, ops.to_device(mel), ops.to_device(video)).cpu().numpy()
+    print(f"split tiny video: rel {rel_rms(got, ref):.3e}")
+    assert rel_rms(got, ref) <= FP32_REL

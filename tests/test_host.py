@@ -42,7 +42,7 @@ def test_abi_version_and_blob_size():
     from avse_amd import _lib
     from avse_amd.model import blob_floats
     lib = _lib.load()
-    assert lib.avse_abi_version() == 1
+    assert lib.avse_abi_version() == _lib.ABI_VERSION == 2
     assert lib.avse_weights_blob_floats() == blob_floats()
 
 
