@@ -243,12 +243,24 @@ size_t buf_elems(const NetPlan& p, int b) {
     return e[b];
 }
 
-// Split-K plan for a single-phase GEMM of M rows x Co columns x kpad on k_conv: double the split while the
-// grid stays <= ~1024 workgroups and every split keeps >= 16 k-slabs (64-byte slabs).
+// Split-K plan for a single-phase GEMM of M rows x Co columns x kpad on k_conv.
+//  bf16: double the split while the grid stays <= ~1024 workgroups and every split keeps >= 16 k-slabs.
+//  fp32 (AVSE_F32, and the generic layers of AVSE_F32_SPLIT): block-exact, as the training step's train_split —
+//  every split is exactly one block of k_conv's blocked fp32 summation (kFp32Block 16-product slabs) and
+//  k_splitk_reduce_tiles adds the splits in order, so each sum is the unsplit kernel's bit for bit.  Whether a launch
+//  splits (short grids only) then changes no result: the fp32 forward of a clip is the same whatever batch it runs
+//  in (the batched CLI predict reproduces the per-sample one exactly; tests/test_gpu_split.py).
+constexpr int64_t kSplitTileCap = 2048;   // fp32 tiles x splits per launch (128 x 128-float partials each)
 int choose_ksplit(int64_t M, int Co, int kpad, int dtype) {
     const int BN = Co <= 64 ? 64 : 128;
     const int64_t tiles = ((M + 127) / 128) * ((Co + BN - 1) / BN);
-    const int nslab = kpad / (dtype == AVSE_BF16 ? 32 : 16);
+    if (dtype != AVSE_BF16) {
+        const int nslab = kpad / 16;
+        const int ks = (nslab + kFp32Block - 1) / kFp32Block;
+        if (tiles >= 256 || ks < 2 || (nslab + ks - 1) / ks != kFp32Block || tiles * ks > kSplitTileCap) return 1;
+        return ks;
+    }
+    const int nslab = kpad / 32;
     int ks = 1;
     while (tiles * ks * 2 <= 1024 && nslab / (ks * 2) >= 16) ks *= 2;
     return ks;

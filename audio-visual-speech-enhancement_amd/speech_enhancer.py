@@ -18,7 +18,11 @@ Differences (host plumbing outside the hot path):
     build never unpickles);
   * predict runs ONE forward per sample: the printed loss (speech_enhancer.py:76-77, an MSE over the
     sample like Model.evaluate) is computed from the same prediction that is reconstructed (the reference
-    runs evaluate and predict, two forwards of the same input).
+    runs evaluate and predict, two forwards of the same input);
+  * predict batches: samples of one shape (slice count, frame rate, mixture length) run as one forward and one
+    batched STFT / ISTFT (BatchPredictor) — every result equals the per-sample path's bit for bit (the fp32 forward
+    is batch-invariant, csrc/capi.hip choose_ksplit); `-g N` (parsed and ignored by the reference,
+    speech_enhancer.py:289) runs N ranks, one per GPU, each on a contiguous block of the samples.
 All spectrogram / network / reconstruction arithmetic goes through libavse (K1, forward, K6).
 """
 import argparse
@@ -26,6 +30,9 @@ import json
 import logging
 import os
 import random
+import socket
+import subprocess
+import sys
 from collections import namedtuple
 
 import numpy as np
@@ -179,27 +186,149 @@ def train(args):
     network.save(layout.model_file(args.model))
 
 
+def predict_one(network, video_normalizer, sample):
+    """The per-sample predict path of speech_enhancer.py:66-81: normalise + evaluate + predict as ONE forward (the
+    normaliser fused into the first video conv), then reconstruct -> (loss, enhanced AudioSignal)."""
+    pred, loss = network.predict_and_evaluate(sample.mixed_spectrograms, sample.video_samples,
+                                              sample.speech_spectrograms, video_normalizer=video_normalizer)
+    return loss, data_processor.reconstruct_speech_signal(sample.mixed_signal, pred, sample.video_frame_rate)
+
+
+def sample_groups(samples):
+    """Indices of the samples that run as one batch — same slice count and shapes, frame rate and mixture length
+    (the batched ISTFT takes equal-length utterances) — in first-seen order."""
+    groups = {}
+    for i, smp in enumerate(samples):
+        key = (tuple(smp.mixed_spectrograms.shape), tuple(smp.video_samples.shape), float(smp.video_frame_rate),
+               smp.mixed_signal.get_number_of_samples(), smp.mixed_signal.get_sample_rate())
+        groups.setdefault(key, []).append(i)
+    return list(groups.values())
+
+
+class BatchPredictor:
+    """predict + evaluate + reconstruct of a group of equal-shape samples as one batch on one device: one forward over
+    all their slices (in chunks of <= `chunk` clips), one MSE per sample (the avse_mse of the per-sample path), one
+    STFT of the stacked mixtures for the phase and one ISTFT.  Each result equals predict_one's bit for bit."""
+
+    def __init__(self, network, video_normalizer=None, chunk=1024):
+        self.network = network
+        self.video_normalizer = video_normalizer
+        self.chunk = int(chunk)
+
+    def __call__(self, group):
+        import torch
+        from . import ops
+        dw = self.network.device_weights()
+        dev = torch.device("cuda", dw.ctx.device_index)
+        U = len(group)
+        S, nm, T = group[0].mixed_spectrograms.shape
+        mixed = torch.from_numpy(np.stack([g.mixed_spectrograms for g in group]).astype(np.float32)).to(dev)
+        video = torch.from_numpy(np.stack([g.video_samples for g in group]).astype(np.float32)).to(dev)
+        speech = torch.from_numpy(np.stack([g.speech_spectrograms for g in group]).astype(np.float32)).to(dev)
+        m = s = None
+        if self.video_normalizer is not None:
+            m, s = self.video_normalizer.device_stats(dev)
+        n = U * S
+        clips, frames = mixed.view(n, nm, T), video.view((n,) + tuple(video.shape[2:]))
+        pred = torch.empty_like(clips)
+        for a in range(0, n, self.chunk):
+            b = min(n, a + self.chunk)
+            ops.forward(dw, clips[a:b], frames[a:b], m, s, out=pred[a:b])
+        pred = pred.view(U, S, nm, T)
+        losses = [ops.mse(pred[u], speech[u]) for u in range(U)]
+        sr, fps = group[0].mixed_signal.get_sample_rate(), group[0].video_frame_rate
+        n_fft = int(float(sr) / fps)
+        hop = int(n_fft / 4)
+        sig = torch.from_numpy(np.stack([np.asarray(g.mixed_signal.get_data(channel_index=0)) for g in group])
+                               .astype(np.float32)).to(dev)
+        _, D = ops.spectrogram(sig, sample_rate=sr, n_fft=n_fft, hop_length=hop, n_mels=data_processor.N_MELS,
+                               fmin=data_processor.MEL_FMIN, fmax=data_processor.MEL_FMAX, return_stft=True)
+        y = ops.istft(pred.contiguous(), D, sample_rate=sr, n_fft=n_fft, hop_length=hop, n_mels=data_processor.N_MELS,
+                      fmin=data_processor.MEL_FMIN, fmax=data_processor.MEL_FMAX).cpu().numpy()
+        return [(float(losses[u].item()), AudioSignal(y[u], sr)) for u in range(U)]
+
+
+def predict_samples(samples, predictor, run_dir, world=1, rank=0, write=write_prediction, fallback=None):
+    """The predict loop over this rank's contiguous block of `samples` (parallel.shard_bounds), a batch per
+    sample_groups group; outputs are written by the rank that owns the sample (one node: a shared file system).  A
+    group that fails is retried sample by sample (`fallback`, or the predictor on one sample) so that, as in the
+    reference (speech_enhancer.py:87-88), only the failing sample is skipped.  Returns {sample index: loss or None}
+    for every sample on rank 0 (gathered from all ranks), this rank's own otherwise."""
+    from .parallel import shard_bounds
+    lo, hi = shard_bounds(len(samples), world, rank)
+    mine = samples[lo:hi]
+    losses = {}
+    for idxs in sample_groups(mine):
+        try:
+            outs = predictor([mine[i] for i in idxs])
+        except Exception:  # noqa: BLE001 — isolate the failing sample below
+            outs = None
+        for k, i in enumerate(idxs):
+            try:
+                loss, signal = outs[k] if outs is not None else (fallback or (lambda smp: predictor([smp])[0]))(mine[i])
+                write(run_dir, mine[i], signal)
+                losses[lo + i] = loss
+            except Exception:  # noqa: BLE001 — mirrors speech_enhancer.py:87-88
+                logging.exception("failed to predict %s. skipping" % mine[i].video_file_path)
+                losses[lo + i] = None
+    if world > 1:
+        import torch.distributed as dist
+        parts = [None] * world
+        dist.all_gather_object(parts, losses)
+        if rank == 0:
+            for p in parts:
+                losses.update(p)
+    return losses
+
+
+def _launch_ranks(n):
+    """`predict -g N` outside a launcher: one rank per GPU as a child torch.distributed.run (rendezvous on
+    127.0.0.1), same arguments; nothing in this process has touched the GPU."""
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    return subprocess.call([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+                            "--master-addr", "127.0.0.1", "--master-port", str(port), sys.argv[0]] + sys.argv[1:])
+
+
 def predict(args):
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(_launch_ranks(args.gpus))
+    world, rank = int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0"))
     layout = Layout(args.base_dir)
-    run_dir = layout.prediction_run_dir(args.model, args.data_name)
     model_path, keras_path = layout.model_file(args.model), layout.keras_model_file(args.model)
     if not os.path.exists(model_path) and os.path.exists(keras_path):
         raise SystemExit("%s is a Keras model: convert it once with\n  /opt/conda/bin/python3.9 tools/keras_h5_to_avse.py "
                          "%s %s" % (keras_path, keras_path, model_path))
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # one timestamped run directory for every rank: rank 0 creates it
+        box = [str(layout.prediction_run_dir(args.model, args.data_name)) if rank == 0 else None]
+        dist.broadcast_object_list(box, 0)
+        run_dir = box[0]
+    else:
+        run_dir = layout.prediction_run_dir(args.model, args.data_name)
     network = SpeechEnhancementNetwork.load(model_path, compute_dtype=args.dtype)
     video_normalizer = data_processor.VideoNormalizer.load(layout.normalizer_file(args.model))
     samples = load_preprocessed_blob(layout.preprocessed(args.data_name))
-    for sample in samples:
-        try:
-            print("predicting (%s, %s)..." % (sample.video_file_path, sample.noise_file_path))
-            # normalize + evaluate + predict as ONE forward, the normaliser fused into the first video conv
-            pred, loss = network.predict_and_evaluate(sample.mixed_spectrograms, sample.video_samples,
-                                                      sample.speech_spectrograms, video_normalizer=video_normalizer)
-            print("loss: %f" % loss)
-            signal = data_processor.reconstruct_speech_signal(sample.mixed_signal, pred, sample.video_frame_rate)
-            write_prediction(run_dir, sample, signal)
-        except Exception:  # noqa: BLE001 — mirrors speech_enhancer.py:87-88
-            logging.exception("failed to predict %s. skipping" % sample.video_file_path)
+    if args.per_sample:
+        predictor = lambda group: [predict_one(network, video_normalizer, smp) for smp in group]  # noqa: E731
+    else:
+        predictor = BatchPredictor(network, video_normalizer)
+    losses = predict_samples(samples, predictor, run_dir, world, rank,
+                             fallback=lambda smp: predict_one(network, video_normalizer, smp))
+    if rank == 0:
+        for i, smp in enumerate(samples):
+            print("predicting (%s, %s)..." % (smp.video_file_path, smp.noise_file_path))
+            if losses.get(i) is not None:
+                print("loss: %f" % losses[i])
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
 
 
 def main(argv=None):
@@ -229,7 +358,8 @@ def main(argv=None):
     q.add_argument("-mn", "--model", type=str, required=True)
     q.add_argument("-dn", "--data_name", type=str, required=True)
     q.add_argument("-g", "--gpus", type=int, default=1)
-    q.add_argument("--dtype", default="float32", choices=["float32", "bfloat16"])
+    q.add_argument("--dtype", default="float32_split", choices=["float32_split", "float32", "bfloat16"])
+    q.add_argument("--per-sample", action="store_true", help="one forward / STFT / ISTFT per sample (unbatched)")
     q.set_defaults(func=predict)
 
     args = parser.parse_args(argv)

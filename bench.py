@@ -2,9 +2,14 @@
 
 One "step" = one pass of the hot path over one batch of synthetic 200-ms clips already resident in
 HBM: K1 spectrogram of B x 3200 samples -> mel-dB [B, 80, 20] -> full fusion forward (BASELINE.json
-configs[3], bf16, batch 512 per GPU) -> [B, 80, 20] predicted speech spectrograms; for N > 1 the
+configs[3]'s workload, batch 512 per GPU) -> [B, 80, 20] predicted speech spectrograms; for N > 1 the
 outputs are all-gathered over RCCL (the north star's final gather).  Weak scaling by default (every
 rank processes B clips per step); --strong splits a fixed global batch of B clips over the ranks.
+
+The headline runs at the north star's accuracy (float32 arithmetic of the Keras reference, output within 1e-4 RMS):
+--dtype fp32_split (default) = include/avse.h AVSE_F32_SPLIT (video convs on split-f16 matrix-core products, fp32
+accumulation; measured at least as accurate as exact-fp32 MFMA), fp32 = exact-fp32 MFMA everywhere, bf16 = the
+reduced-precision path (a leg at N = 1, with its parity against the 1e-4 bound).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--strong]
     python bench.py --e2e [--steps K]        (BASELINE configs[4], its own JSON line)
@@ -47,6 +52,20 @@ FLOP_AUDIO_BRANCH = 2e6 * sum(MMAC.values())     # configs[2]: audio encoder + d
 FLOP_V_CONV2 = 2 * 64 * 64 * 128 * 3200          # dominant kernel: v_conv2 implicit GEMM (M=4096, N=128, K=3200)
 STFT_BYTES_PER_CLIP = SEG * 4 + 80 * 20 * 4      # 12,800 B in + 6,400 B out
 PEAK_TFLOPS = {"bf16": 256 * 4 * 2.4e9 * 1024 / 1e12, "fp32": 256 * 4 * 2.4e9 * 64 / 1e12}   # 2516.6 / 157.3
+# AVSE_F32_SPLIT's video convs issue 4 f16 MFMA products (h h, h l, l h, l l) per fp32 multiply-add: their matrix-core
+# ceiling in fp32 FLOP/s is the dense f16 peak (= bf16's, MI355X_MICROARCH.md) / 4
+PEAK_TFLOPS["fp32_split"] = PEAK_TFLOPS["bf16"] / 4                                           # 629.1
+LIB_DTYPE = {"fp32": "float32", "fp32_split": "float32_split", "bf16": "bf16"}
+ARITHMETIC = {
+    "fp32": "float32 everywhere: exact-fp32 MFMA (v_mfma_f32_16x16x4_f32), fp32 activations",
+    "fp32_split": "float32 inputs / outputs / accumulation / activations between the generic layers; the video convs "
+                  "v_conv1..v_conv5 carry each fp32 operand as an f16 pair x = h + l and form all four products on "
+                  "v_mfma_f32_16x16x32_f16 (32 exact products rounded once into the fp32 accumulator): include/avse.h "
+                  "AVSE_F32_SPLIT; the other layers exact-fp32 MFMA",
+    "bf16": "bf16 activations and weights, fp32 accumulation (reduced precision)"}
+KERNEL_NAME = {"bf16": "k_conv_stream<5, 16, 16, 1, true, 10, 0, 1, false>",
+               "fp32_split": "k_conv_stream<5, 16, 16, 1, true, 10, 0, 1, true>",
+               "fp32": "k_conv<float, 128, true>"}
 PEAK_HBM_GBS = 8000.0
 
 
@@ -60,10 +79,11 @@ def synth(rng, B, video=True):
     return audio, vid
 
 
-def pmc_summary(B):
-    """Per-kernel PMC summary of a committed profile of THIS source tree at this batch (profiles/<tag>_pmc.json,
-    written by tools/pmc_summary.py from separate rocprofv3 FETCH_SIZE / WRITE_SIZE / MFMA-busy passes, carrying the
-    source digest of the tree it measured).  A profile of another tree is never attached: (None, None, reason)."""
+def pmc_summary(B, dtype):
+    """Per-kernel PMC summary of a committed profile of THIS source tree at this batch and dtype
+    (profiles/<tag>_pmc.json, written by tools/pmc_summary.py from separate rocprofv3 FETCH_SIZE / WRITE_SIZE /
+    MFMA-busy passes, carrying the source digest of the tree it measured): (file, {"kernels": .., "kernel_stats_avg_ms":
+    ..}, None).  A profile of another tree is never attached: (None, None, reason)."""
     digest = _lib.source_digest()
     stale = []
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")), reverse=True):
@@ -71,10 +91,10 @@ def pmc_summary(B):
             d = json.load(open(f))
         except ValueError:
             continue
-        if d.get("batch") != B or "kernels" not in d:
+        if d.get("batch") != B or dtype not in d.get("dtypes", {}):
             continue
         if d.get("source_digest") == digest:
-            return os.path.basename(f), d, None
+            return os.path.basename(f), d["dtypes"][dtype], None
         stale.append(os.path.basename(f))
     return None, None, (f"no committed PMC profile of source digest {digest} (newest of another tree: "
                         f"{stale[0] if stale else 'none'}); counters not attached")
@@ -157,13 +177,14 @@ def leg_audio_fp32(dev, model, reps=50, B=256):
             "stage_ms": {k: round(v, 4) for k, v in st.items() if v > 0.0005}, "reps": reps}
 
 
-def leg_fwd_fp32(dev, model, audio, video, mean, std, reps=10):
-    """configs[3]'s workload at the north star's accuracy: the same B = 512 clips, STFT + full fusion forward with
-    fp32 weights and activations (exact-fp32 MFMA, fp32 accumulation), priced against the fp32 MFMA peak.  Returns
-    (leg dict, the timed output) — the output's RMS against the float64 oracle is added by the cpu_baseline step."""
+def leg_fwd(dev, model, audio, video, mean, std, dtype, reps=10):
+    """configs[3]'s workload (the same B = 512 clips, STFT + full fusion forward) in another compute dtype: "fp32"
+    (exact-fp32 MFMA everywhere, priced against the fp32 MFMA peak) or "bf16" (the reduced-precision path, priced
+    against the bf16 peak).  Returns (leg dict, the timed output) — the output's RMS against the float64 oracle is
+    added by the cpu_baseline step."""
     B = audio.shape[0]
-    dw = ops.DeviceWeights(model, "float32", dev)
-    dw.ctx.reserve(B, dw.dtype)
+    dw = ops.DeviceWeights(model, LIB_DTYPE[dtype], dev)
+    dw.ctx.reserve_for(dw, B)
     mel = torch.empty((B, 1, 80, 20), dtype=torch.float32, device=dev)
     out = torch.empty((B, 80, 20), dtype=torch.float32, device=dev)
 
@@ -184,13 +205,15 @@ def leg_fwd_fp32(dev, model, audio, video, mean, std, reps=10):
     timed = out.cpu().numpy()
     _, st = ops.forward_profile(dw, mel.view(B, 80, 20), video, mean, std, out=out)
     tf = FLOP_PER_CLIP * B / (ms * 1e-3) / 1e12
-    top = sorted(((v, k) for k, v in st.items()), reverse=True)[:4]
+    top = sorted(((v, k) for k, v in st.items()), reverse=True)[:5]
     del dw
-    return {"config": "BASELINE configs[3] workload (B = 512, STFT + full audio-visual forward) in fp32: the "
-                      "arithmetic of the Keras reference (floatx float32) and of the north star's 1e-4 RMS bound",
-            "dtype": "fp32", "ms_per_step": round(ms, 3), "clips_per_s": round(B / (ms * 1e-3), 1),
-            "roofline": {"bound": "mfma", "achieved": round(tf, 2), "peak": round(PEAK_TFLOPS["fp32"], 1),
-                         "unit": "TFLOP/s", "frac": round(tf / PEAK_TFLOPS["fp32"], 4), "flop_per_clip": FLOP_PER_CLIP},
+    return {"config": f"BASELINE configs[3] workload (B = 512, STFT + full audio-visual forward), {dtype}",
+            "dtype": dtype, "arithmetic": ARITHMETIC[dtype], "ms_per_step": round(ms, 3),
+            "clips_per_s": round(B / (ms * 1e-3), 1),
+            "step_roofline": {"bound": "mfma", "achieved": round(tf, 2), "peak": round(PEAK_TFLOPS[dtype], 1),
+                              "unit": "TFLOP/s", "frac": round(tf / PEAK_TFLOPS[dtype], 4), "flop_per_clip": FLOP_PER_CLIP},
+            "v_conv2_ms": round(st["v_conv2"], 4),
+            "v_conv2_frac": round(FLOP_V_CONV2 * B / (st["v_conv2"] * 1e-3) / 1e12 / PEAK_TFLOPS[dtype], 4),
             "top_stage_ms": {k: round(v, 4) for v, k in top}, "reps": reps}, timed
 
 
@@ -280,9 +303,9 @@ def run_e2e(args, world, rank, dev, model):
     flat = video.view(-1, 128, 128, 5)
     vmean = flat.mean(dim=(0, 3)).contiguous()
     vstd = flat.std(dim=(0, 3), unbiased=False).contiguous()
-    dw = ops.DeviceWeights(model, args.dtype, dev)
+    dw = ops.DeviceWeights(model, LIB_DTYPE[args.dtype], dev)
     enh = Enhancer(dw, chunk=args.e2e_chunk)
-    dw.ctx.reserve(min(args.e2e_chunk, n_local * S), dw.dtype)
+    dw.ctx.reserve_for(dw, min(args.e2e_chunk, n_local * S))
 
     def step():
         out = enh(sig, video, vmean, vstd)
@@ -320,7 +343,8 @@ def run_e2e(args, world, rank, dev, model):
     res = {"metric": "clips/sec end-to-end predict (STFT -> fusion CNN -> ISTFT) on 200-ms@16kHz segments",
            "value": round(clips * args.steps / elapsed, 1), "unit": "clips/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True,
-           "scaling": "strong", "vs_baseline": None, "dtype": args.dtype,
+           "scaling": "strong", "vs_baseline": None, "dtype": "bf16" if args.dtype == "bf16" else "fp32",
+           "arithmetic": ARITHMETIC[args.dtype],
            "data": "synthetic on device: int16-scale noise+tone 3-s utterances, uint8-valued mouth crops; "
                    "random-init Keras-layout weights",
            "config": {"workload": "e2e: BASELINE configs[4], %d utterances x %d slices = %d clips, utterance-sharded"
@@ -353,7 +377,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=512, help="clips per GPU per step (global batch with --strong)")
     ap.add_argument("--strong", action="store_true", help="split a fixed global batch of --batch clips over the ranks")
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--dtype", default="fp32_split", choices=["fp32_split", "fp32", "bf16"],
+                    help="headline compute dtype (fp32_split / fp32 meet the north star's 1e-4 RMS; bf16 does not)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-legs", action="store_true", help="skip the configs[1] / configs[2] legs")
     ap.add_argument("--profile-reps", type=int, default=5)
@@ -401,8 +426,8 @@ def main():
         if world > 1:
             dist.destroy_process_group()
         return
-    dw = ops.DeviceWeights(model, args.dtype, dev)
-    dw.ctx.reserve(max(B, 1), dw.dtype)
+    dw = ops.DeviceWeights(model, LIB_DTYPE[args.dtype], dev)
+    dw.ctx.reserve_for(dw, max(B, 1))
 
     # every rank draws the same global batch and keeps its block (weak: its own seeded batch)
     rng = np.random.default_rng(1234 + (0 if args.strong else rank))
@@ -467,10 +492,16 @@ def main():
     dom = "v_conv2"
     achieved = FLOP_V_CONV2 * B / (stage_ms[dom] * 1e-3) / 1e12
     peak = PEAK_TFLOPS[args.dtype]
-    pmc_file, pmc, pmc_status = pmc_summary(B) if args.dtype == "bf16" else (None, None, "fp32 run: no profile")
+    pmc_file, pmc, pmc_status = pmc_summary(B, args.dtype)
     kp = (pmc or {}).get("kernels", {}).get(dom, {})
-    rp_ms = (pmc or {}).get("kernel_stats_avg_ms", {}).get(dom)
+    rp_ms = (pmc or {}).get("kernel_stats_avg_ms", {}).get(KERNEL_NAME[args.dtype])
     fwd_ms = sum(stage_ms.values())
+    kdesc = {"bf16": "k_conv_stream<5,16,16,1> bf16: persistent warp-specialised implicit GEMM M=4096/clip N=128 "
+                     "K=3200, fused BN+LReLU+2x2 maxpool",
+             "fp32_split": "k_conv_stream<5,16,16,1,S16>: the persistent warp-specialised implicit GEMM (M=4096/clip "
+                           "N=128 K=3200, fused BN+LReLU+2x2 maxpool) on split-f16 operands, 4 f16 MFMA products per "
+                           "fp32 MAC; peak = dense f16 MFMA peak / 4",
+             "fp32": "k_conv<float,128> implicit GEMM, exact-fp32 MFMA"}[args.dtype]
     result = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -482,16 +513,15 @@ def main():
         "higher_is_better": True,
         "scaling": "strong" if args.strong else "weak",
         "vs_baseline": None,
-        "dtype": args.dtype,
+        "dtype": "bf16" if args.dtype == "bf16" else "fp32",
+        "arithmetic": ARITHMETIC[args.dtype],
         "data": "synthetic: seeded int16-scale noise+harmonic audio (3200 samples/clip), uint8-valued 128x128x5 "
                 "mouth crops, random-init Keras-layout weights with randomised BN; inputs resident in HBM",
         "config": {"workload": "STFT (n_fft 640, hop 160, 80 mel, dB) + full audio-visual fusion forward "
                                "(BASELINE configs[3]) on 200-ms@16kHz clips",
                    "global_batch": global_batch, "per_gpu_batch": B, "parallelism": f"dp{world}"},
         "window_ms_per_step": win.summary(),
-        "roofline": {"kernel": f"{dom} (k_conv_stream<5,16,16,1>: persistent warp-specialised implicit GEMM "
-                               "M=4096/clip N=128 K=3200, fused BN+LReLU+2x2 maxpool)" if args.dtype == "bf16" else
-                               f"{dom} (k_conv<float,128> implicit GEMM, exact-fp32 MFMA)",
+        "roofline": {"kernel": f"{dom} ({kdesc})", "kernel_symbol": KERNEL_NAME[args.dtype],
                      "bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4), "traffic": kp.get("traffic_bytes"),
                      "algorithmic_bytes": kp.get("algorithmic_bytes"),
@@ -503,7 +533,8 @@ def main():
                                "frac_rocprof: rocprofv3 --kernel-trace --stats average of the same source tree "
                                "(profiles/<tag>_kernel_stats.csv, a separate profiled run)",
                      "avg_launch_ms_rocprof": rp_ms,
-                     "frac_rocprof": round(FLOP_V_CONV2 * B / (rp_ms * 1e-3) / 1e12 / peak, 4) if rp_ms else None},
+                     "frac_rocprof": round(FLOP_V_CONV2 * B / (rp_ms * 1e-3) / 1e12 / peak, 4) if rp_ms else None,
+                     "achieved_vs_fp32_mfma_peak": round(achieved / PEAK_TFLOPS["fp32"], 4)},
         "breakdown": {
             "stft_ms": round(stft_ms, 4),
             "stft_hbm_gbs": round(STFT_BYTES_PER_CLIP * B / (stft_ms * 1e-3) / 1e9, 1),
@@ -515,15 +546,19 @@ def main():
     }
     outs = {args.dtype: timed_out}
     if rank == 0 and world == 1 and not args.no_legs:
-        fp32_leg, outs["fp32_leg"] = leg_fwd_fp32(dev, model, audio, video, mean, std)
-        result["legs"] = {"fwd_fp32_b512": fp32_leg, "stft_b4096": leg_stft(dev),
-                          "audio_fp32_b256": leg_audio_fp32(dev, model), "train_fp32_b16": leg_train(dev, model)}
+        result["legs"] = {}
+        for ldt in ("fp32", "fp32_split", "bf16"):
+            if ldt != args.dtype:
+                result["legs"][f"fwd_{ldt}_b512"], outs[ldt] = leg_fwd(dev, model, audio, video, mean, std, ldt)
+        result["legs"].update({"stft_b4096": leg_stft(dev), "audio_fp32_b256": leg_audio_fp32(dev, model),
+                               "train_fp32_b16": leg_train(dev, model)})
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         base, parity = cpu_baseline(audio_np, video_np, mean_np, std_np, model, outs)
         result["cpu_baseline"] = base
-        result["parity"] = parity
-        if "fp32_leg" in parity:
-            result["legs"]["fwd_fp32_b512"]["parity"] = parity.pop("fp32_leg")
+        result["parity"] = {k: v for k, v in parity.items() if k not in outs or k == args.dtype}
+        for ldt in outs:
+            if ldt != args.dtype and f"fwd_{ldt}_b512" in result.get("legs", {}):
+                result["legs"][f"fwd_{ldt}_b512"]["parity"] = parity[ldt]
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

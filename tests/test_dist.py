@@ -128,3 +128,70 @@ def test_shard_bounds_cover_exactly_once():
             assert all(spans[i][1] == spans[i + 1][0] for i in range(w - 1))
             sizes = [b - a for a, b in spans]
             assert max(sizes) - min(sizes) <= 1
+
+
+def _cli_worker(rank, world, port, n, fail_at, outdir, q):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import avse_pkg
+    avse_pkg.load()
+    import numpy as np
+    from avse_amd import speech_enhancer as se
+    from avse_amd.audio_io import AudioSignal
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rng = np.random.default_rng(0)
+        samples = []
+        for i in range(n):
+            S = 15 if i % 3 else 10          # two shape groups
+            samples.append(se.Sample("spk%d" % (i % 2), "v%d.npy" % i, "s%d.wav" % i, "n%d.wav" % i,
+                                     rng.normal(size=(S, 4, 4, 5)).astype(np.float32),
+                                     rng.normal(size=(S, 80, 20)).astype(np.float32),
+                                     rng.normal(size=(S, 80, 20)).astype(np.float32), None,
+                                     AudioSignal(rng.normal(size=3200 * S).astype(np.float32), 16000), 25.0))
+        calls = []
+
+        def stand_in(group):                 # duck-typed BatchPredictor: per-sample loss and "signal"
+            calls.append(len(group))
+            if any(g.video_file_path == "v%d.npy" % fail_at for g in group):
+                raise RuntimeError("stand-in failure")
+            return [(float(np.mean((g.mixed_spectrograms - g.speech_spectrograms) ** 2)),
+                     AudioSignal(g.mixed_signal.get_data()[::2] * 0.5, 16000)) for g in group]
+
+        def write(run_dir, smp, signal):
+            with open(os.path.join(run_dir, os.path.basename(smp.video_file_path) + ".%d" % rank), "wb") as fh:
+                fh.write(np.asarray(signal.get_data(), np.float32).tobytes())
+
+        losses = se.predict_samples(samples, stand_in, outdir, world, rank, write=write,
+                                    fallback=lambda smp: stand_in([smp])[0] if smp.video_file_path != "v%d.npy" % fail_at
+                                    else (_ for _ in ()).throw(RuntimeError("stand-in failure")))
+        expect = {i: float(np.mean((s.mixed_spectrograms - s.speech_spectrograms) ** 2)) for i, s in enumerate(samples)}
+        expect[fail_at] = None
+        q.put((rank, losses == expect if rank == 0 else True, calls))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n", [(2, 7), (3, 11)])
+def test_sharded_cli_predict_writes_every_sample_once(world, n, tmp_path):
+    """speech_enhancer.predict_samples under `predict -g N` (gloo here, RCCL on the GPUs): each rank batches its
+    contiguous block of samples per shape group, writes the outputs of the samples it owns, a failing sample is
+    skipped alone (its group retried sample by sample), and rank 0 gathers every loss in sample order."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    fail_at = 3
+    procs = [ctx.Process(target=_cli_worker, args=(r, world, port, n, fail_at, str(tmp_path), q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(ok for _, ok, _ in res), res
+    written = sorted(os.listdir(tmp_path))
+    names = [w.rsplit(".", 1)[0] for w in written]
+    assert sorted(names) == sorted("v%d.npy" % i for i in range(n) if i != fail_at)   # each once, failure skipped
+    assert any(c > 1 for _, _, calls in res for c in calls)                           # groups ran batched

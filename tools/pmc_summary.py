@@ -1,6 +1,7 @@
 """Summarise a tools/profile.sh run into profiles/<tag>_kernel_stats.csv and profiles/<tag>_pmc.json.
 
-Per forward kernel (labelled by its position in the launch sequence) the median over dispatches of:
+Per compute dtype profiled (tools/fwd_loop.py passes: AVSE_F32_SPLIT = "fp32_split", bf16) and per forward kernel
+(labelled by its position in the launch sequence) the median over dispatches of:
   * HBM traffic, corrected as MI355X_MICROARCH.md §HBM prescribes: FETCH_SIZE / WRITE_SIZE are KiB; on gfx950
     FETCH_SIZE reports exactly half the bytes of a wide (16 B/lane) coalesced streaming read, so the read side is
     doubled; WRITE_SIZE is taken as is;
@@ -20,16 +21,18 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # kernel-name prefix -> labels in launch order within one forward
-LABELS = [("k_spec_seg", ["stft"]), ("k_spec640", ["stft"]), ("k_spec_dft", ["stft"]), ("k_aud_enc", ["audio_enc"]), ("k_conv_v1r", ["v_conv1"]),
+LABELS = [("k_spec_seg", ["stft"]), ("k_spec640", ["stft"]), ("k_spec_dft", ["stft"]), ("k_aud_enc", ["audio_enc"]),
+          ("k_conv_v1r", ["v_conv1"]), ("k_conv_v1s", ["v_conv1"]), ("k_splitk_reduce", ["splitk_reduce"]),
           ("k_conv_stream<5,", ["v_conv2"]), ("k_conv_stream<3, 16, 16", ["v_conv3", "v_conv4"]),
           ("k_conv_stream<3, 8, 8", ["v_conv5"]), ("k_gemm<1>", ["v_conv6"]),
           ("k_gemm<0>", ["enc_dense", "dec_dense1", "dec_dense2"]), ("k_dec_head", ["dec_head"]),
           ("k_dec_tail", ["dec_tail"]), ("k_conv<", ["k_conv"]), ("k_istft", ["istft"]), ("k_ola", ["istft_ola"])]
-ALGO_BYTES = {  # algorithmic HBM bytes per launch
-    ("v_conv2", 512): 512 * (64 * 64 * 128 * 2 + 32 * 32 * 128 * 2) + 128 * 3200 * 2,
-    ("stft", 4096): 4096 * (3200 * 4 + 80 * 20 * 4),
-    ("stft", 512): 512 * (3200 * 4 + 80 * 20 * 4),
+ALGO_BYTES = {  # algorithmic HBM bytes per launch: bf16 2 B per value; split pairs 4 B
+    ("bf16", "v_conv2", 512): 512 * (64 * 64 * 128 * 2 + 32 * 32 * 128 * 2) + 128 * 3200 * 2,
+    ("fp32_split", "v_conv2", 512): 512 * (64 * 64 * 128 * 4 + 32 * 32 * 128 * 4) + 128 * 3200 * 4,
+    ("stft", "stft", 4096): 4096 * (3200 * 4 + 80 * 20 * 4),
 }
+DTYPES = ("fp32_split", "bf16")   # tools/profile.sh passes pmc_<tag>_<dtype>_<counter>
 
 
 def short(name):
@@ -81,14 +84,16 @@ def main():
     stats = glob.glob(os.path.join(out, f"prof_{tag}", "**", "*kernel_stats.csv"), recursive=True)
     if stats:
         shutil.copy(stats[0], os.path.join(prof, f"{tag}_kernel_stats.csv"))
-    kern = collections.defaultdict(dict)
-    for batch, (pf, pw, pm) in ((512, ("fetch", "write", "mfma")), (4096, ("sfetch", "swrite", None))):
+    groups = {}
+    passes = [(dt, 512, (f"{dt}_fetch", f"{dt}_write", f"{dt}_mfma")) for dt in DTYPES] + \
+             [("stft", 4096, ("sfetch", "swrite", None))]
+    for dt, batch, (pf, pw, pm) in passes:
+        kern = groups.setdefault(dt, collections.defaultdict(dict))
         fetch = read_pass(os.path.join(out, f"pmc_{tag}_{pf}"))
         write = read_pass(os.path.join(out, f"pmc_{tag}_{pw}"))
         mfma = read_pass(os.path.join(out, f"pmc_{tag}_{pm}")) if pm else {}
         for lab in sorted(set(fetch) | set(write) | set(mfma)):
-            key = lab if batch == 512 else f"{lab}_b{batch}"
-            e = kern[key]
+            e = kern[lab]
             e["batch"] = batch
             f = med([c.get("FETCH_SIZE", 0.0) * 1024 for _, c in fetch.get(lab, [])])
             w = med([c.get("WRITE_SIZE", 0.0) * 1024 for _, c in write.get(lab, [])])
@@ -99,8 +104,8 @@ def main():
                 e["write_bytes"] = w
             if f is not None and w is not None:
                 e["traffic_bytes"] = 2 * f + w
-            if (lab, batch) in ALGO_BYTES:
-                e["algorithmic_bytes"] = ALGO_BYTES[(lab, batch)]
+            if (dt, lab, batch) in ALGO_BYTES:
+                e["algorithmic_bytes"] = ALGO_BYTES[(dt, lab, batch)]
             if lab in mfma:
                 busy = med([c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) for _, c in mfma[lab]])
                 gui = med([c.get("GRBM_GUI_ACTIVE", 0.0) for _, c in mfma[lab]])
@@ -111,22 +116,22 @@ def main():
                     e["eff_clock_ghz"] = round(gui / 8 / dur, 3) if dur else None
             e["dispatches"] = len(fetch.get(lab, []))
     # rocprofv3 --kernel-trace --stats averages of the same tree (the bench's HIP-event figure is a separate run)
+    # keyed by the full kernel symbol (template arguments tell the dtype variants apart)
     stats_avg_ms = {}
     if stats:
         for r in csv.DictReader(open(stats[0])):
-            k = short(r["Name"])
-            for prefix, labels in LABELS:
-                if k.startswith(prefix) and len(labels) == 1:
-                    stats_avg_ms[labels[0]] = round(float(r["AverageNs"]) / 1e6, 5)
-                    break
+            stats_avg_ms[short(r["Name"])] = round(float(r["AverageNs"]) / 1e6, 5)
     sys.path.insert(0, ROOT)
     import avse_pkg
     avse_pkg.load()
     from avse_amd import _lib
     res = {"tag": tag, "batch": 512, "source_digest": _lib.source_digest(),
-           "kernel_stats_avg_ms": stats_avg_ms, "source": "rocprofv3 --pmc passes FETCH_SIZE | WRITE_SIZE | "
-           "SQ_VALU_MFMA_BUSY_CYCLES+GRBM_GUI_ACTIVE over tools/fwd_loop.py (B=512 bf16 spectrogram + forward) and "
-           "FETCH_SIZE | WRITE_SIZE over AVSE_MODE=stft (B=4096, 5 rotated buffer sets)", "kernels": kern}
+           "source": "rocprofv3 --kernel-trace --stats of `bench.py --steps 20` (kernel_stats_avg_ms, by kernel "
+           "symbol); --pmc passes FETCH_SIZE | WRITE_SIZE | SQ_VALU_MFMA_BUSY_CYCLES+GRBM_GUI_ACTIVE over "
+           "tools/fwd_loop.py (B=512 spectrogram + forward, AVSE_DTYPE per dtype) and FETCH_SIZE | WRITE_SIZE over "
+           "AVSE_MODE=stft (B=4096, 5 rotated buffer sets)",
+           "dtypes": {dt: {"kernels": groups.get(dt, {}), "kernel_stats_avg_ms": stats_avg_ms} for dt in DTYPES},
+           "stft_b4096": groups.get("stft", {})}
     with open(os.path.join(prof, f"{tag}_pmc.json"), "w") as fh:
         json.dump(res, fh, indent=1)
     print(json.dumps(res)[:3000])
