@@ -7,6 +7,7 @@
 typedef __bf16 bf16_t;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 
@@ -212,6 +213,9 @@ struct ConvArgs {
 // is added to the running sum in slab order.  A split-K whose every split is exactly one such block, reduced in split
 // order, therefore reproduces the unsplit sums bit for bit (train.hip train_split).
 constexpr int kFp32Block = 8;
+// launch_conv dtype: 0 fp32 (exact-fp32 MFMA), 1 bf16, kConvSplit fp32 storage with split-f16 products (the generic
+// layers of AVSE_F32_SPLIT: weights packed [Cout][kpad] with each 16-k slab row [Bh(16) | Bl(16)] f16)
+constexpr int kConvSplit = 2;
 int launch_conv(const ConvArgs& a, int dtype, hipStream_t s);
 
 // fused decoder tail d_deconv4 -> d_deconv5 -> d_deconv6, one workgroup per clip (conv_dec.hip, bf16)

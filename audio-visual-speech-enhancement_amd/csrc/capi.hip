@@ -614,12 +614,41 @@ int build_layer(avse_weights* W, int li, const float* kernel, const float* bias,
         }
     }
     int rc;
-    const bool split = W->dtype == AVSE_F32_SPLIT;   // generic layers of the split dtype run the fp32 packing
+    const bool split = W->dtype == AVSE_F32_SPLIT;
+    std::vector<float> scale_g = scale;   // the generic kernel's epilogue scale (split: with the weight exponents undone)
     if (W->dtype == AVSE_BF16) {
         std::vector<uint16_t> pb(packed.size());
         for (size_t i = 0; i < packed.size(); ++i) pb[i] = f2bf(packed[i]);
         uint16_t* d;
         if ((rc = upload(W, pb, &d))) return rc;
+        G.w = d;
+    } else if (split) {
+        // conv.hip k_conv<float, .., S16>: each 16-k slab row of [Cout][kpad] becomes [Bh(16) | Bl(16)] f16 (the same
+        // bytes), output channel n scaled by 2^e_n (max |w| 2^e_n in [2^14, 2^15), as the video layers' packing)
+        std::vector<int> ex(L.cout, 0);
+        for (int n = 0; n < L.cout; ++n) {
+            float mx = 0.f;
+            for (int p = 0; p < G.nphase; ++p)
+                for (int k = 0; k < G.ph[p].kpad; ++k)
+                    mx = std::max(mx, std::fabs(packed[(size_t)G.ph[p].w_off + (size_t)n * G.ph[p].kpad + k]));
+            int e2 = 0;
+            if (mx > 0.f) (void)std::frexp(mx, &e2);
+            ex[n] = mx > 0.f ? 15 - e2 : 0;
+            scale_g[n] = std::ldexp(scale[n], -ex[n]);
+        }
+        std::vector<uint16_t> sp(2 * packed.size(), 0);
+        for (int p = 0; p < G.nphase; ++p)
+            for (int n = 0; n < L.cout; ++n)
+                for (int k = 0; k < G.ph[p].kpad; ++k) {
+                    const size_t src = (size_t)G.ph[p].w_off + (size_t)n * G.ph[p].kpad + k;
+                    const size_t dst = 2 * ((size_t)G.ph[p].w_off + (size_t)n * G.ph[p].kpad) + (size_t)(k / 16) * 32 + k % 16;
+                    const float v = std::ldexp(packed[src], ex[n]);
+                    const uint16_t h = f2h(v);
+                    sp[dst] = h;
+                    sp[dst + 16] = f2h(v - h2f(h));
+                }
+        uint16_t* d;
+        if ((rc = upload(W, sp, &d))) return rc;
         G.w = d;
     } else {
         float* d;
@@ -635,7 +664,7 @@ int build_layer(avse_weights* W, int li, const float* kernel, const float* bias,
         if ((rc = upload(W, dw, &d))) return rc;
         G.w_dense = d;
     }
-    if ((rc = upload(W, scale, &G.scale))) return rc;
+    if ((rc = upload(W, scale_g, &G.scale))) return rc;
     if ((rc = upload(W, shift, &G.shift))) return rc;
     if ((rc = upload(W, taps, &G.taps))) return rc;
     for (size_t t = 0; t < taps.size() && t < (size_t)(MAX_TAPS * MAX_PHASES); ++t) G.htaps[t] = taps[t];
@@ -1174,6 +1203,7 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
     const int dt = W->dtype;
     const bool split = dt == AVSE_F32_SPLIT;               // video convs on split-f16 operands, the rest fp32
     const int gdt = dt == AVSE_BF16 ? AVSE_BF16 : AVSE_F32;   // dtype of the generic kernels' buffers
+    const int cdt = split ? kConvSplit : gdt;                 // launch_conv's arithmetic (split: f16 split products)
     size_t off[B_COUNT + 1];
     arena_bytes(N, dt, c->opt, off, P);
     const long long CAT = P.cat, AEMB = P.aemb, EMB = P.emb;
@@ -1254,7 +1284,7 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
             ConvArgs a = (i < 5) ? conv_args(G, vb(v_in[i]), in_cs, vb(v_in[i + 1]), (long long)G.ho * G.wo * G.def.cout, G.def.cout, 0, n)
                                  : conv_args(G, vb(v_in[i]), in_cs, cat, CAT, G.def.cout, AEMB, n);  // concat[aemb:]
             if (i == 5) ksplit(a);
-            if ((rc = launch_conv(a, gdt, s)) || (rc = mark())) return rc;
+            if ((rc = launch_conv(a, cdt, s)) || (rc = mark())) return rc;
         }
         return 0;
     };
@@ -1347,7 +1377,7 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
         const long long in_cs = (long long)G.def.hin * G.def.win * (i == 0 ? G.cin_pad : G.def.cin);
         ConvArgs a = (i < 4) ? conv_args(G, buf(a_in[i]), in_cs, buf(a_in[i + 1]), (long long)G.ho * G.wo * G.def.cout, G.def.cout, 0, N)
                              : conv_args(G, buf(a_in[i]), in_cs, buf(B_CAT), CAT, G.def.cout, 0, N);   // Flatten -> concat[0:aemb]
-        if ((rc = launch_conv(a, gdt, sa)) || (rc = mark())) return rc;
+        if ((rc = launch_conv(a, cdt, sa)) || (rc = mark())) return rc;
     }
     if (concurrent) AVSE_HIP_CHECK(hipEventRecord(c->join, sa));
     if (video) {
@@ -1368,13 +1398,13 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
     } else {
         ConvArgs a = conv_args(L(11), buf(B_CAT), CAT, buf(B_E1), EMB, EMB, 0, N);
         ksplit(a);
-        if ((rc = launch_conv(a, gdt, s)) || (rc = mark())) return rc;
+        if ((rc = launch_conv(a, cdt, s)) || (rc = mark())) return rc;
         a = conv_args(L(12), buf(B_E1), EMB, buf(B_E2), EMB, EMB, 0, N);
         ksplit(a);
-        if ((rc = launch_conv(a, gdt, s)) || (rc = mark())) return rc;
+        if ((rc = launch_conv(a, cdt, s)) || (rc = mark())) return rc;
         a = conv_args(L(13), buf(B_E2), EMB, buf(B_E3), AEMB, AEMB, 0, N);
         ksplit(a);
-        if ((rc = launch_conv(a, gdt, s)) || (rc = mark())) return rc;
+        if ((rc = launch_conv(a, cdt, s)) || (rc = mark())) return rc;
     }
     // audio decoder (network.py:112-135)
     const int d_in[6] = {B_E3, B_D1, B_D2, B_D3, B_D4, B_D5};
@@ -1429,11 +1459,11 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
             a.fuse_w = W->d6_w;
             a.fuse_bias = W->d6_bias;
             a.fuse_out = out;
-            if ((rc = launch_conv(a, gdt, s)) || (rc = mark())) return rc;
+            if ((rc = launch_conv(a, cdt, s)) || (rc = mark())) return rc;
             continue;
         }
         ConvArgs a = conv_args(G, buf(d_in[i]), in_cs, buf(d_in[i + 1]), (long long)G.ho * G.wo * G.def.cout, G.def.cout, 0, N);
-        if ((rc = launch_conv(a, gdt, s)) || (rc = mark())) return rc;
+        if ((rc = launch_conv(a, cdt, s)) || (rc = mark())) return rc;
     }
     if (opt.unfused_tail) {
         if ((rc = launch_out_conv(buf(B_D5), W->d6_w, W->d6_bias, out, N * kMels * P.T, gdt, s)) || (rc = mark())) return rc;

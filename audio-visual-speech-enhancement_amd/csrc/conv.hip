@@ -72,8 +72,15 @@ template <typename T, int BN, bool FAST> constexpr int conv_occupancy() {
 // K / 4 (one per 16x16x4 MFMA).
 constexpr int FP32_BLOCK = kFp32Block;   // avse_common.h (train.hip's block-exact split-K plans on it)
 
-template <typename T, int BN, bool FAST>
+// S16 (T = float, AVSE_F32_SPLIT's generic layers): fp32 activations in HBM, split-f16 products on the 16-bit matrix
+// cores.  store_slab writes a fp32 A slab row (16 k) as [h(16) | l(16)] f16 (h = f16(x), l = f16(x - h)) — the same
+// 64 bytes — and the host packs each weight slab row as [Bh(16) | Bl(16)] (per-channel power-of-two scaled, the BN
+// scale undoes it).  Per slab two v_mfma_f32_16x16x32_f16 per fragment pair: the B fragment of the first reads the
+// Bh half for every lane (k-group fg & 1), of the second the Bl half, so they sum Ah Bh + Al Bh and Ah Bl + Al Bl
+// (conv_stream.hip's split notes; 4x fewer matrix-core cycles than four 16x16x4 f32 MFMAs per slab).
+template <typename T, int BN, bool FAST, bool S16 = false>
 __global__ __launch_bounds__(256, (conv_occupancy<T, BN, FAST>())) void k_conv(ConvArgs a) {
+    static_assert(!S16 || sizeof(T) == 4, "split operands: fp32 storage");
     constexpr int CH = 16 / sizeof(T);          // elements per 16-byte chunk
     constexpr int SLAB = 64 / sizeof(T);        // elements per 64-byte k-slab
     constexpr int WN = BN / 2;                  // wave tile N
@@ -228,7 +235,21 @@ __global__ __launch_bounds__(256, (conv_occupancy<T, BN, FAST>())) void k_conv(C
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const int row = (tid >> 2) + 64 * h;
-            *reinterpret_cast<i32x4*>(AS(buf) + row * 64 + ((g ^ swz(row)) << 4)) = ra[h];
+            if constexpr (S16) {
+                // floats 4g .. 4g+3 of the row: their h pieces to k-group g >> 1 (half g & 1), l pieces to 2 + (g >> 1)
+                const f32x4 x = __builtin_bit_cast(f32x4, ra[h]);
+                f16x4 hi, lo;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    hi[e] = (_Float16)x[e];
+                    lo[e] = (_Float16)(x[e] - (float)hi[e]);
+                }
+                char* rp = AS(buf) + row * 64 + (g & 1) * 8;
+                *reinterpret_cast<f16x4*>(rp + (((g >> 1) ^ swz(row)) << 4)) = hi;
+                *reinterpret_cast<f16x4*>(rp + (((2 + (g >> 1)) ^ swz(row)) << 4)) = lo;
+            } else {
+                *reinterpret_cast<i32x4*>(AS(buf) + row * 64 + ((g ^ swz(row)) << 4)) = ra[h];
+            }
         }
 #pragma unroll
         for (int h = 0; h < BCH; ++h) {
@@ -258,7 +279,7 @@ __global__ __launch_bounds__(256, (conv_occupancy<T, BN, FAST>())) void k_conv(C
         constexpr int q = decltype(qidx)::value;           // (s - s_begin) % P
         constexpr int qn = (q + 1) % P;
         const int buf = FAST ? q : (s - s_begin) & 1;      // FAST: three buffers, slab x in buffer (x - s_begin) % 3
-        i32x4 fa[NI], fb[NJ];
+        i32x4 fa[NI], fb[NJ], fl[NJ];
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
             const int row = wm * 64 + 16 * i + fr;
@@ -267,13 +288,19 @@ __global__ __launch_bounds__(256, (conv_occupancy<T, BN, FAST>())) void k_conv(C
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
             const int row = wn * WN + 16 * j + fr;
-            fb[j] = *reinterpret_cast<const i32x4*>(BS(buf) + row * 64 + ((fg ^ swz(row)) << 4));
+            fb[j] = *reinterpret_cast<const i32x4*>(BS(buf) + row * 64 + (((S16 ? (fg & 1) : fg) ^ swz(row)) << 4));
+            if constexpr (S16) fl[j] = *reinterpret_cast<const i32x4*>(BS(buf) + row * 64 + (((2 + (fg & 1)) ^ swz(row)) << 4));
         }
 #pragma unroll
         for (int i = 0; i < NI; ++i)
 #pragma unroll
             for (int j = 0; j < NJ; ++j) {
-                if constexpr (sizeof(T) == 2) {
+                if constexpr (S16) {
+                    part[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
+                        __builtin_bit_cast(f16x8, fa[i]), __builtin_bit_cast(f16x8, fb[j]), part[i][j], 0, 0, 0);
+                    part[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
+                        __builtin_bit_cast(f16x8, fa[i]), __builtin_bit_cast(f16x8, fl[j]), part[i][j], 0, 0, 0);
+                } else if constexpr (sizeof(T) == 2) {
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
                         __builtin_bit_cast(bf16x8, fa[i]), __builtin_bit_cast(bf16x8, fb[j]), acc[i][j], 0, 0, 0);
                 } else {
@@ -595,7 +622,15 @@ int launch_conv(const ConvArgs& a, int dtype, hipStream_t s) {
         }
     dim3 grid((M + BM - 1) / BM, (a.Co + BN - 1) / BN, a.nphase * a.ksplit);
     const bool fast = a.Ci % (dtype == 1 ? 32 : 16) == 0;   // else the per-slab tap decode (a_conv1, v_conv1)
-    if (dtype == 1) {
+    if (dtype == kConvSplit) {
+        if (fast) {
+            if (BN == 64) hipLaunchKernelGGL((k_conv<float, 64, true, true>), grid, dim3(256), 0, s, a);
+            else hipLaunchKernelGGL((k_conv<float, 128, true, true>), grid, dim3(256), 0, s, a);
+        } else {
+            if (BN == 64) hipLaunchKernelGGL((k_conv<float, 64, false, true>), grid, dim3(256), 0, s, a);
+            else hipLaunchKernelGGL((k_conv<float, 128, false, true>), grid, dim3(256), 0, s, a);
+        }
+    } else if (dtype == 1) {
         if (fast) {
             if (BN == 64) hipLaunchKernelGGL((k_conv<bf16_t, 64, true>), grid, dim3(256), 0, s, a);
             else hipLaunchKernelGGL((k_conv<bf16_t, 128, true>), grid, dim3(256), 0, s, a);
