@@ -47,8 +47,11 @@ enum avse_status {
  *   AVSE_F32_SPLIT  float32 accuracy on the 16-bit matrix cores: the video convolutions v_conv1..v_conv5 carry every
  *                   fp32 operand as an f16 pair x = h + l (h = f16(x), l = f16(x - h); weights scaled per output
  *                   channel by a power of two) and form all four products h h, h l, l h, l l with
- *                   v_mfma_f32_16x16x32_f16, each MFMA rounding its 32 exact products once into the fp32 accumulator —
- *                   measured MORE accurate than AVSE_F32 (tools/split_probe.hip); the other layers run as AVSE_F32.
+ *                   v_mfma_f32_16x16x32_f16, each MFMA rounding its 32 exact products once into the fp32 accumulator
+ *                   (a K = 3200 dot product: more accurate than exact-fp32 MFMA, tools/split_probe.hip); the other
+ *                   layers the same on k_conv.  Activations pass between the split video layers as the pairs (about
+ *                   22 significant bits): whole-network error measured 1.3x AVSE_F32's (6.9e-5 vs 5.1e-5 absolute RMS
+ *                   on dB-scale outputs, tests/test_gpu_split.py), inside the north star's 1e-4.
  *                   Activations of these layers must stay below 65504 in magnitude (f16 range; BatchNormalization
  *                   keeps a trained network's far below). */
 enum avse_dtype { AVSE_F32 = 0, AVSE_BF16 = 1, AVSE_F32_SPLIT = 2 };

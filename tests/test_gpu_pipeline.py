@@ -2,8 +2,9 @@
 K6 against the oracle pipeline (librosa restatement preprocess -> float64 Keras-semantics forward -> librosa
 restatement reconstruct_speech_signal, i.e. speech_enhancer.py:61-88 per sample).
 
-Tolerance: fp32 weights — the enhanced waveform within relative RMS 1e-4 of the oracle (the ISTFT's own bound,
-DESIGN.md "Parity"); bf16 — relative RMS of the predicted mel-dB slices within the bf16 forward bound (3e-2).
+Tolerance: fp32 and fp32-split weights — the enhanced waveform within relative RMS 1e-4 of the oracle (the ISTFT's
+own bound, DESIGN.md "Parity"); bf16 — the predicted mel-dB slices within the few-clip bf16 forward bound
+(test_gpu_forward.BF16_REL, 1.5e-2) and the waveform within WAVE_BF16 (~2x the measured error, profiles/*_gputest.log).
 """
 import numpy as np
 import pytest
@@ -30,7 +31,11 @@ def oracle_enhance(model, x, video, mean, std):
     return R.reconstruct_speech_signal(x, 16000, pred.astype(np.float32), 25.0), pred
 
 
-@pytest.mark.parametrize("dtype,n_samples", [("float32", 48000), ("float32", 47000), ("bfloat16", 48000)])
+WAVE_BF16 = 3e-2
+
+
+@pytest.mark.parametrize("dtype,n_samples", [("float32", 48000), ("float32", 47000), ("float32_split", 48000),
+                                             ("bfloat16", 48000)])
 def test_enhancer_matches_oracle_pipeline(gpu, dtype, n_samples):
     from avse_amd import ops
     from avse_amd.model import KerasModel
@@ -47,12 +52,24 @@ def test_enhancer_matches_oracle_pipeline(gpu, dtype, n_samples):
     got = got.cpu().numpy()
     assert got.shape == (U, 160 * (S * 20 - 1))
     assert set(timings) == {"stft_ms", "forward_ms", "istft_ms"}
+    # the predicted slices of the same launch geometry (spectrogram + chunked forward), for the mel-dB bound
+    sig = torch.nn.functional.pad(ops.to_device(x), (0, max(0, 3200 * S - n_samples)))[:, :3200 * S].contiguous()
+    mel = ops.spectrogram(sig, frames_per_slice=20).view(U * S, 80, 20)
+    pred = torch.empty_like(mel)
+    frames = ops.to_device(video).view(U * S, 128, 128, 5)
+    for a in range(0, U * S, 16):
+        ops.forward(enh.weights, mel[a:a + 16], frames[a:a + 16], ops.to_device(mean), ops.to_device(std),
+                    out=pred[a:a + 16])
+    pred = pred.view(U, S, 80, 20).cpu().numpy()
     for u in range(U):
         xu = R.fit_length(x[u], 3200 * S)
-        ref, _ = oracle_enhance(model, xu, video[u], mean, std)
-        err = rel_rms(got[u], ref)
-        print(f"{dtype} utterance {u}: waveform rel RMS {err:.3e}")
-        assert err <= (1e-4 if dtype == "float32" else 3e-2), (u, err)
+        ref, ref_pred = oracle_enhance(model, xu, video[u], mean, std)
+        err, perr = rel_rms(got[u], ref), rel_rms(pred[u], ref_pred)
+        print(f"{dtype} utterance {u}: waveform rel RMS {err:.3e}, predicted mel-dB rel RMS {perr:.3e}")
+        if dtype == "bfloat16":
+            assert perr <= 1.5e-2 and err <= WAVE_BF16, (u, perr, err)
+        else:
+            assert err <= 1e-4 and perr <= 1e-5, (u, err, perr)
 
 
 def test_enhancer_rejects_mismatched_geometry(gpu):
