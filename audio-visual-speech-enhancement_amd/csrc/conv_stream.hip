@@ -93,11 +93,11 @@ struct StreamGeom {
     // during step j (loaded WD = LAT + BP + 1 steps ahead) into a ring of NWS = 2 BP weight slots: the slot
     // it overwrites held slice j + 1 - BP, whose fragments the compute waves read during step j - BP, before
     // the previous barrier; 3 halo chunk slots
-    // S16 (split-f16 operands): the compute waves read slice t's lo weights during step t as well, so the ring
-    // has a third slot (the loader's slot (j + 2) % 3 was last read during step j - 1)
-    static constexpr int LAT = LAT_, BP = BP_, NWS = S16_ ? 3 : 2 * BP, WD = LAT + BP + 1, NHS = 3, PAIR = 2 * NTAP;
+    // S16 (split-f16 operands): slice pairs (2p, 2p+1) per barrier (BP 2); the compute waves read the weights of
+    // slices 2p, 2p+1 and 2p+2 during period p while the loader stores 2p+3 and 2p+4: a ring of five slots
+    static constexpr int LAT = LAT_, BP = BP_, NWS = S16_ ? 5 : 2 * BP, WD = LAT + BP + 1, NHS = 3, PAIR = 2 * NTAP;
     static_assert(BP == 1 || BP == 2, "barrier period");
-    static_assert(!S16_ || BP == 1, "split-f16 operands: one step per barrier");
+    static_assert(!S16_ || BP == 2, "split-f16 operands: one slice pair per barrier");
     static constexpr int LDS = NHS * CSLOT + NWS * WSLOT;
     static_assert(LDS + 1024 <= 160 * 1024, "LDS");   // one workgroup per CU: ~250 VGPRs x 8 waves fill the register file
     static_assert(NCLIP * TH * TW == 256, "tile = 256 conv pixels (4 waves x 4 fragments)");
@@ -128,11 +128,15 @@ struct StreamGeom {
 // S16: fp32-accurate split-f16 operands (DESIGN.md §3 "split-f16").  Every fp32 value x is carried as the f16 pair
 // (h, l) = (f16(x), f16(x - h)); the input activation holds, per pixel and per 16 channels, 32 f16 = [h(16) | l(16)]
 // (a "chunk" of 32 halves is then 16 real channels), the weight row of output channel co per slice 32 f16 =
-// [Bh(16) | Bl(16)] of the same 16 channels (scaled by a per-channel power of two folded into the BN scale).  A step
-// issues two groups of 32 v_mfma_f32_16x16x32_f16: lanes of k-groups 0, 1 hold Ah, of 2, 3 Al; the B fragment of
-// group 1 reads the Bh half for every lane (k-group kg & 1), of group 2 the Bl half (2 + (kg & 1)), so the two
-// groups sum Ah Bh + Al Bh and Ah Bl + Al Bl: all four products of (Ah + Al)(Bh + Bl), each 32-product MFMA rounded
-// once into the fp32 accumulator (tools/split_probe.hip: more accurate than exact-fp32 MFMA at K = 3200).
+// [Bh(16) | Bl(16)] of the same 16 channels (scaled by a per-channel power of two folded into the BN scale).  The
+// compute waves take two slices t, t+1 per barrier in three groups of 32 v_mfma_f32_16x16x32_f16 (each MFMA rounds
+// its 32 exact products once into the fp32 accumulator):
+//   1. A(t) = [Ah | Al] x the Bh half read for every lane (k-group kg & 1)        -> Ah Bh + Al Bh of slice t
+//   2. the same for slice t+1
+//   3. A' = [Ah(t) | Ah(t+1)] (v_permlane32_swap of the two A fragments: lanes 32..63 take the other slice's Ah) x
+//      B' = [Bl(t) | Bl(t+1)] (lanes of k-groups 0, 1 read slice t's Bl half, 2, 3 slice t+1's) -> Ah Bl of both
+// i.e. three of the four products of (Ah + Al)(Bh + Bl) — Al Bl (2^-22 of |a b|, below the pieces' representation
+// error) is dropped — on 3/4 of the MFMAs of the four-product form.
 template <int KS, int TH, int TW, int NCLIP, bool M16 = true, int LAT_ = StreamGeom<KS, TH, TW, NCLIP>::LAT, int ABL = 0,
           int BP_ = 1, bool S16 = false>
 __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
@@ -354,15 +358,6 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
     }
 
     // =============================== compute waves ===============================
-    // S16 read spacing (MFMAs per fragment read): group 1's 8 Bl reads, group 2's 12 next-slice reads
-#ifndef AVSE_S16_SG1
-#define AVSE_S16_SG1 4
-#endif
-#ifndef AVSE_S16_SG2
-#define AVSE_S16_SG2 2
-#endif
-    constexpr int SG1 = AVSE_S16_SG1, SG2 = AVSE_S16_SG2;
-    static_assert(8 * SG1 <= 32 && 12 * SG2 <= 32, "read spacing");
     // the MFMA stream gets issue priority over the co-resident loader wave of its SIMD (-2% time)
     __builtin_amdgcn_s_setprio(2);
     if constexpr (M16) {
@@ -478,43 +473,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
 
         // bar: the step closes a BP-step group (t % BP == BP - 1; t is even on the first call of each pair)
         auto cstep = [&](auto bar, int t, i32x4 (&ca)[4], i32x4 (&cb)[8], i32x4 (&xa)[4], i32x4 (&xb)[8]) {
-            if constexpr (S16) {
-                // column-block-outer MFMA order: B fragment j is dead after its 4 MFMAs, so the fragment read
-                // issued behind them can take its registers (the step holds ~24 live fragments, as bf16 does)
-                // group 1: Ah Bh + Al Bh, while this slice's Bl fragments (weight slot t % 3) are read
-                i32x4 cl[8];
-                if constexpr (!(ABL & 8)) frags_lo(t % NWS, cl);
-                if constexpr (!(ABL & 16))
-#pragma unroll
-                    for (int j = 0; j < 8; ++j)
-#pragma unroll
-                        for (int i = 0; i < 4; ++i)
-                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
-                                __builtin_bit_cast(f16x8, ca[i]), __builtin_bit_cast(f16x8, cb[j]), acc[i][j], 0, 0, 0);
-#pragma unroll
-                for (int r = 0; r < 8; ++r) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, SG1, 0);   // MFMA
-                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);     // DS read
-                }
-                __builtin_amdgcn_sched_group_barrier(0x008, 32 - 8 * SG1, 0);
-                __builtin_amdgcn_sched_barrier(0);
-                // group 2: Ah Bl + Al Bl, while the next slice's A and Bh fragments are read
-                if constexpr (!(ABL & 8)) frags(hs1, tap1, (t + 1) % NWS, xa, xb);
-                if constexpr (!(ABL & 16))
-#pragma unroll
-                    for (int j = 0; j < 8; ++j)
-#pragma unroll
-                        for (int i = 0; i < 4; ++i)
-                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
-                                __builtin_bit_cast(f16x8, ca[i]), __builtin_bit_cast(f16x8, cl[j]), acc[i][j], 0, 0, 0);
-#pragma unroll
-                for (int r = 0; r < 12; ++r) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, SG2, 0);   // MFMA
-                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);     // DS read
-                }
-                __builtin_amdgcn_sched_group_barrier(0x008, 32 - 12 * SG2, 0);
-                __builtin_amdgcn_sched_barrier(0);
-            } else {
+            if constexpr (!S16) {   // (split-f16 operands run pstep below)
                 if constexpr (!(ABL & 8)) frags(hs1, tap1, (t + 1) & (NWS - 1), xa, xb);
                 if constexpr (!(ABL & 16))
 #pragma unroll
@@ -558,13 +517,85 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
         };
         int t = 0;
         int cur_clip0, cur_oy0, cur_ox0;
-        for (int kt = 0; kt < nmine; ++kt) {
-            for (int s = 0; s < spt; s += 2, t += 2) {
-                cstep(std::bool_constant<BP == 1>{}, t, fa, fb, na, nb);
-                cstep(std::true_type{}, t + 1, na, nb, fa, fb);
+        if constexpr (S16) {
+            auto advance = [&]() {
+                if (++tap1 == NTAP) {
+                    tap1 = 0;
+                    hs1 = hs1 == 2 ? 0 : hs1 + 1;
+                }
+            };
+            auto mfma_group = [&](const i32x4 (&ca)[4], const i32x4 (&cb)[8]) {
+                if constexpr (!(ABL & 16))
+#pragma unroll
+                    for (int j = 0; j < 8; ++j)
+#pragma unroll
+                        for (int i = 0; i < 4; ++i)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
+                                __builtin_bit_cast(f16x8, ca[i]), __builtin_bit_cast(f16x8, cb[j]), acc[i][j], 0, 0, 0);
+            };
+            auto sched = [](auto nds, auto per) {
+                constexpr int ND = decltype(nds)::value, PER = decltype(per)::value;
+#pragma unroll
+                for (int r = 0; r < ND; ++r) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, PER, 0);   // MFMA
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);     // DS read
+                }
+                __builtin_amdgcn_sched_group_barrier(0x008, 32 - ND * PER, 0);
+                __builtin_amdgcn_sched_barrier(0);
+            };
+            const bool hi_half = kg >= 2;   // group 3's B': lanes of k-groups 2, 3 read slice t+1's Bl half
+            // slices t, t+1 with (a0, b0) = A(t), Bh(t) in registers; reads A(t+2), Bh(t+2) into (na, nb)
+            auto pstep = [&](int t, i32x4 (&a0)[4], i32x4 (&b0)[8], i32x4 (&na)[4], i32x4 (&nb)[8]) {
+                i32x4 a1[4], b1[8], bp[8];
+                const int ws0 = t % NWS, ws1 = (t + 1) % NWS, ws2 = (t + 2) % NWS;
+                if constexpr (!(ABL & 8)) frags(hs1, tap1, ws1, a1, b1);
+                advance();
+                mfma_group(a0, b0);
+                sched(std::integral_constant<int, 12>{}, std::integral_constant<int, 1>{});
+                if constexpr (!(ABL & 8)) frags_lo(hi_half ? ws1 : ws0, bp);
+                mfma_group(a1, b1);
+                sched(std::integral_constant<int, 8>{}, std::integral_constant<int, 2>{});
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int d = 0; d < 4; ++d)
+                        a0[i][d] = (int)__builtin_amdgcn_permlane32_swap((unsigned)a0[i][d], (unsigned)a1[i][d], false,
+                                                                         false)[0];
+                if constexpr (!(ABL & 8)) frags(hs1, tap1, ws2, na, nb);
+                advance();
+                mfma_group(a0, bp);
+                sched(std::integral_constant<int, 12>{}, std::integral_constant<int, 1>{});
+                if constexpr (!(ABL & 4)) {
+                    if constexpr ((ABL & 128) != 0) pt0 = __builtin_amdgcn_s_memtime();
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    if constexpr ((ABL & 128) != 0) pt1 = __builtin_amdgcn_s_memtime();
+                    barrier_raw();
+                    if constexpr ((ABL & 128) != 0) {
+                        const unsigned long long pt2 = __builtin_amdgcn_s_memtime();
+                        p_work += pt0 - ptp;
+                        p_wait += pt1 - pt0;
+                        p_bar += pt2 - pt1;
+                        ptp = pt2;
+                    }
+                }
+            };
+            for (int kt = 0; kt < nmine; ++kt) {
+                for (int s = 0; s < spt; s += 4, t += 4) {   // spt % 4 == 0 (launch_stream)
+                    pstep(t, fa, fb, na, nb);
+                    pstep(t + 2, na, nb, fa, fb);
+                }
+                tile_origin(kt, cur_clip0, cur_oy0, cur_ox0);
+                epilogue(cur_clip0, cur_oy0, cur_ox0);
             }
-            tile_origin(kt, cur_clip0, cur_oy0, cur_ox0);
-            epilogue(cur_clip0, cur_oy0, cur_ox0);
+        } else {
+            for (int kt = 0; kt < nmine; ++kt) {
+                for (int s = 0; s < spt; s += 2, t += 2) {
+                    cstep(std::bool_constant<BP == 1>{}, t, fa, fb, na, nb);
+                    cstep(std::true_type{}, t + 1, na, nb, fa, fb);
+                }
+                tile_origin(kt, cur_clip0, cur_oy0, cur_ox0);
+                epilogue(cur_clip0, cur_oy0, cur_ox0);
+            }
         }
         if constexpr ((ABL & 128) != 0)
             if (lane == 0) {
@@ -724,8 +755,9 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
 
 template <int KS, int TH, int TW, int NCLIP, bool M16, bool S16 = false>
 int launch_stream(const HaloArgs& a, hipStream_t s) {
-    using G = StreamGeom<KS, TH, TW, NCLIP, StreamGeom<KS, TH, TW, NCLIP>::LAT, 1, S16>;
-    constexpr auto kern = k_conv_stream<KS, TH, TW, NCLIP, M16, G::LAT, 0, 1, S16>;
+    constexpr int BP = S16 ? 2 : 1;
+    using G = StreamGeom<KS, TH, TW, NCLIP, StreamGeom<KS, TH, TW, NCLIP>::LAT, BP, S16>;
+    constexpr auto kern = k_conv_stream<KS, TH, TW, NCLIP, M16, G::LAT, 0, BP, S16>;
     if (int rc = ensure_lds_attr((const void*)kern, G::LDS + 1024)) return rc;
     if (a.Hc % TH || a.Wc % TW || a.Co % 128 || a.Ci % 64) {   // an even number of 32-channel chunks
         set_error("stream conv: tile does not divide the layer");
@@ -740,8 +772,8 @@ int launch_stream(const HaloArgs& a, hipStream_t s) {
     int gx = ncu / cob;
     gx = gx >= 8 ? gx / 8 * 8 : (gx < 1 ? 1 : gx);
     if (gx > tiles) gx = tiles;
-    if (S16 && a.out_mode != OUT_S16 && a.out_mode != OUT_F32) {
-        set_error("stream conv: split-f16 operands write split or f32 outputs");
+    if (S16 && ((a.out_mode != OUT_S16 && a.out_mode != OUT_F32) || (a.Ci / 32 * KS * KS) % 4)) {
+        set_error("stream conv: split-f16 operands write split or f32 outputs, over slice counts divisible by 4");
         return 3;
     }
     hipLaunchKernelGGL(kern, dim3(gx, cob), dim3(512), G::LDS + 1024, s, a);

@@ -338,9 +338,9 @@ __global__ __launch_bounds__(512, 1) void k_conv_v1r(HaloArgs a) {
 // k_conv_v1s: v_conv1 with split-f16 operands (AVSE_F32_SPLIT, DESIGN.md §3 "split-f16"), the same row-run K
 // layout.  The normalised window is stored twice — h = f16(x) and l = f16(x - h), 12-byte pixels each — and the
 // weights as Bh / Bl images [piece][kernel row][Co][32] f16 (80 KB, resident; scaled by a per-channel power of two
-// that the BN scale undoes).  A K-slice is four groups of 32 v_mfma_f32_16x16x32_f16 (Ah Bh, Ah Bl, Al Bl, Al Bh: all
-// four products, each MFMA rounding its 32 products once into fp32), ordered so that at most 24 fragments are live:
-//   Ah Bh (reading Bl) -> Ah Bl (reading Al) -> Al Bl (reading the next slice's Ah) -> Al Bh (reading its Bh).
+// that the BN scale undoes).  A K-slice is three groups of 32 v_mfma_f32_16x16x32_f16 (Ah Bh, Ah Bl, Al Bh, each MFMA
+// rounding its 32 products once into fp32; Al Bl dropped, see V1S_LL), ordered so that at most 24 fragments are live:
+//   Ah Bh (reading Bl) -> Ah Bl (reading Al, then the next slice's Ah) -> Al Bh (reading the next slice's Bh).
 // With four times the MFMAs per window the compute waves run the epilogue themselves (BN + LeakyReLU on the pooled
 // maxima, split, stores into the next layer's split-pair layout: per pixel and 16 channels [h(16) | l(16)]); the
 // loader waves only stage windows.  Window / barrier protocol as k_conv_v1r (3 slots, window k+2 stored while
@@ -349,6 +349,12 @@ constexpr int HIMG = HSLOT;                                    // one window ima
 constexpr int SSLOT = 2 * HIMG;                                // window slot: h image, l image
 constexpr int WIMG_S = 2 * NSL * 128 * 64;                     // Bh, Bl: 80 KB
 constexpr int LDS_S = WIMG_S + NWS * SSLOT + SSH;
+// the l x l product (2^-22 of |a b|, below the pieces' own representation error) is dropped: three MFMA groups per
+// K-slice instead of four (AVSE_V1S_LL=1 keeps it, for A/B and accuracy checks)
+#ifndef AVSE_V1S_LL
+#define AVSE_V1S_LL 0
+#endif
+constexpr bool V1S_LL = AVSE_V1S_LL != 0;
 static_assert(LDS_S <= 160 * 1024, "LDS (split v_conv1)");
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 
@@ -536,11 +542,15 @@ __global__ __launch_bounds__(512, 1) void k_conv_v1s(HaloArgs a) {
         mfmas(ah, bl, false);
         sched(std::integral_constant<int, 16>{});
         fragA(hsn, 0, kyn, nah);
-        mfmas(al, bl, false);
-        sched(std::integral_constant<int, 16>{});
-        fragB(0, kyn, nbh);
+        if constexpr (V1S_LL) {
+            mfmas(al, bl, false);
+            sched(std::integral_constant<int, 16>{});
+            fragB(0, kyn, nbh);
+        } else {
+            fragB(0, kyn, nbh);
+        }
         mfmas(al, bh, false);
-        sched(std::integral_constant<int, 8>{});
+        sched(std::integral_constant<int, V1S_LL ? 8 : 24>{});
     };
     const int Wp = a.Wc / 2;
     const long long cbytes = a.out_clip_stride * 2;

@@ -52,20 +52,20 @@ FLOP_AUDIO_BRANCH = 2e6 * sum(MMAC.values())     # configs[2]: audio encoder + d
 FLOP_V_CONV2 = 2 * 64 * 64 * 128 * 3200          # dominant kernel: v_conv2 implicit GEMM (M=4096, N=128, K=3200)
 STFT_BYTES_PER_CLIP = SEG * 4 + 80 * 20 * 4      # 12,800 B in + 6,400 B out
 PEAK_TFLOPS = {"bf16": 256 * 4 * 2.4e9 * 1024 / 1e12, "fp32": 256 * 4 * 2.4e9 * 64 / 1e12}   # 2516.6 / 157.3
-# AVSE_F32_SPLIT's video convs issue 4 f16 MFMA products (h h, h l, l h, l l) per fp32 multiply-add: their matrix-core
-# ceiling in fp32 FLOP/s is the dense f16 peak (= bf16's, MI355X_MICROARCH.md) / 4
-PEAK_TFLOPS["fp32_split"] = PEAK_TFLOPS["bf16"] / 4                                           # 629.1
+# AVSE_F32_SPLIT's video convs issue 3 f16 MFMA products (h h, l h, h l; l l dropped) per fp32 multiply-add: their
+# matrix-core ceiling in fp32 FLOP/s is the dense f16 peak (= bf16's, MI355X_MICROARCH.md) / 3
+PEAK_TFLOPS["fp32_split"] = PEAK_TFLOPS["bf16"] / 3                                           # 838.9
 LIB_DTYPE = {"fp32": "float32", "fp32_split": "float32_split", "bf16": "bf16"}
 ARITHMETIC = {
     "fp32": "float32 everywhere: exact-fp32 MFMA (v_mfma_f32_16x16x4_f32), fp32 activations",
     "fp32_split": "float32 inputs / outputs / accumulation; every layer's matrix-core products from f16 pairs x = h + l "
-                  "of each fp32 operand (h = f16(x), l = f16(x - h); weights scaled per channel by a power of two), "
-                  "all four products on v_mfma_f32_16x16x32_f16 (32 exact products rounded once into the fp32 "
-                  "accumulator); activations fp32 between generic layers, (h, l) pairs between the split video "
-                  "convs: include/avse.h AVSE_F32_SPLIT",
+                  "of each fp32 operand (h = f16(x), l = f16(x - h); weights scaled per channel by a power of two) on "
+                  "v_mfma_f32_16x16x32_f16 (32 exact products rounded once into the fp32 accumulator): h h, l h, h l "
+                  "in the video convs (l l, 2^-22 of |a b|, dropped), all four in the other layers; activations fp32 "
+                  "between generic layers, (h, l) pairs between the split video convs: include/avse.h AVSE_F32_SPLIT",
     "bf16": "bf16 activations and weights, fp32 accumulation (reduced precision)"}
 KERNEL_NAME = {"bf16": "k_conv_stream<5, 16, 16, 1, true, 10, 0, 1, false>",
-               "fp32_split": "k_conv_stream<5, 16, 16, 1, true, 10, 0, 1, true>",
+               "fp32_split": "k_conv_stream<5, 16, 16, 1, true, 10, 0, 2, true>",
                "fp32": "k_conv<float, 128, true>"}
 PEAK_HBM_GBS = 8000.0
 
@@ -519,8 +519,8 @@ def main():
     kdesc = {"bf16": "k_conv_stream<5,16,16,1> bf16: persistent warp-specialised implicit GEMM M=4096/clip N=128 "
                      "K=3200, fused BN+LReLU+2x2 maxpool",
              "fp32_split": "k_conv_stream<5,16,16,1,S16>: the persistent warp-specialised implicit GEMM (M=4096/clip "
-                           "N=128 K=3200, fused BN+LReLU+2x2 maxpool) on split-f16 operands, 4 f16 MFMA products per "
-                           "fp32 MAC; peak = dense f16 MFMA peak / 4",
+                           "N=128 K=3200, fused BN+LReLU+2x2 maxpool) on split-f16 operands, 3 f16 MFMA products per "
+                           "fp32 MAC; peak = dense f16 MFMA peak / 3",
              "fp32": "k_conv<float,128> implicit GEMM, exact-fp32 MFMA"}[args.dtype]
     result = {
         "metric": METRIC,

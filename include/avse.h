@@ -44,14 +44,14 @@ enum avse_status {
 /* Compute dtypes of avse_weights_load (inputs, outputs and accumulation are float32 in all three):
  *   AVSE_F32        every layer on exact-fp32 MFMA (v_mfma_f32_16x16x4_f32: a k-ordered fmaf chain)
  *   AVSE_BF16       activations and weights rounded to bf16 (the fast path; ~2e-3 relative output error)
- *   AVSE_F32_SPLIT  float32 accuracy on the 16-bit matrix cores: the video convolutions v_conv1..v_conv5 carry every
- *                   fp32 operand as an f16 pair x = h + l (h = f16(x), l = f16(x - h); weights scaled per output
- *                   channel by a power of two) and form all four products h h, h l, l h, l l with
- *                   v_mfma_f32_16x16x32_f16, each MFMA rounding its 32 exact products once into the fp32 accumulator
- *                   (a K = 3200 dot product: more accurate than exact-fp32 MFMA, tools/split_probe.hip); the other
- *                   layers the same on k_conv.  Activations pass between the split video layers as the pairs (about
- *                   22 significant bits): whole-network error measured 1.3x AVSE_F32's (6.9e-5 vs 5.1e-5 absolute RMS
- *                   on dB-scale outputs, tests/test_gpu_split.py), inside the north star's 1e-4.
+ *   AVSE_F32_SPLIT  float32 accuracy on the 16-bit matrix cores: every layer carries each fp32 operand as an f16 pair
+ *                   x = h + l (h = f16(x), l = f16(x - h); weights scaled per output channel by a power of two) and
+ *                   forms the products with v_mfma_f32_16x16x32_f16, each MFMA rounding its 32 exact products once
+ *                   into the fp32 accumulator (a K = 3200 dot product: more accurate than exact-fp32 MFMA,
+ *                   tools/split_probe.hip): h h, l h, h l in the video convolutions v_conv1..v_conv5 (l l, 2^-22 of
+ *                   |a b|, dropped), all four in the other layers.  Activations pass between the split video layers as
+ *                   the pairs (about 22 significant bits): whole-network error measured 1.3x AVSE_F32's (6.8e-5 vs
+ *                   5.1e-5 absolute RMS on dB-scale outputs, tests/test_gpu_split.py), inside the north star's 1e-4.
  *                   Activations of these layers must stay below 65504 in magnitude (f16 range; BatchNormalization
  *                   keeps a trained network's far below). */
 enum avse_dtype { AVSE_F32 = 0, AVSE_BF16 = 1, AVSE_F32_SPLIT = 2 };

@@ -3,8 +3,8 @@ K6 against the oracle pipeline (librosa restatement preprocess -> float64 Keras-
 restatement reconstruct_speech_signal, i.e. speech_enhancer.py:61-88 per sample).
 
 Tolerance: fp32 and fp32-split weights — the enhanced waveform within relative RMS 1e-4 of the oracle (the ISTFT's
-own bound, DESIGN.md "Parity"); bf16 — the predicted mel-dB slices within the few-clip bf16 forward bound
-(test_gpu_forward.BF16_REL, 1.5e-2) and the waveform within WAVE_BF16 (~2x the measured error, profiles/*_gputest.log).
+own bound, DESIGN.md "Parity"); bf16 — the predicted mel-dB slices within MEL_BF16 and the waveform within WAVE_BF16,
+each ~2x the measured error (profiles/r04a_gputest.log: mel-dB 2.65e-3, waveform 4.3e-5 relative RMS).
 """
 import numpy as np
 import pytest
@@ -31,7 +31,7 @@ def oracle_enhance(model, x, video, mean, std):
     return R.reconstruct_speech_signal(x, 16000, pred.astype(np.float32), 25.0), pred
 
 
-WAVE_BF16 = 3e-2
+MEL_BF16, WAVE_BF16 = 6e-3, 1e-4
 
 
 @pytest.mark.parametrize("dtype,n_samples", [("float32", 48000), ("float32", 47000), ("float32_split", 48000),
@@ -67,7 +67,7 @@ def test_enhancer_matches_oracle_pipeline(gpu, dtype, n_samples):
         err, perr = rel_rms(got[u], ref), rel_rms(pred[u], ref_pred)
         print(f"{dtype} utterance {u}: waveform rel RMS {err:.3e}, predicted mel-dB rel RMS {perr:.3e}")
         if dtype == "bfloat16":
-            assert perr <= 1.5e-2 and err <= WAVE_BF16, (u, perr, err)
+            assert perr <= MEL_BF16 and err <= WAVE_BF16, (u, perr, err)
         else:
             assert err <= 1e-4 and perr <= 1e-5, (u, err, perr)
 
