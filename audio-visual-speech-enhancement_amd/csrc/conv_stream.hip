@@ -93,11 +93,15 @@ struct StreamGeom {
     // during step j (loaded WD = LAT + BP + 1 steps ahead) into a ring of NWS = 2 BP weight slots: the slot
     // it overwrites held slice j + 1 - BP, whose fragments the compute waves read during step j - BP, before
     // the previous barrier; 3 halo chunk slots
-    // S16 (split-f16 operands): slice pairs (2p, 2p+1) per barrier (BP 2); the compute waves read the weights of
-    // slices 2p, 2p+1 and 2p+2 during period p while the loader stores 2p+3 and 2p+4: a ring of five slots
-    static constexpr int LAT = LAT_, BP = BP_, NWS = S16_ ? 5 : 2 * BP, WD = LAT + BP + 1, NHS = 3, PAIR = 2 * NTAP;
-    static_assert(BP == 1 || BP == 2, "barrier period");
-    static_assert(!S16_ || BP == 2, "split-f16 operands: one slice pair per barrier");
+    // S16 (split-f16 operands): BP / 2 slice pairs per barrier; during period p the compute waves read the weights of
+    // slices BP p .. BP p + BP (one past the period: the next pair's first slice) while the loader stores the BP
+    // slices after those: a ring of 2 BP + 1 slots
+    // PAIR: loader steps per unrolled iteration (2 chunks; 4 when a period of 4 steps would not divide 2 chunks)
+    static constexpr int LAT = LAT_, BP = BP_, NWS = S16_ ? 2 * BP + 1 : 2 * BP, WD = LAT + BP + 1, NHS = 3,
+                         PAIR = ((2 * NTAP) % BP ? 4 : 2) * NTAP, CPI = PAIR / NTAP;
+    static_assert(PAIR % BP == 0, "barrier periods align with the unrolled loader iteration");
+    static_assert(BP == 1 || BP == 2 || (S16_ && BP == 4), "barrier period");
+    static_assert(!S16_ || BP % 2 == 0, "split-f16 operands: whole slice pairs per barrier");
     static constexpr int LDS = NHS * CSLOT + NWS * WSLOT;
     static_assert(LDS + 1024 <= 160 * 1024, "LDS");   // one workgroup per CU: ~250 VGPRs x 8 waves fill the register file
     static_assert(NCLIP * TH * TW == 256, "tile = 256 conv pixels (4 waves x 4 fragments)");
@@ -105,7 +109,8 @@ struct StreamGeom {
     // chunk g+2's pieces are loaded at taps 0..HPW-1 of chunk g and written LAT steps later, before
     // the first fragment read of chunk g+2 at step NTAP-1 of chunk g+1
     // (a store is visible after the barrier closing its BP-step group: at most BP - 1 steps later)
-    static_assert(HPW <= NTAP && HPW - 1 + LAT + BP - 1 <= 2 * NTAP - 2, "halo pieces must land in time");
+    // (S16 reads A fragments up to the slice after its period: chunk g+2's first slice is read BP + 1 steps before it)
+    static_assert(HPW <= NTAP && HPW - 1 + LAT + BP - 1 <= 2 * NTAP - (S16_ ? BP + 1 : 2), "halo pieces must land in time");
     // loads issued by step j (tap j % NTAP): two weight chunks + one piece on the first HPW taps
     static constexpr int loads(int j, int abl) {
         const int tap = ((j % NTAP) + NTAP) % NTAP;
@@ -342,7 +347,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
             }
             if constexpr (tap == NTAP - 1) chunk_end();
         };
-        for (int pr = 0; pr < nchunks; pr += 2) {
+        for (int pr = 0; pr < nchunks; pr += G::CPI) {   // nchunks % CPI == 0 (launch_stream)
             [&]<int... J>(std::integer_sequence<int, J...>) {
                 (lstep(std::integral_constant<int, J>{}), ...);
             }(std::make_integer_sequence<int, PAIR>{});
@@ -544,8 +549,9 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
                 __builtin_amdgcn_sched_barrier(0);
             };
             const bool hi_half = kg >= 2;   // group 3's B': lanes of k-groups 2, 3 read slice t+1's Bl half
-            // slices t, t+1 with (a0, b0) = A(t), Bh(t) in registers; reads A(t+2), Bh(t+2) into (na, nb)
-            auto pstep = [&](int t, i32x4 (&a0)[4], i32x4 (&b0)[8], i32x4 (&na)[4], i32x4 (&nb)[8]) {
+            // slices t, t+1 with (a0, b0) = A(t), Bh(t) in registers; reads A(t+2), Bh(t+2) into (na, nb); bar: the
+            // pair closes a BP-slice period
+            auto pstep = [&](auto bar, int t, i32x4 (&a0)[4], i32x4 (&b0)[8], i32x4 (&na)[4], i32x4 (&nb)[8]) {
                 i32x4 a1[4], b1[8], bp[8];
                 const int ws0 = t % NWS, ws1 = (t + 1) % NWS, ws2 = (t + 2) % NWS;
                 if constexpr (!(ABL & 8)) frags(hs1, tap1, ws1, a1, b1);
@@ -565,7 +571,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
                 advance();
                 mfma_group(a0, bp);
                 sched(std::integral_constant<int, 12>{}, std::integral_constant<int, 1>{});
-                if constexpr (!(ABL & 4)) {
+                if constexpr (!(ABL & 4) && decltype(bar)::value) {
                     if constexpr ((ABL & 128) != 0) pt0 = __builtin_amdgcn_s_memtime();
                     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                     if constexpr ((ABL & 128) != 0) pt1 = __builtin_amdgcn_s_memtime();
@@ -581,8 +587,8 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
             };
             for (int kt = 0; kt < nmine; ++kt) {
                 for (int s = 0; s < spt; s += 4, t += 4) {   // spt % 4 == 0 (launch_stream)
-                    pstep(t, fa, fb, na, nb);
-                    pstep(t + 2, na, nb, fa, fb);
+                    pstep(std::bool_constant<BP == 2>{}, t, fa, fb, na, nb);
+                    pstep(std::true_type{}, t + 2, na, nb, fa, fb);
                 }
                 tile_origin(kt, cur_clip0, cur_oy0, cur_ox0);
                 epilogue(cur_clip0, cur_oy0, cur_ox0);
@@ -753,9 +759,14 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
         }
 }
 
+// split-f16 v_conv2 (5x5): two slice pairs per barrier (a 9-slot weight ring fits beside the 3 halo slots); the 3x3
+// layers' halo pieces would not land in time at BP 4 (StreamGeom)
+#ifndef AVSE_S16_BP5
+#define AVSE_S16_BP5 4
+#endif
 template <int KS, int TH, int TW, int NCLIP, bool M16, bool S16 = false>
 int launch_stream(const HaloArgs& a, hipStream_t s) {
-    constexpr int BP = S16 ? 2 : 1;
+    constexpr int BP = S16 ? (KS == 5 ? AVSE_S16_BP5 : 2) : 1;
     using G = StreamGeom<KS, TH, TW, NCLIP, StreamGeom<KS, TH, TW, NCLIP>::LAT, BP, S16>;
     constexpr auto kern = k_conv_stream<KS, TH, TW, NCLIP, M16, G::LAT, 0, BP, S16>;
     if (int rc = ensure_lds_attr((const void*)kern, G::LDS + 1024)) return rc;
@@ -772,7 +783,7 @@ int launch_stream(const HaloArgs& a, hipStream_t s) {
     int gx = ncu / cob;
     gx = gx >= 8 ? gx / 8 * 8 : (gx < 1 ? 1 : gx);
     if (gx > tiles) gx = tiles;
-    if (S16 && ((a.out_mode != OUT_S16 && a.out_mode != OUT_F32) || (a.Ci / 32 * KS * KS) % 4)) {
+    if ((a.Ci / 32) % G::CPI || (S16 && ((a.out_mode != OUT_S16 && a.out_mode != OUT_F32) || (a.Ci / 32 * KS * KS) % 4))) {
         set_error("stream conv: split-f16 operands write split or f32 outputs, over slice counts divisible by 4");
         return 3;
     }
