@@ -759,15 +759,23 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
         }
 }
 
-// split-f16 v_conv2 (5x5): two slice pairs per barrier (a 9-slot weight ring fits beside the 3 halo slots); the 3x3
-// layers' halo pieces would not land in time at BP 4 (StreamGeom)
+// split-f16: two slice pairs per barrier (a 9-slot weight ring fits beside the 3 halo slots; v_conv2 3.64 -> 3.49 ms).
+// The 3x3 layers' halo pieces land in time at BP 4 only with LAT 4 (a split step is ~3x a bf16 step, so 4 steps still
+// cover the load latency): v_conv3 / v_conv4 / v_conv5 0.688 / 0.337 / 0.170 -> 0.665 / 0.324 / 0.165 ms
 #ifndef AVSE_S16_BP5
 #define AVSE_S16_BP5 4
 #endif
+#ifndef AVSE_S16_BP3
+#define AVSE_S16_BP3 4
+#endif
+#ifndef AVSE_S16_LAT3
+#define AVSE_S16_LAT3 4
+#endif
 template <int KS, int TH, int TW, int NCLIP, bool M16, bool S16 = false>
 int launch_stream(const HaloArgs& a, hipStream_t s) {
-    constexpr int BP = S16 ? (KS == 5 ? AVSE_S16_BP5 : 2) : 1;
-    using G = StreamGeom<KS, TH, TW, NCLIP, StreamGeom<KS, TH, TW, NCLIP>::LAT, BP, S16>;
+    constexpr int BP = S16 ? (KS == 5 ? AVSE_S16_BP5 : AVSE_S16_BP3) : 1;
+    constexpr int LAT = (S16 && KS == 3) ? AVSE_S16_LAT3 : StreamGeom<KS, TH, TW, NCLIP>::LAT;
+    using G = StreamGeom<KS, TH, TW, NCLIP, LAT, BP, S16>;
     constexpr auto kern = k_conv_stream<KS, TH, TW, NCLIP, M16, G::LAT, 0, BP, S16>;
     if (int rc = ensure_lds_attr((const void*)kern, G::LDS + 1024)) return rc;
     if (a.Hc % TH || a.Wc % TW || a.Co % 128 || a.Ci % 64) {   // an even number of 32-channel chunks

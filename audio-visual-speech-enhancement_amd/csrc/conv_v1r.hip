@@ -355,6 +355,11 @@ constexpr int LDS_S = WIMG_S + NWS * SSLOT + SSH;
 #define AVSE_V1S_LL 0
 #endif
 constexpr bool V1S_LL = AVSE_V1S_LL != 0;
+// ablation builds only (0 in the library): 1 = no epilogue stores, 2 = loaders skip the window staging, 4 = no MFMAs
+#ifndef AVSE_V1S_ABL
+#define AVSE_V1S_ABL 0
+#endif
+constexpr int V1S_ABL = AVSE_V1S_ABL;
 static_assert(LDS_S <= 160 * 1024, "LDS (split v_conv1)");
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 
@@ -476,7 +481,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_v1s(HaloArgs a) {
         barrier_raw();   // B_-1: weights, BN tail, windows 0 and 1
         auto iter = [&](auto set, int k) {
             if (k + 2 < nmine) {
-                win_store(set, (k + 2) % NWS);   // slot of window k-1, last read during tile k-1
+                if constexpr (!(V1S_ABL & 2)) win_store(set, (k + 2) % NWS);   // slot of window k-1, last read during tile k-1
                 if (k + 4 < nmine) win_load(set, k + 4);
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -512,6 +517,11 @@ __global__ __launch_bounds__(512, 1) void k_conv_v1s(HaloArgs a) {
 
     f32x4 acc[4][8];
     auto mfmas = [&](const i32x4 (&ca)[4], const i32x4 (&cb)[8], bool first) {
+        if constexpr ((V1S_ABL & 4) != 0) {   // keep the fragments live without the matrix work
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc[i][0][0] += __builtin_bit_cast(float, ca[i][0] ^ cb[i][1]);
+            return;
+        }
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -570,6 +580,10 @@ __global__ __launch_bounds__(512, 1) void k_conv_v1s(HaloArgs a) {
                 x = fmaxf(x, LRELU * x);
                 const _Float16 h = (_Float16)x;
                 const _Float16 l = (_Float16)(x - (float)h);
+                if constexpr (V1S_ABL & 1) {
+                    if (x == 12345.f) __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, h), ors, 0, 0, 0);
+                    continue;
+                }
                 __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, h), ors, (pbase + 32 * j) * 2, 0, 0);
                 __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, l), ors, (pbase + 32 * j + 16) * 2, 0, 0);
             }
