@@ -206,6 +206,7 @@ struct ConvArgs {
     const float* fuse_w;
     float fuse_bias;
     float* fuse_out;
+    int out_s16;         // 1: the output in the split pair layout (strides and offset in halves), else T / fp32
     ConvPhase ph[MAX_PHASES];
 };
 
@@ -213,9 +214,10 @@ struct ConvArgs {
 // is added to the running sum in slab order.  A split-K whose every split is exactly one such block, reduced in split
 // order, therefore reproduces the unsplit sums bit for bit (train.hip train_split).
 constexpr int kFp32Block = 8;
-// launch_conv dtype: 0 fp32 (exact-fp32 MFMA), 1 bf16, kConvSplit fp32 storage with split-f16 products (the generic
-// layers of AVSE_F32_SPLIT: weights packed [Cout][kpad] with each 16-k slab row [Bh(16) | Bl(16)] f16)
-constexpr int kConvSplit = 2;
+// launch_conv dtype: 0 fp32 (exact-fp32 MFMA), 1 bf16, kConvSplit fp32 input with split-f16 products (the generic
+// layers of AVSE_F32_SPLIT: weights packed [Cout][kpad] with each 16-k slab row [Bh(16) | Bl(16)] f16),
+// kConvSplitPairs the same on an input already in the split pair layout (Ci, strides, kpad, w_off in halves)
+constexpr int kConvSplit = 2, kConvSplitPairs = 3;
 int launch_conv(const ConvArgs& a, int dtype, hipStream_t s);
 
 // fused decoder tail d_deconv4 -> d_deconv5 -> d_deconv6, one workgroup per clip (conv_dec.hip, bf16)

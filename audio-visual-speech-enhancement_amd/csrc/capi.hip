@@ -1203,7 +1203,28 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
     const int dt = W->dtype;
     const bool split = dt == AVSE_F32_SPLIT;               // video convs on split-f16 operands, the rest fp32
     const int gdt = dt == AVSE_BF16 ? AVSE_BF16 : AVSE_F32;   // dtype of the generic kernels' buffers
-    const int cdt = split ? kConvSplit : gdt;                 // launch_conv's arithmetic (split: f16 split products)
+    // launch_conv's arithmetic.  Split dtype: f16 split products; every generic layer writes its output as split pairs
+    // (the next layer loads them as they are), except d_deconv5 (fused d_deconv6 -> float output, or fp32 unfused); the
+    // layers fed by the fp32 preps (a_conv1, a generic v_conv1) split their fp32 input in the kernel
+    const int cdt = split ? kConvSplit : gdt;
+    auto pairs = [&](ConvArgs& a, bool in_pairs, bool out_pairs) -> int {
+        if (!split) return gdt;
+        if (in_pairs) {
+            a.Ci *= 2;
+            a.in_clip_stride *= 2;
+            for (int p = 0; p < a.nphase; ++p) {
+                a.ph[p].kpad *= 2;
+                a.ph[p].w_off *= 2;
+            }
+        }
+        if (out_pairs) {
+            a.out_s16 = 1;
+            a.out_clip_stride *= 2;
+            a.out_pix_stride *= 2;
+            a.out_c_off *= 2;
+        }
+        return in_pairs ? kConvSplitPairs : kConvSplit;
+    };
     size_t off[B_COUNT + 1];
     arena_bytes(N, dt, c->opt, off, P);
     const long long CAT = P.cat, AEMB = P.aemb, EMB = P.emb;
@@ -1262,14 +1283,13 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
                 if (split) {
                     // split-pair input (2 halves per channel) from the previous split layer; output split pairs for
                     // a next split layer, fp32 for a generic one (weights_load keeps the split layers a prefix)
+                    // every consumer (the next split layer or the generic v_conv6) takes the pair layout
                     h.split = 1;
                     if (G.halo != HALO_V1) h.Ci = 2 * G.def.cin;
-                    const bool next_split = i < 5 && L(6 + i).halo != HALO_NONE;
-                    h.out_mode = next_split ? OUT_S16 : OUT_F32;
-                    if (next_split) {
-                        h.out_clip_stride *= 2;
-                        h.out_pix_stride *= 2;
-                    }
+                    h.out_mode = OUT_S16;
+                    h.out_clip_stride *= 2;
+                    h.out_pix_stride *= 2;
+                    h.out_c_off *= 2;
                 }
                 rc = G.halo == HALO_V1 ? launch_conv_v1r(h, s) : launch_conv_stream(h, s);
                 if (rc || (rc = mark())) return rc;
@@ -1284,7 +1304,8 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
             ConvArgs a = (i < 5) ? conv_args(G, vb(v_in[i]), in_cs, vb(v_in[i + 1]), (long long)G.ho * G.wo * G.def.cout, G.def.cout, 0, n)
                                  : conv_args(G, vb(v_in[i]), in_cs, cat, CAT, G.def.cout, AEMB, n);  // concat[aemb:]
             if (i == 5) ksplit(a);
-            if ((rc = launch_conv(a, cdt, s)) || (rc = mark())) return rc;
+            const int dti = pairs(a, i > 0, true);   // v_conv1 generic: fp32 video-prep input
+            if ((rc = launch_conv(a, split ? dti : cdt, s)) || (rc = mark())) return rc;
         }
         return 0;
     };
@@ -1377,7 +1398,8 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
         const long long in_cs = (long long)G.def.hin * G.def.win * (i == 0 ? G.cin_pad : G.def.cin);
         ConvArgs a = (i < 4) ? conv_args(G, buf(a_in[i]), in_cs, buf(a_in[i + 1]), (long long)G.ho * G.wo * G.def.cout, G.def.cout, 0, N)
                              : conv_args(G, buf(a_in[i]), in_cs, buf(B_CAT), CAT, G.def.cout, 0, N);   // Flatten -> concat[0:aemb]
-        if ((rc = launch_conv(a, cdt, sa)) || (rc = mark())) return rc;
+        const int dti = pairs(a, i > 0, true);   // a_conv1: fp32 audio-prep input
+        if ((rc = launch_conv(a, split ? dti : cdt, sa)) || (rc = mark())) return rc;
     }
     if (concurrent) AVSE_HIP_CHECK(hipEventRecord(c->join, sa));
     if (video) {
@@ -1398,13 +1420,16 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
     } else {
         ConvArgs a = conv_args(L(11), buf(B_CAT), CAT, buf(B_E1), EMB, EMB, 0, N);
         ksplit(a);
-        if ((rc = launch_conv(a, cdt, s)) || (rc = mark())) return rc;
+        int dti = pairs(a, true, true);
+        if ((rc = launch_conv(a, split ? dti : cdt, s)) || (rc = mark())) return rc;
         a = conv_args(L(12), buf(B_E1), EMB, buf(B_E2), EMB, EMB, 0, N);
         ksplit(a);
-        if ((rc = launch_conv(a, cdt, s)) || (rc = mark())) return rc;
+        dti = pairs(a, true, true);
+        if ((rc = launch_conv(a, split ? dti : cdt, s)) || (rc = mark())) return rc;
         a = conv_args(L(13), buf(B_E2), EMB, buf(B_E3), AEMB, AEMB, 0, N);
         ksplit(a);
-        if ((rc = launch_conv(a, cdt, s)) || (rc = mark())) return rc;
+        dti = pairs(a, true, true);
+        if ((rc = launch_conv(a, split ? dti : cdt, s)) || (rc = mark())) return rc;
     }
     // audio decoder (network.py:112-135)
     const int d_in[6] = {B_E3, B_D1, B_D2, B_D3, B_D4, B_D5};
@@ -1459,11 +1484,13 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
             a.fuse_w = W->d6_w;
             a.fuse_bias = W->d6_bias;
             a.fuse_out = out;
-            if ((rc = launch_conv(a, cdt, s)) || (rc = mark())) return rc;
+            const int dti = pairs(a, true, false);
+            if ((rc = launch_conv(a, split ? dti : cdt, s)) || (rc = mark())) return rc;
             continue;
         }
         ConvArgs a = conv_args(G, buf(d_in[i]), in_cs, buf(d_in[i + 1]), (long long)G.ho * G.wo * G.def.cout, G.def.cout, 0, N);
-        if ((rc = launch_conv(a, cdt, s)) || (rc = mark())) return rc;
+        const int dti = pairs(a, true, i < 4 || !opt.unfused_tail);   // an unfused d_deconv5 feeds launch_out_conv fp32
+        if ((rc = launch_conv(a, split ? dti : cdt, s)) || (rc = mark())) return rc;
     }
     if (opt.unfused_tail) {
         if ((rc = launch_out_conv(buf(B_D5), W->d6_w, W->d6_bias, out, N * kMels * P.T, gdt, s)) || (rc = mark())) return rc;

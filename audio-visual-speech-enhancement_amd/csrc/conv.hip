@@ -33,6 +33,7 @@ constexpr float LRELU = 0.3f;
 template <typename T> struct Vec16;
 template <> struct Vec16<bf16_t> { typedef i32x4 type; };
 template <> struct Vec16<float> { typedef i32x4 type; };
+template <> struct Vec16<_Float16> { typedef i32x4 type; };
 
 __device__ __forceinline__ int swz(int row) { return ((row >> 3) & 1) * 3; }
 
@@ -41,6 +42,20 @@ __device__ __forceinline__ float to_f(float v) { return v; }
 template <typename T> __device__ __forceinline__ T from_f(float v);
 template <> __device__ __forceinline__ bf16_t from_f<bf16_t>(float v) { return (bf16_t)v; }
 template <> __device__ __forceinline__ float from_f<float>(float v) { return v; }
+
+// one output value at element rowbase + n of a layer output: OutT (bf16 / fp32), or with a.out_s16 the split pair
+// layout (include/avse.h AVSE_F32_SPLIT: per pixel and 16 channels [h(16) | l(16)] f16; rowbase in halves)
+template <typename OutT>
+__device__ __forceinline__ void store_val(const ConvArgs& a, long long rowbase, int n, float x) {
+    if (a.out_s16) {
+        _Float16* o = reinterpret_cast<_Float16*>(a.out) + rowbase + 32 * (n >> 4) + (n & 15);
+        const _Float16 h = (_Float16)x;
+        o[0] = h;
+        o[16] = (_Float16)(x - (float)h);
+    } else {
+        reinterpret_cast<OutT*>(a.out)[rowbase + n] = from_f<OutT>(x);
+    }
+}
 
 struct RowInfo {
     int cbase;          // byte offset of the row's clip from the block's first clip
@@ -64,23 +79,29 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, lo
 // occupancy: more resident workgroups hide the per-tile load latency of the short-K layers (8-18 slabs per
 // tile for the decoder): 4 per CU for BN = 64 (<= 128 VGPRs, 36 KB LDS), 3 for BN = 128 (<= 168, 48 KB)
 // fp32: one workgroup per CU fewer (the blocked-summation partials below need another 32 / 64 VGPRs)
-template <typename T, int BN, bool FAST> constexpr int conv_occupancy() {
-    return !FAST ? 2 : (BN == 64 ? 4 : 3) - (sizeof(T) == 4 ? 1 : 0);
+template <typename T, int BN, bool FAST, bool S16 = false> constexpr int conv_occupancy() {
+    return !FAST ? 2 : (BN == 64 ? 4 : 3) - (sizeof(T) == 4 || S16 ? 1 : 0);
 }
 // fp32 blocked summation: the K loop accumulates FP32_BLOCK slabs (FP32_BLOCK * 16 products per output) into a
 // zeroed partial that is then added to the running sum, so the running sum takes K / 128 roundings instead of
 // K / 4 (one per 16x16x4 MFMA).
 constexpr int FP32_BLOCK = kFp32Block;   // avse_common.h (train.hip's block-exact split-K plans on it)
 
-// S16 (T = float, AVSE_F32_SPLIT's generic layers): fp32 activations in HBM, split-f16 products on the 16-bit matrix
-// cores.  store_slab writes a fp32 A slab row (16 k) as [h(16) | l(16)] f16 (h = f16(x), l = f16(x - h)) — the same
-// 64 bytes — and the host packs each weight slab row as [Bh(16) | Bl(16)] (per-channel power-of-two scaled, the BN
-// scale undoes it).  Per slab two v_mfma_f32_16x16x32_f16 per fragment pair: the B fragment of the first reads the
-// Bh half for every lane (k-group fg & 1), of the second the Bl half, so they sum Ah Bh + Al Bh and Ah Bl + Al Bl
-// (conv_stream.hip's split notes; 4x fewer matrix-core cycles than four 16x16x4 f32 MFMAs per slab).
+// S16 (AVSE_F32_SPLIT's generic layers): split-f16 products on the 16-bit matrix cores.  The LDS A slab row is
+// [h(16) | l(16)] f16 of 16 real k (h = f16(x), l = f16(x - h)): with T = float (fp32 input: a_conv1, a 6-frame
+// v_conv1) store_slab splits the loaded floats into those 64 bytes; with T = _Float16 the input already holds the pairs
+// in that layout (written by the producing layer's epilogue, a.out_s16) and a slab is copied as is — Ci, strides, kpad
+// and w_off then count halves.  The host packs each weight slab row as [Bh(16) | Bl(16)] (per-channel power-of-two
+// scaled, the BN scale undoes it).  Per slab two v_mfma_f32_16x16x32_f16 per fragment pair: the B fragment of the first
+// reads the Bh half for every lane (k-group fg & 1), of the second the Bl half, so they sum Ah Bh + Al Bh and Ah Bl +
+// Al Bl (conv_stream.hip's split notes; 4x fewer matrix-core cycles than four 16x16x4 f32 MFMAs per slab).  Outputs
+// are fp32 or, with a.out_s16, pairs.
 template <typename T, int BN, bool FAST, bool S16 = false>
-__global__ __launch_bounds__(256, (conv_occupancy<T, BN, FAST>())) void k_conv(ConvArgs a) {
-    static_assert(!S16 || sizeof(T) == 4, "split operands: fp32 storage");
+__global__ __launch_bounds__(256, (conv_occupancy<T, BN, FAST, S16>())) void k_conv(ConvArgs a) {
+    static_assert(!S16 || sizeof(T) == 4 || std::is_same_v<T, _Float16>, "split operands: fp32 or pair storage");
+    static_assert(S16 || !std::is_same_v<T, _Float16>, "f16 storage only as split pairs");
+    constexpr bool PAIRS = S16 && sizeof(T) == 2;   // the input holds split pairs (slab = 32 halves = 16 real k)
+    using OutT = std::conditional_t<S16, float, T>;
     constexpr int CH = 16 / sizeof(T);          // elements per 16-byte chunk
     constexpr int SLAB = 64 / sizeof(T);        // elements per 64-byte k-slab
     constexpr int WN = BN / 2;                  // wave tile N
@@ -235,7 +256,7 @@ __global__ __launch_bounds__(256, (conv_occupancy<T, BN, FAST>())) void k_conv(C
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const int row = (tid >> 2) + 64 * h;
-            if constexpr (S16) {
+            if constexpr (S16 && !PAIRS) {
                 // floats 4g .. 4g+3 of the row: their h pieces to k-group g >> 1 (half g & 1), l pieces to 2 + (g >> 1)
                 const f32x4 x = __builtin_bit_cast(f32x4, ra[h]);
                 f16x4 hi, lo;
@@ -311,7 +332,7 @@ __global__ __launch_bounds__(256, (conv_occupancy<T, BN, FAST>())) void k_conv(C
                         part[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], bv[e], part[i][j], 0, 0, 0);
                 }
             }
-        if constexpr (sizeof(T) == 4) {
+        if constexpr (sizeof(T) == 4 || S16) {
             if (++nblk == FP32_BLOCK) {
                 nblk = 0;
 #pragma unroll
@@ -343,7 +364,7 @@ __global__ __launch_bounds__(256, (conv_occupancy<T, BN, FAST>())) void k_conv(C
 
 #undef AS
 #undef BS
-    if constexpr (sizeof(T) == 4) {
+    if constexpr (sizeof(T) == 4 || S16) {
 #pragma unroll
         for (int i = 0; i < NI; ++i)
 #pragma unroll
@@ -363,7 +384,6 @@ __global__ __launch_bounds__(256, (conv_occupancy<T, BN, FAST>())) void k_conv(C
             for (int j = 0; j < NJ; ++j) part[(i * NJ + j) * 256] = acc[i][j];
         return;
     }
-    T* out = reinterpret_cast<T*>(a.out);
     // output row -> element offset, decomposed once per (fragment, row) instead of per element: the
     // three runtime integer divisions per stored value used to be the floor of every short-K layer
     long long orow[NI][4];
@@ -404,7 +424,7 @@ __global__ __launch_bounds__(256, (conv_occupancy<T, BN, FAST>())) void k_conv(C
                     for (int r = 0; r < 4; ++r) {
                         float x = acc[i][j][r] * esc[j] + esh[j];
                         if (a.act) x = x >= 0.f ? x : LRELU * x;
-                        part[i][r] = fmaf(to_f(from_f<T>(x)), ewf[j], part[i][r]);
+                        part[i][r] = fmaf(S16 ? x : to_f(from_f<OutT>(x)), ewf[j], part[i][r]);
                     }
             }
             // sum over the 16 lanes holding the same rows (lane bits 0..3 = column within a fragment): DPP
@@ -452,14 +472,14 @@ __global__ __launch_bounds__(256, (conv_occupancy<T, BN, FAST>())) void k_conv(C
                 if (orow[i][0] < 0) continue;
                 float x = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
                 if (a.act) x = x >= 0.f ? x : LRELU * x;
-                out[orow[i][0] + n] = from_f<T>(x);
+                store_val<OutT>(a, orow[i][0], n, x);
             } else {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     if (orow[i][r] < 0) continue;
                     float x = v[r];
                     if (a.act) x = x >= 0.f ? x : LRELU * x;
-                    out[orow[i][r] + n] = from_f<T>(x);
+                    store_val<OutT>(a, orow[i][r], n, x);
                 }
             }
         }
@@ -476,7 +496,6 @@ __global__ void k_splitk_reduce_tiles(ConvArgs a) {
     const int mtiles = (M + BM - 1) / BM, tiles = mtiles * ((a.Co + BN - 1) / BN);
     const long long total = (long long)tiles * NIJ * 256;
     const f32x4* part = reinterpret_cast<const f32x4*>(a.partial);
-    T* out = reinterpret_cast<T*>(a.out);
     for (long long u = blockIdx.x * (long long)blockDim.x + threadIdx.x; u < total; u += (long long)gridDim.x * blockDim.x) {
         const int tid = (int)(u & 255), ij = (int)((u >> 8) % NIJ), tile = (int)((u >> 8) / NIJ);
         const int bx = tile % mtiles, by = tile / mtiles, i = ij / NJ, j = ij % NJ;
@@ -492,14 +511,14 @@ __global__ void k_splitk_reduce_tiles(ConvArgs a) {
             if (a.act) x = x >= 0.f ? x : LRELU * x;
             const int p = mb >> 2, pw = a.Wq >> 1, phh = a.Hq >> 1;
             const int clip = p / (phh * pw), rr = p - clip * phh * pw;
-            out[clip * a.out_clip_stride + (long long)rr * a.out_pix_stride + a.out_c_off + n] = from_f<T>(x);
+            store_val<T>(a, clip * a.out_clip_stride + (long long)rr * a.out_pix_stride + a.out_c_off, n, x);
         } else {
             for (int r = 0; r < 4 && mb + r < M; ++r) {
                 float x = acc[r] * sc + sh;
                 if (a.act) x = x >= 0.f ? x : LRELU * x;
                 const int m = mb + r, clip = m / (a.Hq * a.Wq), rr = m - clip * a.Hq * a.Wq;
                 const int oy = (rr / a.Wq) * a.oys, ox = (rr % a.Wq) * a.oxs;
-                out[clip * a.out_clip_stride + (long long)(oy * a.Wo + ox) * a.out_pix_stride + a.out_c_off + n] = from_f<T>(x);
+                store_val<T>(a, clip * a.out_clip_stride + (long long)(oy * a.Wo + ox) * a.out_pix_stride + a.out_c_off, n, x);
             }
         }
     }
@@ -621,8 +640,16 @@ int launch_conv(const ConvArgs& a, int dtype, hipStream_t s) {
             return 3;
         }
     dim3 grid((M + BM - 1) / BM, (a.Co + BN - 1) / BN, a.nphase * a.ksplit);
-    const bool fast = a.Ci % (dtype == 1 ? 32 : 16) == 0;   // else the per-slab tap decode (a_conv1, v_conv1)
-    if (dtype == kConvSplit) {
+    const bool fast = a.Ci % ((dtype == 1 || dtype == kConvSplitPairs) ? 32 : 16) == 0;   // else the per-slab tap decode
+    if (dtype == kConvSplitPairs) {
+        if (fast) {
+            if (BN == 64) hipLaunchKernelGGL((k_conv<_Float16, 64, true, true>), grid, dim3(256), 0, s, a);
+            else hipLaunchKernelGGL((k_conv<_Float16, 128, true, true>), grid, dim3(256), 0, s, a);
+        } else {
+            if (BN == 64) hipLaunchKernelGGL((k_conv<_Float16, 64, false, true>), grid, dim3(256), 0, s, a);
+            else hipLaunchKernelGGL((k_conv<_Float16, 128, false, true>), grid, dim3(256), 0, s, a);
+        }
+    } else if (dtype == kConvSplit) {
         if (fast) {
             if (BN == 64) hipLaunchKernelGGL((k_conv<float, 64, true, true>), grid, dim3(256), 0, s, a);
             else hipLaunchKernelGGL((k_conv<float, 128, true, true>), grid, dim3(256), 0, s, a);

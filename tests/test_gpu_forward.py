@@ -36,8 +36,10 @@ BUF_SHAPES = {"video_in": (128, 128, 8), "audio_in": (80, 20, 8), "a_conv1": (40
               "d_deconv5": (80, 20, 64)}
 
 
-# AVSE_F32_SPLIT: buffers written by one split video layer for the next (v_conv5 feeds the generic v_conv6 in fp32)
-SPLIT_PAIR_BUFS = ("v_conv1", "v_conv2", "v_conv3", "v_conv4")
+# AVSE_F32_SPLIT: buffers in the split pair layout (every layer output that feeds another conv / dense layer; the fp32
+# preps' video_in / audio_in and an unfused d_deconv5 stay fp32)
+SPLIT_PAIR_BUFS = ("a_conv1", "a_conv2", "a_conv3", "a_conv4", "v_conv1", "v_conv2", "v_conv3", "v_conv4", "v_conv5",
+                   "concat", "enc_dense", "dec_dense1", "dec_dense2", "d_deconv1", "d_deconv2", "d_deconv3", "d_deconv4")
 
 
 def make_inputs(N, seed):
