@@ -363,7 +363,13 @@ constexpr int V1S_ABL = AVSE_V1S_ABL;
 static_assert(LDS_S <= 160 * 1024, "LDS (split v_conv1)");
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 
-__global__ __launch_bounds__(512, 1) void k_conv_v1s(HaloArgs a) {
+// CW compute waves + 4 loader waves.  CW = 4: compute wave w owns conv rows 4w .. 4w+3 x all 128 channels (one
+// compute wave per SIMD); CW = 8: rows 4 (w & 3) .. x channels 64 (w >> 2) .. +63 — two compute waves per SIMD, so one
+// wave's MFMAs cover the other's LDS waits (half the accumulators, the A fragments read by both)
+template <int CW>
+__global__ __launch_bounds__(64 * (CW + 4), 1) void k_conv_v1s(HaloArgs a) {
+    static_assert(CW == 4 || CW == 8, "compute waves");
+    constexpr int NJ = 32 / CW;                      // 16-channel column blocks per compute wave
     extern __shared__ __attribute__((aligned(1024))) char lds[];
     char* const wimg = lds;                          // [2 pieces][5 rows][128 co][64 B]
     char* const halo = lds + WIMG_S;                 // [NWS][h image | l image]
@@ -372,7 +378,8 @@ __global__ __launch_bounds__(512, 1) void k_conv_v1s(HaloArgs a) {
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int w = wave & 3;
+    const int w = wave < CW ? (wave & 3) : wave - CW;   // compute: row block; loader: loader index
+    const int cb0 = wave < CW ? (wave >> 2) * NJ : 0;  // compute: first column block
 
     const int tiles_x = a.Wc / TW, tiles_per_clip = tiles_x * (a.Hc / TH);
     const int ntiles = a.N * tiles_per_clip;
@@ -388,7 +395,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_v1s(HaloArgs a) {
         ox0 = (tt % tiles_x) * TW;
     };
 
-    if (wave >= 4) {
+    if (wave >= CW) {
         // =============================== loader waves ===============================
         const int L = w * 64 + lane;
         {
@@ -499,7 +506,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_v1s(HaloArgs a) {
     const int r16 = lane & 15, kg = lane >> 4;
     const int q = r16 >> 2, dy = (r16 >> 1) & 1, dx = r16 & 1;
     const int abase = ((4 * w + 2 * (q >> 1) + dy) * HWP + 2 * (q & 1) + dx) * PB + 16 * kg;
-    const int bbase = r16 * 64 + ((kg ^ wsw(r16)) << 4);   // + piece * 40960 + slice * 8192 + 1024 j
+    const int bbase = r16 * 64 + ((kg ^ wsw(r16)) << 4) + 1024 * cb0;   // + piece * 40960 + slice * 8192 + 1024 j
     auto fragA = [&](int hs, int piece, int ky, i32x4 (&fa)[4]) {
         const char* hp = halo + hs * SSLOT + piece * HIMG + abase + ky * HWP * PB;
 #pragma unroll
@@ -508,15 +515,15 @@ __global__ __launch_bounds__(512, 1) void k_conv_v1s(HaloArgs a) {
             fa[i] = (i32x4){(int)p[0], (int)p[1], (int)p[2], (int)p[3]};
         }
     };
-    auto fragB = [&](int piece, int ky, i32x4 (&fb)[8]) {
+    auto fragB = [&](int piece, int ky, i32x4 (&fb)[NJ]) {
         const char* wp = wimg + piece * (NSL * 8192) + ky * 8192 + bbase;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) fb[j] = *reinterpret_cast<const i32x4*>(wp + 1024 * j);
+        for (int j = 0; j < NJ; ++j) fb[j] = *reinterpret_cast<const i32x4*>(wp + 1024 * j);
     };
     barrier_raw();   // B_-1
 
-    f32x4 acc[4][8];
-    auto mfmas = [&](const i32x4 (&ca)[4], const i32x4 (&cb)[8], bool first) {
+    f32x4 acc[4][NJ];
+    auto mfmas = [&](const i32x4 (&ca)[4], const i32x4 (&cb)[NJ], bool first) {
         if constexpr ((V1S_ABL & 4) != 0) {   // keep the fragments live without the matrix work
 #pragma unroll
             for (int i = 0; i < 4; ++i) acc[i][0][0] += __builtin_bit_cast(float, ca[i][0] ^ cb[i][1]);
@@ -525,29 +532,31 @@ __global__ __launch_bounds__(512, 1) void k_conv_v1s(HaloArgs a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int j = 0; j < 8; ++j)
+            for (int j = 0; j < NJ; ++j)
                 acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, ca[i]),
                                                                     __builtin_bit_cast(f16x8, cb[j]),
                                                                     first ? (f32x4){0.f, 0.f, 0.f, 0.f} : acc[i][j], 0, 0, 0);
     };
+    // a group of 4 NJ MFMAs with ND DS reads spread over it (at most one read per MFMA, the rest after the last)
     auto sched = [](auto nds) {
-        constexpr int ND = decltype(nds)::value;
+        constexpr int ND = decltype(nds)::value, NM = 4 * NJ, P = ND < NM ? ND : NM;
 #pragma unroll
-        for (int r = 0; r < ND; ++r) {
+        for (int r = 0; r < P; ++r) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
             __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
         }
-        __builtin_amdgcn_sched_group_barrier(0x008, 32 - ND, 0);
+        if constexpr (NM > P) __builtin_amdgcn_sched_group_barrier(0x008, NM - P, 0);
+        if constexpr (ND > P) __builtin_amdgcn_sched_group_barrier(0x100, ND - P, 0);
         __builtin_amdgcn_sched_barrier(0);
     };
     // K-slice ky of window slot hs, with (ah, bh) = its Ah / Bh fragments in registers; reads the next slice's
     // (hsn, kyn) Ah / Bh into (nah, nbh)
-    auto slice = [&](int hs, int ky, int hsn, int kyn, i32x4 (&ah)[4], i32x4 (&bh)[8], i32x4 (&nah)[4],
-                     i32x4 (&nbh)[8], bool first) {
-        i32x4 bl[8], al[4];
+    auto slice = [&](int hs, int ky, int hsn, int kyn, i32x4 (&ah)[4], i32x4 (&bh)[NJ], i32x4 (&nah)[4],
+                     i32x4 (&nbh)[NJ], bool first) {
+        i32x4 bl[NJ], al[4];
         fragB(1, ky, bl);
         mfmas(ah, bh, first);
-        sched(std::integral_constant<int, 8>{});
+        sched(std::integral_constant<int, NJ>{});
         fragA(hs, 1, ky, al);
         mfmas(ah, bl, false);
         sched(std::integral_constant<int, 16>{});
@@ -560,7 +569,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_v1s(HaloArgs a) {
             fragB(0, kyn, nbh);
         }
         mfmas(al, bh, false);
-        sched(std::integral_constant<int, V1S_LL ? 8 : 24>{});
+        sched(std::integral_constant<int, V1S_LL ? NJ : 16 + NJ>{});
     };
     const int Wp = a.Wc / 2;
     const long long cbytes = a.out_clip_stride * 2;
@@ -572,11 +581,12 @@ __global__ __launch_bounds__(512, 1) void k_conv_v1s(HaloArgs a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int px = (ox0 >> 1) + 2 * i + (kg & 1);
-            const int pbase = (py * Wp + px) * a.out_pix_stride + a.out_c_off + r16;
+            const int pbase = (py * Wp + px) * a.out_pix_stride + a.out_c_off + 32 * cb0 + r16;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
+            for (int j = 0; j < NJ; ++j) {
                 const float mx = fmaxf(fmaxf(acc[i][j][0], acc[i][j][1]), fmaxf(acc[i][j][2], acc[i][j][3]));
-                float x = fmaf(mx, ssh[16 * j + r16], ssh[128 + 16 * j + r16]);
+                const int co = 16 * (cb0 + j) + r16;
+                float x = fmaf(mx, ssh[co], ssh[128 + co]);
                 x = fmaxf(x, LRELU * x);
                 const _Float16 h = (_Float16)x;
                 const _Float16 l = (_Float16)(x - (float)h);
@@ -589,8 +599,8 @@ __global__ __launch_bounds__(512, 1) void k_conv_v1s(HaloArgs a) {
             }
         }
     };
-    i32x4 fa[4], fb[8], na[4], nb[8];
-    auto tile = [&](int k, i32x4 (&xa)[4], i32x4 (&xb)[8], i32x4 (&ya)[4], i32x4 (&yb)[8]) {
+    i32x4 fa[4], fb[NJ], na[4], nb[NJ];
+    auto tile = [&](int k, i32x4 (&xa)[4], i32x4 (&xb)[NJ], i32x4 (&ya)[4], i32x4 (&yb)[NJ]) {
         const int hs = k % NWS, hn = (k + 1) % NWS;
         slice(hs, 0, hs, 1, xa, xb, ya, yb, true);
         slice(hs, 1, hs, 2, ya, yb, xa, xb, false);
@@ -613,9 +623,13 @@ __global__ __launch_bounds__(512, 1) void k_conv_v1s(HaloArgs a) {
 
 }  // namespace
 
+#ifndef AVSE_V1S_CW
+#define AVSE_V1S_CW 8
+#endif
 int launch_conv_v1r(const HaloArgs& a, hipStream_t s) {
     if (a.split) {
-        if (int rc = ensure_lds_attr((const void*)k_conv_v1s, LDS_S)) return rc;
+        constexpr int CW = AVSE_V1S_CW;
+        if (int rc = ensure_lds_attr((const void*)k_conv_v1s<CW>, LDS_S)) return rc;
         if (a.Hc % TH || a.Wc % TW || a.Co != 128 || a.Ci != NF || !a.w || a.out_mode != OUT_S16) {
             set_error("v_conv1 split kernel: unexpected layer shape, packing or output format");
             return 3;
@@ -626,7 +640,7 @@ int launch_conv_v1r(const HaloArgs& a, hipStream_t s) {
         const int tiles = a.N * (a.Hc / TH) * (a.Wc / TW);
         int gx = ncu >= 8 ? ncu / 8 * 8 : ncu;
         if (gx > tiles) gx = tiles;
-        hipLaunchKernelGGL(k_conv_v1s, dim3(gx), dim3(512), LDS_S, s, a);
+        hipLaunchKernelGGL(k_conv_v1s<CW>, dim3(gx), dim3(64 * (CW + 4)), LDS_S, s, a);
         AVSE_HIP_CHECK(hipGetLastError());
         return 0;
     }

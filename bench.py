@@ -65,7 +65,7 @@ ARITHMETIC = {
                   "between generic layers, (h, l) pairs between the split video convs: include/avse.h AVSE_F32_SPLIT",
     "bf16": "bf16 activations and weights, fp32 accumulation (reduced precision)"}
 KERNEL_NAME = {"bf16": "k_conv_stream<5, 16, 16, 1, true, 10, 0, 1, false>",
-               "fp32_split": "k_conv_stream<5, 16, 16, 1, true, 10, 0, 2, true>",
+               "fp32_split": "k_conv_stream<5, 16, 16, 1, true, 10, 0, 4, true>",
                "fp32": "k_conv<float, 128, true>"}
 PEAK_HBM_GBS = 8000.0
 
