@@ -27,6 +27,7 @@ import glob
 import json
 import os
 import statistics
+import re
 import sys
 import time
 
@@ -64,9 +65,18 @@ ARITHMETIC = {
                   "in the video convs (l l, 2^-22 of |a b|, dropped), all four in the other layers; activations fp32 "
                   "between generic layers, (h, l) pairs between the split video convs: include/avse.h AVSE_F32_SPLIT",
     "bf16": "bf16 activations and weights, fp32 accumulation (reduced precision)"}
-KERNEL_NAME = {"bf16": "k_conv_stream<5, 16, 16, 1, true, 10, 0, 1, false>",
-               "fp32_split": "k_conv_stream<5, 16, 16, 1, true, 10, 0, 4, true>",
-               "fp32": "k_conv<float, 128, true>"}
+# the dominant kernel's rocprof symbol per dtype (template arguments LAT / ABL / BP / S16 / compute waves as built)
+KERNEL_PATTERN = {"bf16": r"k_conv_stream<5, 16, 16, 1, true, \d+, 0, 1, false(, \d+)?>",
+                  "fp32_split": r"k_conv_stream<5, 16, 16, 1, true, \d+, 0, \d+, true(, \d+)?>",
+                  "fp32": r"k_conv<float, 128, true>"}
+
+
+def kernel_stat(stats, dtype):
+    """(symbol, average ms) of the dominant kernel in a rocprof stats map, or (None, None)."""
+    for name, ms in (stats or {}).items():
+        if re.fullmatch(KERNEL_PATTERN[dtype], name):
+            return name, ms
+    return None, None
 PEAK_HBM_GBS = 8000.0
 
 
@@ -514,7 +524,7 @@ def main():
     peak = PEAK_TFLOPS[args.dtype]
     pmc_file, pmc, pmc_status = pmc_summary(B, args.dtype)
     kp = (pmc or {}).get("kernels", {}).get(dom, {})
-    rp_ms = (pmc or {}).get("kernel_stats_avg_ms", {}).get(KERNEL_NAME[args.dtype])
+    ksym, rp_ms = kernel_stat((pmc or {}).get("kernel_stats_avg_ms"), args.dtype)
     fwd_ms = sum(stage_ms.values())
     kdesc = {"bf16": "k_conv_stream<5,16,16,1> bf16: persistent warp-specialised implicit GEMM M=4096/clip N=128 "
                      "K=3200, fused BN+LReLU+2x2 maxpool",
@@ -541,7 +551,7 @@ def main():
                                "(BASELINE configs[3]) on 200-ms@16kHz clips",
                    "global_batch": global_batch, "per_gpu_batch": B, "parallelism": f"dp{world}"},
         "window_ms_per_step": win.summary(),
-        "roofline": {"kernel": f"{dom} ({kdesc})", "kernel_symbol": KERNEL_NAME[args.dtype],
+        "roofline": {"kernel": f"{dom} ({kdesc})", "kernel_symbol": ksym or KERNEL_PATTERN[args.dtype],
                      "bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4), "traffic": kp.get("traffic_bytes"),
                      "algorithmic_bytes": kp.get("algorithmic_bytes"),
