@@ -2,6 +2,7 @@
 // the v_conv2 bench shape (N=512, 64x64, 128 -> 128 real channels = 256 halves of [h | l] pairs, 5x5, BP 4).  Timing
 // only: outputs are meaningless for ABL != 0.  Random f16 data (MFMA power, hence clock, depends on it).
 //   hipcc --offload-arch=gfx950 -O3 -std=c++20 -o /tmp/s16abl tools/stream_s16_ablate.hip && /tmp/s16abl
+//   (-DAVSE_S16_APLDS=1: the A'-from-LDS form of the third MFMA group)
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -81,21 +82,42 @@ int main() {
     rep("full again", run<0>(a, reps));
     unsigned long long* prof;
     (void)hipMalloc(&prof, 256 * 8 * 4 * 8);
-    (void)hipMemset(prof, 0, 256 * 8 * 4 * 8);
     a.prof = prof;
-    rep("instrumented (128)", run<128>(a, reps));
-    std::vector<unsigned long long> hp(256 * 8 * 4);
-    (void)hipMemcpy(hp.data(), prof, hp.size() * 8, hipMemcpyDeviceToHost);
-    double s[2][3] = {}, steps[2] = {};
-    for (int b = 0; b < 256; ++b)
-        for (int wv = 0; wv < 8; ++wv) {
-            const int role = wv >= 4;
-            for (int k = 0; k < 3; ++k) s[role][k] += (double)hp[(b * 8 + wv) * 4 + k];
-            steps[role] += (double)hp[(b * 8 + wv) * 4 + 3];
-        }
-    const char* names[2] = {"compute", "loader"};
-    for (int r = 0; r < 2; ++r)
-        std::printf("%-8s cycles/slice: work %7.1f  wait(vm/lgkm) %7.1f  barrier %7.1f\n", names[r], s[r][0] / steps[r],
-                    s[r][1] / steps[r], s[r][2] / steps[r]);
+    // instrumented variants: cycles per slice of the compute / loader waves, and the effective shader clock =
+    // compute-wave cycles per CU (all of its slices) / kernel time
+    auto inst = [&](const char* name, float ms) {
+        std::vector<unsigned long long> hp(256 * 8 * 4);
+        (void)hipMemcpy(hp.data(), prof, hp.size() * 8, hipMemcpyDeviceToHost);
+        double s[2][3] = {}, steps[2] = {};
+        for (int b = 0; b < 256; ++b)
+            for (int wv = 0; wv < 8; ++wv) {
+                const int role = wv >= 4;
+                for (int k = 0; k < 3; ++k) s[role][k] += (double)hp[(b * 8 + wv) * 4 + k];
+                steps[role] += (double)hp[(b * 8 + wv) * 4 + 3];
+            }
+        const double cyc = (s[0][0] + s[0][1] + s[0][2]) / 4 / 256;   // per compute wave = per CU
+        std::printf("%-28s %7.4f ms  clock %.2f GHz | compute work %6.1f wait %5.1f bar %5.1f | loader work %6.1f "
+                    "wait %5.1f bar %6.1f (cycles/slice)\n", name, ms, cyc / (ms * 1e6), s[0][0] / steps[0],
+                    s[0][1] / steps[0], s[0][2] / steps[0], s[1][0] / steps[1], s[1][1] / steps[1], s[1][2] / steps[1]);
+    };
+    (void)hipMemset(prof, 0, 256 * 8 * 4 * 8);
+    inst("full (128)", run<128>(a, 1));
+    (void)hipMemset(prof, 0, 256 * 8 * 4 * 8);
+    inst("no pieces (129)", run<129>(a, 1));
+    (void)hipMemset(prof, 0, 256 * 8 * 4 * 8);
+    inst("no weights (130)", run<130>(a, 1));
+    (void)hipMemset(prof, 0, 256 * 8 * 4 * 8);
+    inst("no loads (131)", run<131>(a, 1));
+    (void)hipMemset(prof, 0, 256 * 8 * 4 * 8);
+    inst("no frag reads (136)", run<136>(a, 1));
+    (void)hipMemset(prof, 0, 256 * 8 * 4 * 8);
+    inst("L2-resident input (192)", run<192>(a, 1));
+    (void)hipMemset(prof, 0, 256 * 8 * 4 * 8);
+    inst("full again (128)", run<128>(a, 1));
+    (void)hipMemset(prof, 0, 256 * 8 * 4 * 8);
+    inst("MFMA + permlane only (143)", run<143>(a, 1));
+    (void)hipMemset(prof, 0, 256 * 8 * 4 * 8);
+    inst("no frag reads, no loads (139)", run<139>(a, 1));
+    rep("L2-resident input (64)", run<64>(a, reps));
     return 0;
 }
