@@ -62,8 +62,9 @@ ARITHMETIC = {
     "fp32_split": "float32 inputs / outputs / accumulation; every layer's matrix-core products from f16 pairs x = h + l "
                   "of each fp32 operand (h = f16(x), l = f16(x - h); weights scaled per channel by a power of two) on "
                   "v_mfma_f32_16x16x32_f16 (32 exact products rounded once into the fp32 accumulator): h h, l h, h l "
-                  "in the video convs (l l, 2^-22 of |a b|, dropped), all four in the other layers; activations fp32 "
-                  "between generic layers, (h, l) pairs between the split video convs: include/avse.h AVSE_F32_SPLIT",
+                  "in the video convs (l l, 2^-22 of |a b|, dropped), all four in the other layers; activations pass "
+                  "between layers as the (h, l) pairs (the fp32 network inputs are split on load, the decoder's "
+                  "last output is fp32): include/avse.h AVSE_F32_SPLIT",
     "bf16": "bf16 activations and weights, fp32 accumulation (reduced precision)"}
 # the dominant kernel's rocprof symbol per dtype (template arguments LAT / ABL / BP / S16 / compute waves as built)
 KERNEL_PATTERN = {"bf16": r"k_conv_stream<5, 16, 16, 1, true, \d+, 0, 1, false(, \d+)?>",

@@ -36,7 +36,13 @@ DTYPES = ("fp32_split", "bf16")   # tools/profile.sh passes pmc_<tag>_<dtype>_<c
 
 
 def short(name):
-    """'void avse::(anonymous namespace)::k_conv_stream<5, 16, ...>(avse::HaloArgs)' -> 'k_conv_stream<5, 16, ...>'"""
+    """'void avse::(anonymous namespace)::k_conv_stream<5, 16, ...>(avse::HaloArgs)' -> 'k_conv_stream<5, 16, ...>'.
+    rocprofv3 leaves the _Float16 instantiations mangled ('_ZN4avse12_GLOBAL__N_16k_convIDF16_Li64ELb1ELb1EEEv...'):
+    those are spelled out by hand."""
+    m = re.search(r"k_convIDF16_Li(\d+)ELb([01])ELb([01])E", name)
+    if m:
+        tf = {"0": "false", "1": "true"}
+        return f"k_conv<_Float16, {m.group(1)}, {tf[m.group(2)]}, {tf[m.group(3)]}>"
     m = re.search(r"\b(k_\w+(<[^>]*>)?)", name)
     return m.group(1) if m else name
 
