@@ -623,9 +623,12 @@ int launch_conv(const ConvArgs& a, int dtype, hipStream_t s) {
     const int M = a.N * a.Hq * a.Wq;
     // short grids (< 256 tiles of 128 x 128) take 64-column tiles: twice the workgroups, and every output keeps its
     // summation order (the K loop is per fragment), so results are bitwise equal (batch-16 training step 6.56 -> 5.90
-    // ms).  Not with split-K, whose reduction is planned on 128-column tiles, nor the fused d_deconv6 tail.
+    // ms).  Not with split-K, whose reduction is planned on 128-column tiles, nor the fused d_deconv6 tail.  Split
+    // pairs: up to 256 tiles (v_conv6 at N = 512: one 128-column workgroup per CU, 0.171 -> 0.161 ms with 64 columns;
+    // a 512-tile bound also moved a_conv3 / d_deconv3, both slower)
     const long long tiles128 = (long long)((M + BM - 1) / BM) * ((a.Co + 127) / 128);
-    const int BN = (a.Co <= 64 || (a.ksplit == 1 && !a.fuse_w && tiles128 < 256)) ? 64 : 128;
+    const long long short_grid = dtype == kConvSplitPairs ? 257 : 256;
+    const int BN = (a.Co <= 64 || (a.ksplit == 1 && !a.fuse_w && tiles128 < short_grid)) ? 64 : 128;
     if (a.ksplit < 1 || (a.ksplit > 1 && (a.nphase != 1 || !a.partial))) {
         set_error("bad split-K configuration");
         return 1;

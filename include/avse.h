@@ -49,8 +49,9 @@ enum avse_status {
  *                   forms the products with v_mfma_f32_16x16x32_f16, each MFMA rounding its 32 exact products once
  *                   into the fp32 accumulator (a K = 3200 dot product: more accurate than exact-fp32 MFMA,
  *                   tools/split_probe.hip): h h, l h, h l in the video convolutions v_conv1..v_conv5 (l l, 2^-22 of
- *                   |a b|, dropped), all four in the other layers.  Activations pass between the split video layers as
- *                   the pairs (about 22 significant bits): whole-network error measured 1.3x AVSE_F32's (6.8e-5 vs
+ *                   |a b|, dropped), all four in the other layers.  Activations pass between layers as the pairs
+ *                   (about 22 significant bits; the float32 network inputs are split on load, the decoder's last
+ *                   output is float32): whole-network error measured 1.3x AVSE_F32's (6.8e-5 vs
  *                   5.1e-5 absolute RMS on dB-scale outputs, tests/test_gpu_split.py), inside the north star's 1e-4.
  *                   Activations of these layers must stay below 65504 in magnitude (f16 range; BatchNormalization
  *                   keeps a trained network's far below). */
