@@ -161,10 +161,12 @@ def leg_stft(dev, reps=50, B=4096, sets=5):
             "buffer_sets": sets, "working_set_mb": round(sets * B * STFT_BYTES_PER_CLIP / 1e6, 1), "reps": reps}
 
 
-def leg_audio_fp32(dev, model, reps=50, B=256):
-    """configs[2]: the audio branch alone, fp32, batch 256, all-zero video (video=None: the video embedding is
-    computed once per weights object and broadcast).  fp32 MFMA roofline on 0.3646 GFLOP per clip."""
-    dw = ops.DeviceWeights(model, "float32", dev)
+def leg_audio_fp32(dev, model, reps=50, B=256, dtype="fp32"):
+    """configs[2]: the audio branch alone, fp32 accuracy, batch 256, all-zero video (video=None: the video embedding is
+    computed once per weights object and broadcast).  Roofline on 0.3646 GFLOP per clip: the fp32 MFMA peak for
+    "fp32" (exact-fp32 MFMA), the split ceiling for "fp32_split" (these generic layers issue 4 f16 products per MAC:
+    f16 peak / 4)."""
+    dw = ops.DeviceWeights(model, LIB_DTYPE[dtype], dev)
     rng = np.random.default_rng(256)
     audio = torch.from_numpy(synth(rng, B, video=False)[0]).to(dev)
     mel = ops.spectrogram(audio, frames_per_slice=20).view(B, 80, 20)
@@ -181,10 +183,12 @@ def leg_audio_fp32(dev, model, reps=50, B=256):
     ms = e0.elapsed_time(e1) / reps
     tf = FLOP_AUDIO_BRANCH * B / (ms * 1e-3) / 1e12
     _, st = ops.forward_profile(dw, mel, None, out=out)
-    return {"config": "BASELINE configs[2]: audio-branch CNN forward, fp32 (exact-fp32 MFMA), batch 256, video zeros",
+    peak = PEAK_TFLOPS["fp32"] if dtype == "fp32" else PEAK_TFLOPS["bf16"] / 4
+    arith = "exact-fp32 MFMA" if dtype == "fp32" else "split-f16 products, AVSE_F32_SPLIT"
+    return {"config": f"BASELINE configs[2]: audio-branch CNN forward, fp32 ({arith}), batch 256, video zeros",
             "ms_per_forward": round(ms, 4), "clips_per_s": round(B / (ms * 1e-3), 1),
-            "roofline": {"bound": "mfma", "achieved": round(tf, 2), "peak": round(PEAK_TFLOPS["fp32"], 1),
-                         "unit": "TFLOP/s", "frac": round(tf / PEAK_TFLOPS["fp32"], 4),
+            "roofline": {"bound": "mfma", "achieved": round(tf, 2), "peak": round(peak, 1),
+                         "unit": "TFLOP/s", "frac": round(tf / peak, 4),
                          "flop_per_clip": FLOP_AUDIO_BRANCH},
             "stage_ms": {k: round(v, 4) for k, v in st.items() if v > 0.0005}, "reps": reps}
 
@@ -582,6 +586,7 @@ def main():
             if ldt != args.dtype:
                 result["legs"][f"fwd_{ldt}_b512"], outs[ldt] = leg_fwd(dev, model, audio, video, mean, std, ldt)
         result["legs"].update({"stft_b4096": leg_stft(dev), "audio_fp32_b256": leg_audio_fp32(dev, model),
+                               "audio_fp32_split_b256": leg_audio_fp32(dev, model, dtype="fp32_split"),
                                "train_fp32_b16": leg_train(dev, model)})
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # the same 16 clips through a dB-scale copy of the model in every dtype timed (north star bound on dB outputs)
