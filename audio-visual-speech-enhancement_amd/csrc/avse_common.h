@@ -200,6 +200,7 @@ struct ConvArgs {
     int act;             // 1 = LeakyReLU(0.3)
     int nphase;
     int ksplit;          // >1: split-K over blockIdx.z, fp32 partials + k_splitk_reduce (nphase == 1)
+    int ksplit_slabs;    // > 0: K slabs (16-k units) per split, else ceil(slabs / ksplit)
     float* partial;      // [ksplit][M][Co] workspace
     // fused trailing 1x1 Cout -> 1 layer (d_deconv6, network.py:133): out_f[pixel] = bias + sum_c w[c] * y[c],
     // y = this layer's output rounded to T; the T output is not stored (Co == 64, ksplit == 1, no pool)

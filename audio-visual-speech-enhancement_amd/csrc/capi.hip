@@ -250,10 +250,23 @@ size_t buf_elems(const NetPlan& p, int b) {
 //  k_splitk_reduce_tiles adds the splits in order, so each sum is the unsplit kernel's bit for bit.  Whether a launch
 //  splits (short grids only) then changes no result: the fp32 forward of a clip is the same whatever batch it runs
 //  in (the batched CLI predict reproduces the per-sample one exactly; tests/test_gpu_split.py).
+//  AVSE_F32_SPLIT dense layers (one tap): groups of G blocks per split, G and the split count from K and Cout only
+//  (never from M), so every batch size takes the same splits and the same ordered reduction — batch-invariant as
+//  above, with G x fewer fp32 partials (enc_dense: 41 one-block splits moved 236 MB of partials per launch at B = 512;
+//  11 four-block splits move 64 MB).  slabs_per_split (k_conv's ConvArgs::ksplit_slabs) = 8 G.
 constexpr int64_t kSplitTileCap = 2048;   // fp32 tiles x splits per launch (128 x 128-float partials each)
-int choose_ksplit(int64_t M, int Co, int kpad, int dtype) {
+int choose_ksplit(int64_t M, int Co, int kpad, int dtype, bool dense = false, int* slabs_per_split = nullptr) {
     const int BN = Co <= 64 ? 64 : 128;
     const int64_t tiles = ((M + 127) / 128) * ((Co + BN - 1) / BN);
+    if (slabs_per_split) *slabs_per_split = 0;
+    if (dtype == AVSE_F32_SPLIT && dense) {
+        const int nblocks = (kpad / 16 + kFp32Block - 1) / kFp32Block, tiles_n = (Co + 127) / 128;
+        const int G = std::max(1, (nblocks * tiles_n + 127) / 128);
+        const int ks = (nblocks + G - 1) / G;
+        if (ks < 2) return 1;
+        if (slabs_per_split) *slabs_per_split = G * kFp32Block;
+        return ks;
+    }
     if (dtype != AVSE_BF16) {
         const int nslab = kpad / 16;
         const int ks = (nslab + kFp32Block - 1) / kFp32Block;
@@ -272,7 +285,7 @@ size_t split_ws_bytes(int64_t N, int dtype, const Options& o, const NetPlan& p) 
                                                       {N, p.aemb, (p.emb + 31) / 32 * 32}, {N * 16, 512, 4608}};
     size_t mx = 0;
     for (const auto& x : g) {
-        const int ks = choose_ksplit(x.M, x.Co, x.kpad, dtype);
+        const int ks = choose_ksplit(x.M, x.Co, x.kpad, dtype, &x != &g[3]);
         // k_conv's partials cover whole 128 x BN tiles (MFMA-native order)
         const int bn = x.Co <= 64 ? 64 : 128;
         const size_t mp = (size_t)((x.M + 127) / 128) * 128, np = (size_t)((x.Co + bn - 1) / bn) * bn;
@@ -1256,7 +1269,7 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
     auto ksplit = [&](ConvArgs& a) {   // dense layers / v_conv6: split-K when the grid is small
         if (a.nphase != 1) return;
         const int64_t M = (int64_t)a.N * a.Hq * a.Wq;
-        a.ksplit = choose_ksplit(M, a.Co, a.ph[0].kpad, dt);
+        a.ksplit = choose_ksplit(M, a.Co, a.ph[0].kpad, dt, a.ph[0].ntaps == 1, &a.ksplit_slabs);
         a.partial = reinterpret_cast<float*>(c->arena + off[B_COUNT]);
     };
     auto L = [&](int i) -> const GpuLayer& { return W->layers[i]; };

@@ -129,7 +129,7 @@ __global__ __launch_bounds__(256, (conv_occupancy<T, BN, FAST, S16>())) void k_c
     const int n0 = blockIdx.y * BN;
     // split-K: this block reduces slabs [s_begin, s_end) of the phase's K
     const int nslab_all = ph.kpad / SLAB;
-    const int sps = (nslab_all + a.ksplit - 1) / a.ksplit;
+    const int sps = a.ksplit_slabs > 0 ? a.ksplit_slabs : (nslab_all + a.ksplit - 1) / a.ksplit;
     const int s_begin = zsplit * sps;
     const int s_end = min(nslab_all, s_begin + sps);
     for (int i = threadIdx.x; i < ph.ntaps && i < MAX_TAPS_LDS; i += 256) tap_lds[i] = a.taps[ph.tap_off + i];
