@@ -85,7 +85,13 @@ template <typename T, int BN, bool FAST, bool S16 = false> constexpr int conv_oc
 // fp32 blocked summation: the K loop accumulates FP32_BLOCK slabs (FP32_BLOCK * 16 products per output) into a
 // zeroed partial that is then added to the running sum, so the running sum takes K / 128 roundings instead of
 // K / 4 (one per 16x16x4 MFMA).
-constexpr int FP32_BLOCK = kFp32Block;   // avse_common.h (train.hip's block-exact split-K plans on it)
+constexpr int FP32_BLOCK = kFp32Block;
+// timing ablations of the FAST K loop (tools/kconv_ablate.hip only; 0 in the library): 1 = no global loads, 2 = no
+// LDS slab stores, 4 = no MFMAs, 8 = no workgroup barrier in the loop, 16 = no fragment reads
+#ifndef AVSE_KCONV_ABL
+#define AVSE_KCONV_ABL 0
+#endif
+constexpr int KABL = AVSE_KCONV_ABL;   // avse_common.h (train.hip's block-exact split-K plans on it)
 
 // S16 (AVSE_F32_SPLIT's generic layers): split-f16 products on the 16-bit matrix cores.  The LDS A slab row is
 // [h(16) | l(16)] f16 of 16 real k (h = f16(x), l = f16(x - h)): with T = float (fp32 input: a_conv1, a 6-frame
@@ -214,6 +220,10 @@ __global__ __launch_bounds__(256, (conv_occupancy<T, BN, FAST, S16>())) void k_c
     constexpr int P = 3;
     i32x4 ras[P][2], rbs[P][BCH];
     auto load_slab = [&](int s, i32x4 (&ra)[2], i32x4 (&rb)[BCH]) {
+        if constexpr (FAST && (KABL & 1)) {
+            ra[0][0] ^= s;   // keep the register sets live without the loads
+            return;
+        }
         if constexpr (FAST) {
             // A: the channel chunk is the scalar offset (an out-of-range row offset stays out of range);
             // B: rows past Cout and slabs past the phase's K read zeros (range-checked voffset)
@@ -253,6 +263,10 @@ __global__ __launch_bounds__(256, (conv_occupancy<T, BN, FAST, S16>())) void k_c
         while (kc >= a.Ci) { kc -= a.Ci; ++kj; }
     };
     auto store_slab = [&](int buf, const i32x4 (&ra)[2], const i32x4 (&rb)[BCH]) {
+        if constexpr (FAST && (KABL & 2)) {
+            if (ra[0][0] == 0x7fffffff && rb[0][0] == 0x7fffffff) *reinterpret_cast<int*>(AS(buf)) = 1;
+            return;
+        }
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const int row = (tid >> 2) + 64 * h;
@@ -301,6 +315,12 @@ __global__ __launch_bounds__(256, (conv_occupancy<T, BN, FAST, S16>())) void k_c
         constexpr int qn = (q + 1) % P;
         const int buf = FAST ? q : (s - s_begin) & 1;      // FAST: three buffers, slab x in buffer (x - s_begin) % 3
         i32x4 fa[NI], fb[NJ], fl[NJ];
+        if constexpr (FAST && (KABL & 16)) {
+#pragma unroll
+            for (int i = 0; i < NI; ++i) fa[i] = (i32x4){s + i, lane, 0, 0};
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) fb[j] = fl[j] = (i32x4){s - j, lane, 1, 0};
+        } else {
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
             const int row = wm * 64 + 16 * i + fr;
@@ -312,11 +332,14 @@ __global__ __launch_bounds__(256, (conv_occupancy<T, BN, FAST, S16>())) void k_c
             fb[j] = *reinterpret_cast<const i32x4*>(BS(buf) + row * 64 + (((S16 ? (fg & 1) : fg) ^ swz(row)) << 4));
             if constexpr (S16) fl[j] = *reinterpret_cast<const i32x4*>(BS(buf) + row * 64 + (((2 + (fg & 1)) ^ swz(row)) << 4));
         }
+        }
 #pragma unroll
         for (int i = 0; i < NI; ++i)
 #pragma unroll
             for (int j = 0; j < NJ; ++j) {
-                if constexpr (S16) {
+                if constexpr (FAST && (KABL & 4)) {
+                    part[i][j][0] += __builtin_bit_cast(float, fa[i][0] ^ fb[j][1] ^ fl[j][2]);
+                } else if constexpr (S16) {
                     part[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
                         __builtin_bit_cast(f16x8, fa[i]), __builtin_bit_cast(f16x8, fb[j]), part[i][j], 0, 0, 0);
                     part[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
@@ -353,7 +376,7 @@ __global__ __launch_bounds__(256, (conv_occupancy<T, BN, FAST, S16>())) void k_c
             store_slab(buf ^ 1, ras[qn], rbs[qn]);   // slab s+1, loaded P-1 steps ago
             load_slab(s + 1 + P, ras[qn], rbs[qn]);  // refill with slab s+1+P (the load cursor is sequential)
         }
-        __syncthreads();
+        if constexpr (!(FAST && (KABL & 8))) __syncthreads();
     };
     for (int s = s_begin; s < s_end; s += P) {
         step(std::integral_constant<int, 0>{}, s);
