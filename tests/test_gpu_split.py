@@ -120,3 +120,29 @@ def test_split_small_activations(gpu):
     got = ops.forward(dw, ops.to_device(mel), ops.to_device(video)).cpu().numpy()
     print(f"split tiny video: rel {rel_rms(got, ref):.3e}")
     assert rel_rms(got, ref) <= FP32_REL
+
+
+@pytest.mark.parametrize("dtype", [SPLIT, "float32"])
+def test_fp32_forward_is_batch_invariant(gpu, dtype):
+    """The fp32-accurate forwards give every clip the same bits whatever batch it runs in: split-K plans either split
+    into whole fp32 summation blocks (v_conv6: one block per split, reduced in order) or into groups fixed by K and
+    Cout alone (the split dtype's dense layers), never by the batch.  600 clips at once against the same clips run
+    alone (N = 1: the most split-K) and in a batch of 7."""
+    from avse_amd import ops
+    from avse_amd.model import KerasModel
+    import bench
+    N = 600
+    rng = np.random.default_rng(77)
+    audio_np, video_np = bench.synth(rng, N)
+    mean_np = video_np.mean(axis=(0, 3)).astype(np.float32)
+    std_np = video_np.std(axis=(0, 3)).astype(np.float32)
+    model = KerasModel.init(seed=3, randomize=True)
+    dw = ops.DeviceWeights(model, dtype)
+    mel = ops.spectrogram(ops.to_device(audio_np), frames_per_slice=20).view(N, 80, 20)
+    video, mean, std = ops.to_device(video_np), ops.to_device(mean_np), ops.to_device(std_np)
+    full = ops.forward(dw, mel, video, mean, std).cpu().numpy()
+    for c in (0, 299, 599):
+        one = ops.forward(dw, mel[c:c + 1].contiguous(), video[c:c + 1].contiguous(), mean, std).cpu().numpy()
+        assert np.array_equal(one.reshape(full[c].shape), full[c]), (c, float(np.abs(one.reshape(full[c].shape) - full[c]).max()))
+    part = ops.forward(dw, mel[290:297].contiguous(), video[290:297].contiguous(), mean, std).cpu().numpy()
+    assert np.array_equal(part, full[290:297])
