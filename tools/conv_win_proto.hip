@@ -25,11 +25,13 @@ namespace {
 constexpr int H = 40, W = 10, HWc = H * W, CI = 128, CO = 64, NT = 16, NCH = CI / 16;   // 16-ch pair chunks
 constexpr int CIH = 2 * CI, KPH = NT * CIH;           // halves per pixel / per weight row
 constexpr int WP = 14;                                 // window pitch (13 columns: x - 2 .. x + 1 over 0..9, + 1)
-constexpr int WROWS = 22;                              // window rows capacity (<= 14 tile rows + 2 x 4 halo rows)
-constexpr int WIN = WROWS * WP * 64;                   // bytes per window buffer (19,712)
 constexpr int BNW = 64, BSL = BNW * 64;                // B slab bytes
-constexpr int NPIECE = (WROWS * WP * 4 + 255) / 256;   // 16-B window pieces per thread per chunk
-constexpr int LDS_W = 2 * WIN + 3 * BSL;
+// TM-row tiles (128: 4 waves, 256: 8 waves sharing every weight slab): window rows capacity = the tile's image rows
+// (<= TM / W + 2 over two clips) + 2 x 4 halo rows
+template <int TM> struct WinGeom {
+    static constexpr int NTH = TM * 2, WROWS = TM / W + 2 + 8, WIN = WROWS * WP * 64;
+    static constexpr int NPIECE = (WROWS * WP * 4 + NTH - 1) / NTH, LDS = 2 * WIN + 3 * BSL;
+};
 
 __device__ __forceinline__ int bswz(int row) { return ((row >> 3) & 1) * 3; }
 // window pixel p's 16-B slots rotate every 4 pixels: 16 lanes reading 16 neighbouring pixels hit 16 distinct bank quads
@@ -38,18 +40,21 @@ __device__ __forceinline__ int bswz(int row) { return ((row >> 3) & 1) * 3; }
 #endif
 __device__ __forceinline__ int wsw(int p) { return WIN_SWZ ? (p >> 2) & 3 : 0; }
 
-// grid: ceil(M / 128) tiles; 256 threads = 4 waves (2 x 2: 64 rows x 32 columns each)
-__global__ __launch_bounds__(256, 3) void k_win4(ConvArgs a) {
+// grid: ceil(M / TM) tiles; TM / 32 waves (TM / 64 x 2: 64 rows x 32 columns each)
+template <int TM>
+__global__ __launch_bounds__(TM * 2, TM == 128 ? 3 : 2) void k_win4(ConvArgs a) {
+    using G = WinGeom<TM>;
+    constexpr int NTH = G::NTH, WROWS = G::WROWS, WIN = G::WIN, NPIECE = G::NPIECE;
     extern __shared__ __attribute__((aligned(16))) char lds[];
     char* const win = lds;                 // [2][WIN]
     char* const bs = lds + 2 * WIN;        // [3][BSL]
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wm = wid >> 1, wn = wid & 1;
     const int fr = lane & 15, fg = lane >> 4;
     const int M = a.N * HWc;
-    const int m0 = blockIdx.x * 128;
+    const int m0 = blockIdx.x * TM;
     // the tile's rows span clip c0 (pixels p0 ..) and possibly c0 + 1
     const int c0 = m0 / HWc, p0 = m0 - c0 * HWc;
-    const int last = min(m0 + 127, M - 1);
+    const int last = min(m0 + TM - 1, M - 1);
     const int c1 = last / HWc;
     const int ylo0 = p0 / W, yhi0 = (c1 == c0) ? (last - c0 * HWc) / W : H - 1;
     const int n0 = yhi0 - ylo0 + 4;                              // window rows of region 0: ylo0 - 2 .. yhi0 + 1
@@ -63,7 +68,7 @@ __global__ __launch_bounds__(256, 3) void k_win4(ConvArgs a) {
     int psrc[NPIECE], pdst[NPIECE];
 #pragma unroll
     for (int k = 0; k < NPIECE; ++k) {
-        const int q = tid + 256 * k, p = q >> 2, qq = q & 3;
+        const int q = tid + NTH * k, p = q >> 2, qq = q & 3;
         const int wrow = p / WP, wcol = p - wrow * WP;
         int src = kOOB;
         if (wrow < n0 + n1) {
@@ -86,7 +91,7 @@ __global__ __launch_bounds__(256, 3) void k_win4(ConvArgs a) {
         abase[i] = wrow * WP + x + 2;   // window pixel at tap (0, 0)
     }
     // B: thread's 16-B piece of the slab: row tid >> 2, chunk tid & 3
-    const int brow = tid >> 2, bg = tid & 3;
+    const int brow = (tid & 255) >> 2, bg = tid & 3;
     const int bsrc = brow * KPH * 2 + bg * 16, bdst = brow * 64 + ((bg ^ bswz(brow)) << 4);
     auto bslab_off = [](int s) { const int c = s / NT, t = s - c * NT; return t * CIH * 2 + c * 64; };
     constexpr int NS = NCH * NT;   // 128 slabs
@@ -111,8 +116,9 @@ __global__ __launch_bounds__(256, 3) void k_win4(ConvArgs a) {
     i32x4 rb[3];
 #pragma unroll
     for (int p = 0; p < 3; ++p) rb[p] = __builtin_amdgcn_raw_buffer_load_b128(rsB, bsrc + bslab_off(p), 0, 0);
-    *reinterpret_cast<i32x4*>(bs + bdst) = rb[0];
-    rb[0] = __builtin_amdgcn_raw_buffer_load_b128(rsB, bsrc + bslab_off(3), 0, 0);
+    const bool bl = tid < 256;   // the weight slab (4 KB) is 256 x 16 B
+    if (bl) *reinterpret_cast<i32x4*>(bs + bdst) = rb[0];
+    rb[0] = __builtin_amdgcn_raw_buffer_load_b128(rsB, bl ? bsrc + bslab_off(3) : kOOB, 0, 0);
     __syncthreads();
 
     f32x4 acc[4][2], part[4][2];
@@ -164,8 +170,8 @@ __global__ __launch_bounds__(256, 3) void k_win4(ConvArgs a) {
                 }
         }
         // B slab s + 1 -> LDS (buffer qn held slab s - 2, read before the barrier of step s - 2); refill with s + 4
-        *reinterpret_cast<i32x4*>(bs + qn * BSL + bdst) = rb[qn];
-        rb[qn] = __builtin_amdgcn_raw_buffer_load_b128(rsB, bsrc + bslab_off(min(s + 4, NS - 1)), 0, 0);
+        if (bl) *reinterpret_cast<i32x4*>(bs + qn * BSL + bdst) = rb[qn];
+        rb[qn] = __builtin_amdgcn_raw_buffer_load_b128(rsB, bl ? bsrc + bslab_off(min(s + 4, NS - 1)) : kOOB, 0, 0);
         if (t == NT - 1 && c + 1 < NCH) {   // next chunk's window -> the other buffer (read last during chunk c - 1)
 #pragma unroll
             for (int k = 0; k < NPIECE; ++k)
@@ -251,8 +257,8 @@ int main() {
     (void)hipMemcpy(sc, scv.data(), CO * 4, hipMemcpyHostToDevice);
     (void)hipMemcpy(sh, shv.data(), CO * 4, hipMemcpyHostToDevice);
     a.in = in; a.w = w; a.taps = reinterpret_cast<const int2*>(tp); a.scale = sc; a.shift = sh;
-    (void)hipFuncSetAttribute((const void*)k_win4, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_W);
-    const int grid = (N * HWc + 127) / 128;
+    (void)hipFuncSetAttribute((const void*)k_win4<128>, hipFuncAttributeMaxDynamicSharedMemorySize, WinGeom<128>::LDS);
+    (void)hipFuncSetAttribute((const void*)k_win4<256>, hipFuncAttributeMaxDynamicSharedMemorySize, WinGeom<256>::LDS);
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
@@ -270,7 +276,13 @@ int main() {
     a1.out = out;
     a2.out = out2;
     const float t_conv = time_it([&] { launch_conv(a1, kConvSplitPairs, 0); });
-    const float t_win = time_it([&] { hipLaunchKernelGGL(k_win4, dim3(grid), dim3(256), LDS_W, 0, a2); });
+    const float t_win = time_it([&] {
+        hipLaunchKernelGGL(k_win4<128>, dim3((N * HWc + 127) / 128), dim3(256), WinGeom<128>::LDS, 0, a2); });
+    (void)hipDeviceSynchronize();
+    std::vector<_Float16> o128(out_b / 2);
+    (void)hipMemcpy(o128.data(), out2, out_b, hipMemcpyDeviceToHost);
+    const float t_win256 = time_it([&] {
+        hipLaunchKernelGGL(k_win4<256>, dim3((N * HWc + 255) / 256), dim3(512), WinGeom<256>::LDS, 0, a2); });
     const float t_conv2 = time_it([&] { launch_conv(a1, kConvSplitPairs, 0); });
     (void)hipDeviceSynchronize();
     std::vector<_Float16> o1(out_b / 2), o2(out_b / 2);
@@ -288,7 +300,10 @@ int main() {
         }
     const double flop = 2.0 * N * HWc * CO * (double)CI * NT;
     std::printf("k_conv   %.4f / %.4f ms  %.1f TF/s\n", t_conv, t_conv2, flop / (t_conv * 1e-3) / 1e12);
-    std::printf("k_win4   %.4f ms  %.1f TF/s  (LDS %d B)\n", t_win, flop / (t_win * 1e-3) / 1e12, LDS_W);
+    std::printf("k_win4<128> %.4f ms  %.1f TF/s  (LDS %d B)\n", t_win, flop / (t_win * 1e-3) / 1e12, WinGeom<128>::LDS);
+    std::printf("k_win4<256> %.4f ms  %.1f TF/s  (LDS %d B); outputs bitwise equal to <128>: %s\n", t_win256,
+                flop / (t_win256 * 1e-3) / 1e12, WinGeom<256>::LDS,
+                std::memcmp(o128.data(), o2.data(), out_b) == 0 ? "yes" : "NO");
     std::printf("outputs: rel RMS %.3e, max abs diff %.3e, RMS %.3e  %s\n", std::sqrt(num / den), mx,
                 std::sqrt(den / ((double)N * HWc * CO)), hipGetErrorString(hipGetLastError()));
     return 0;
