@@ -16,12 +16,24 @@ import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 LIB_PATH = os.environ.get("AVSE_LIBRARY") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libavse.so")
 HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "avse.h")
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 AVSE_F32 = 0
 AVSE_BF16 = 1
 AVSE_F32_SPLIT = 2
 AVSE_PAD_REFLECT = 0
 AVSE_PAD_CONSTANT = 1
+AVSE_ERR_RANGE = 6
+AVSE_RANGE_RECOMPUTE, AVSE_RANGE_ERROR = 0, 1
+# range-guard bits (include/avse.h avse_forward_checked): bit i = plan layer i, 24 / 25 the split audio / video inputs
+LAYER_NAMES = ("a_conv1", "a_conv2", "a_conv3", "a_conv4", "a_conv5", "v_conv1", "v_conv2", "v_conv3", "v_conv4",
+               "v_conv5", "v_conv6", "enc_dense", "dec_dense1", "dec_dense2", "d_deconv1", "d_deconv2", "d_deconv3",
+               "d_deconv4", "d_deconv5", "d_deconv6")
+
+
+def range_bit_names(bits):
+    """The layers / inputs a range-guard word names."""
+    names = [n for i, n in enumerate(LAYER_NAMES) if bits >> i & 1]
+    return names + [n for b, n in ((24, "audio input"), (25, "video input")) if bits >> b & 1]
 AVSE_NUM_STAGES = 22
 STAGE_NAMES = ("video_prep", "audio_prep", "a_conv1", "a_conv2", "a_conv3", "a_conv4", "a_conv5",
                "v_conv1", "v_conv2", "v_conv3", "v_conv4", "v_conv5", "v_conv6", "enc_dense", "dec_dense1",
@@ -57,6 +69,10 @@ SIGNATURES = {
                             _c_void_p]),
     "avse_video_normalize": (_int, [_c_void_p, _c_void_p, _i64, _int, _int, _int, _c_void_p, _c_void_p, _c_void_p]),
     "avse_mse": (_int, [_c_void_p, _c_void_p, _c_void_p, _i64, _c_void_p, _c_void_p]),
+    "avse_forward_checked": (_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _c_void_p,
+                                    _c_void_p, _int, ctypes.POINTER(ctypes.c_uint32)]),
+    "avse_range_status": (_int, [_c_void_p, _c_void_p, ctypes.POINTER(ctypes.c_uint32)]),
+    "avse_weights_act_exponents": (_int, [_c_void_p, ctypes.POINTER(_int), _int]),
     "avse_forward_profile": (_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64,
                                     _c_void_p, _c_void_p, ctypes.POINTER(_flt)]),
     "avse_debug_scratch": (_int, [_c_void_p, _i64, _int, ctypes.POINTER(_c_void_p), ctypes.POINTER(_i64)]),
@@ -117,10 +133,14 @@ def load():
     return _lib
 
 
+class RangeError(AvseError):
+    """avse_forward_checked(AVSE_RANGE_ERROR): an AVSE_F32_SPLIT activation left the f16 pair range."""
+
+
 def check(rc, what):
     if rc != 0:
         msg = load().avse_last_error().decode(errors="replace")
-        raise AvseError(f"{what} failed (status {rc}): {msg}")
+        raise (RangeError if rc == AVSE_ERR_RANGE else AvseError)(f"{what} failed (status {rc}): {msg}")
 
 
 class Context:
@@ -131,6 +151,14 @@ class Context:
         self._cdll = load()   # held for __del__: module globals may be torn down first at interpreter exit
         self.handle = _c_void_p()
         check(load().avse_ctx_create(device_index, ctypes.byref(self.handle)), "avse_ctx_create")
+
+    def range_status(self, stream=None):
+        """avse_range_status: the range-guard bits raised by unchecked split forwards since the last call (waits for
+        `stream`, default torch's current stream on this device, and clears them)."""
+        bits = ctypes.c_uint32()
+        check(load().avse_range_status(self.handle, stream if stream is not None else stream_handle(self.device_index),
+                                       ctypes.byref(bits)), "avse_range_status")
+        return bits.value
 
     def reserve(self, max_clips, dtype):
         check(load().avse_ctx_reserve(self.handle, int(max_clips), int(dtype)), "avse_ctx_reserve")

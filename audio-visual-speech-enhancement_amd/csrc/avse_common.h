@@ -39,6 +39,7 @@ struct Options {
     int graph = 0;            // AVSE_GRAPH: avse_forward replays a hipGraph per argument set
     int gemm_ksplit_cap = 0;  // AVSE_GEMM_KSPLIT: cap k_gemm's split-K factor (0 = no cap)
     int dense_istft = 0;      // AVSE_DENSE_ISTFT: ISTFT through the dense pinv + scratch frames + k_ola (not fused)
+    int no_act_scale = 0;     // AVSE_NO_ACT_SCALE: split weights loaded without per-layer activation exponents
 };
 
 #define AVSE_HIP_CHECK(expr)                                                                   \
@@ -208,8 +209,24 @@ struct ConvArgs {
     float fuse_bias;
     float* fuse_out;
     int out_s16;         // 1: the output in the split pair layout (strides and offset in halves), else T / fp32
+    // AVSE_F32_SPLIT range guard (pair_out_of_range): a stored pair value, or an fp32 input value split on load,
+    // outside the f16 range ORs range_bit / range_in_bit into *range_flag (nullable)
+    unsigned* range_flag;
+    unsigned range_bit, range_in_bit;
     ConvPhase ph[MAX_PHASES];
 };
+
+// AVSE_F32_SPLIT range guard: x cannot be carried as the pair h = f16(x), l = f16(x - h) when h would be infinite
+// (|x| >= 65520, the f16 overflow threshold under round-to-nearest-even) or x is NaN.  Kernels fold the test over the
+// values a lane stores and report once (one vector atomic from the lanes that saw one; the flag word is sticky until
+// avse_range_status / avse_forward_checked read it).
+__device__ __forceinline__ bool pair_out_of_range(float x) { return !(__builtin_fabsf(x) < 65520.f); }
+__device__ __forceinline__ void range_report(unsigned* flag, unsigned bit, bool bad) {
+    if (bad && flag) atomicOr(flag, bit);
+}
+// range flag bits: bit i = layer i of the plan (a_conv1 = 0 .. d_deconv5 = 18), the split network inputs below
+constexpr unsigned kRangeAudioIn = 1u << 24, kRangeVideoIn = 1u << 25;
+int launch_flag_or(unsigned* flag, unsigned bits, hipStream_t s);
 
 // k_conv's fp32 blocked summation: K-slabs (16 products each) summed FP32_BLOCK at a time into a zeroed partial that
 // is added to the running sum in slab order.  A split-K whose every split is exactly one such block, reduced in split
@@ -323,6 +340,8 @@ struct HaloArgs {
                              // (2 x channels), w holds [Bh | Bl] rows; out_mode OUT_S16 or OUT_F32
     int out_mode;            // HaloOut
     unsigned long long* prof;   // ablation harness only (ABL & 128): per-wave cycle counters, else unused
+    unsigned* range_flag;    // split: range guard (ConvArgs::range_flag), nullable
+    unsigned range_bit, range_in_bit;   // OUT_S16 stores / v_conv1's split of the (normalised) video input
 };
 
 int launch_conv_stream(const HaloArgs& a, hipStream_t s);   // conv_stream.hip (non-V1 variants)

@@ -136,6 +136,10 @@ struct avse_ctx {
     float* mse_partial = nullptr;
     float* zero_video = nullptr;    // one all-zero [128][128][8] clip (video == NULL forwards, any F <= 8)
     int* gemm_counters = nullptr;   // gemm.hip split-K tickets (zero between launches)
+    // AVSE_F32_SPLIT range guard words (avse_common.h pair_out_of_range): [0] sticky for avse_forward (read and cleared
+    // by avse_range_status), [1] cleared and read by each avse_forward_checked, [2] the all-zero-video embedding
+    unsigned* range = nullptr;
+    unsigned* range_host = nullptr;   // pinned readback word
     char* arena = nullptr;
     size_t arena_bytes = 0;
     NetPlan last_plan = kPlan25;    // the network shape of the last forward (avse_debug_scratch's arena layout)
@@ -144,7 +148,7 @@ struct avse_ctx {
     hipEvent_t fork = nullptr, join = nullptr;
     // avse_forward's replay cache: the whole forward captured once per argument set into a hipGraph
     struct Graph {
-        const void* key[8];
+        const void* key[9];
         int64_t n;
         Options opt;
         hipGraphExec_t exec;
@@ -192,6 +196,7 @@ const OptionName kOptionNames[] = {
     {"graph", "AVSE_GRAPH", &Options::graph},
     {"gemm_ksplit_cap", "AVSE_GEMM_KSPLIT", &Options::gemm_ksplit_cap},
     {"dense_istft", "AVSE_DENSE_ISTFT", &Options::dense_istft},
+    {"no_act_scale", "AVSE_NO_ACT_SCALE", &Options::no_act_scale},
 };
 
 struct avse_weights {
@@ -207,12 +212,23 @@ struct avse_weights {
     // Published only after its stream has finished (another stream / thread may read it right away), under a lock.
     mutable std::atomic<void*> vzero_emb{nullptr};
     mutable std::mutex vzero_mu;
+    mutable unsigned vzero_range = 0;   // split: range-guard bits the embedding's computation raised (sticky per forward)
+    // AVSE_F32_SPLIT: per-layer power-of-two activation exponents (act_exponents: layer i stores the pairs of
+    // x 2^act_exp[i]), the canonical blob (host copy) and, built from it on the first range-guard hit, the same network
+    // on exact-fp32 MFMA that avse_forward_checked recomputes such a batch on
+    int act_exp[kNumLayers] = {};
+    std::vector<float> blob;
+    mutable avse_weights* f32_twin = nullptr;
+    mutable std::mutex twin_mu;
     std::vector<void*> allocs;
-    ~avse_weights() {
-        (void)hipFree(vzero_emb.load());
-        for (void* p : allocs) (void)hipFree(p);
-    }
+    ~avse_weights();
 };
+
+avse_weights::~avse_weights() {
+    delete f32_twin;
+    (void)hipFree(vzero_emb.load());
+    for (void* p : allocs) (void)hipFree(p);
+}
 
 namespace {
 
@@ -311,7 +327,8 @@ bool valid_dtype(int dtype) { return dtype == AVSE_F32 || dtype == AVSE_BF16 || 
 
 // grows the forward scratch; never while `s` (nullable) is being captured into a graph: the caller must reserve first
 int ensure_arena(avse_ctx* c, int64_t clips, int dtype, const NetPlan& p, hipStream_t s) {
-    const size_t need = arena_bytes(clips, dtype, c->opt, nullptr, p);
+    // at least the N = 1 layout: a video == NULL forward runs a one-clip video encoder (and its split-K) in it
+    const size_t need = std::max(arena_bytes(clips, dtype, c->opt, nullptr, p), arena_bytes(1, dtype, c->opt, nullptr, p));
     if (need <= c->arena_bytes) return 0;
     if (s) {
         hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -528,9 +545,46 @@ int ensure_istft_tables(avse_ctx* c, int sr, int n_fft, int n_mels, double fmin,
     return 0;
 }
 
+// AVSE_F32_SPLIT activation exponents.  The split layers carry activations as f16 pairs, whose ~22 significant bits
+// hold for |x| in [2^-3, 65504): below 2^-3 the lo piece is an f16 subnormal (absolute quantum 2^-24), from 65520 the
+// hi piece overflows (the range guard then reports it).  A BatchNormalization layer's output per channel is
+// gamma xhat + beta with xhat standardised by the moving statistics, so the layer's magnitude is ~ M = max_c (|beta_c| +
+// |gamma_c|).  Layers with M in [2^-2, 2^8] keep exponent 0 (the common case: BN keeps activations O(1), and every
+// stored value is then exactly the unscaled pair); any other layer stores the pairs of x 2^e with M 2^e in (4, 8], so a
+// layer of tiny activations keeps its 22 bits and a layer of huge ones its headroom below 65504 (folded into the
+// layer's own scale / shift and the next layer's scale, build_layer).  The two concat halves (a_conv5, v_conv6) share
+// one exponent, the smaller (enc_dense reads them as one K); d_deconv5 feeds the fp32 d_deconv6 dot (exponent 0).
+void act_exponents(const NetPlan& P, const float* blob, int* e) {
+    const float* p = blob;
+    for (int i = 0; i < kNumLayers; ++i) {
+        const LayerDef& L = P.L[i];
+        p += (size_t)L.kh * L.kw * L.cin * L.cout + L.cout;
+        e[i] = 0;
+        if (!L.bn) continue;
+        const float* g = p;
+        const float* b = p + L.bn_channels;
+        p += 4 * (size_t)L.bn_channels;
+        double m = 0.0;
+        for (int c = 0; c < L.bn_channels; ++c) m = std::max(m, std::fabs((double)b[c]) + std::fabs((double)g[c]));
+        if (!(m > 0.0) || !std::isfinite(m) || (m >= 0.25 && m <= 256.0)) continue;
+        int e2 = 0;
+        (void)std::frexp(m, &e2);                      // m <= 2^e2
+        e[i] = std::max(-24, std::min(24, 3 - e2));    // m 2^e in (4, 8]
+    }
+    e[4] = e[10] = std::min(e[4], e[10]);
+    e[18] = e[19] = 0;
+}
+
+// the exponent of the activations layer i reads (act_exponents; the network inputs: 0)
+int act_exp_in(const int* e, int i) {
+    if (i == 0 || i == 5) return 0;
+    if (i == 11) return e[4];
+    return e[i - 1];
+}
+
 // Build phase/tap tables + packed [Cout][Kpad] weights for one layer.
 int build_layer(avse_weights* W, int li, const float* kernel, const float* bias, const float* bn,
-                const Options& opt) {
+                const Options& opt, int e_in = 0, int e_out = 0) {
     const LayerDef& L = W->plan.L[li];
     GpuLayer& G = W->layers[li];
     G.def = L;
@@ -628,6 +682,15 @@ int build_layer(avse_weights* W, int li, const float* kernel, const float* bias,
     }
     int rc;
     const bool split = W->dtype == AVSE_F32_SPLIT;
+    if (split && (e_in || e_out)) {
+        // activation exponents (act_exponents): this layer reads pairs of x 2^e_in and stores pairs of y 2^e_out, so
+        // y 2^e_out = LReLU(acc 2^-e_in scale 2^e_out + shift 2^e_out) — powers of two: exact, and they commute with
+        // LeakyReLU and max pooling
+        for (int n = 0; n < L.cout; ++n) {
+            scale[n] = std::ldexp(scale[n], e_out - e_in);
+            shift[n] = std::ldexp(shift[n], e_out);
+        }
+    }
     std::vector<float> scale_g = scale;   // the generic kernel's epilogue scale (split: with the weight exponents undone)
     if (W->dtype == AVSE_BF16) {
         std::vector<uint16_t> pb(packed.size());
@@ -933,9 +996,13 @@ int avse_ctx_create(int device, avse_ctx** out) {
     }
     if (hipMalloc((void**)&c->mse_partial, sizeof(float) * 256) != hipSuccess ||
         hipMalloc((void**)&c->gemm_counters, sizeof(int) * 8192) != hipSuccess ||
-        hipMemset(c->gemm_counters, 0, sizeof(int) * 8192) != hipSuccess) {
+        hipMemset(c->gemm_counters, 0, sizeof(int) * 8192) != hipSuccess ||
+        hipMalloc((void**)&c->range, sizeof(unsigned) * 4) != hipSuccess ||
+        hipMemset(c->range, 0, sizeof(unsigned) * 4) != hipSuccess ||
+        hipHostMalloc((void**)&c->range_host, sizeof(unsigned) * 4, hipHostMallocDefault) != hipSuccess) {
         (void)hipFree(c->mse_partial);
-    (void)hipFree(c->gemm_counters);
+        (void)hipFree(c->gemm_counters);
+        (void)hipFree(c->range);
         delete c;
         return fail(AVSE_ERR_OOM, "hipMalloc failed (ctx)");
     }
@@ -953,6 +1020,9 @@ void avse_ctx_destroy(avse_ctx* c) {
     (void)hipFree(c->frames);
     (void)hipFree(c->umax);
     (void)hipFree(c->mse_partial);
+    (void)hipFree(c->gemm_counters);
+    (void)hipFree(c->range);
+    (void)hipHostFree(c->range_host);
     (void)hipFree(c->zero_video);
     (void)hipFree(c->arena);
     for (auto& g : c->graphs) (void)hipGraphExecDestroy(g.exec);
@@ -1155,6 +1225,10 @@ int avse_weights_load_shape(avse_ctx* c, const float* blob, int64_t n_floats, in
     W->dtype = dtype;
     W->device = c->device;
     W->plan = plan;
+    if (dtype == AVSE_F32_SPLIT) {
+        if (!c->opt.no_act_scale) act_exponents(plan, blob, W->act_exp);
+        W->blob.assign(blob, blob + n_floats);   // avse_forward_checked's exact-fp32 twin is built from it on demand
+    }
     const float* p = blob;
     for (int i = 0; i < kNumLayers; ++i) {
         const LayerDef& L = plan.L[i];
@@ -1174,7 +1248,7 @@ int avse_weights_load_shape(avse_ctx* c, const float* blob, int64_t n_floats, in
             W->d6_bias = bias[0];
             continue;
         }
-        int rc = build_layer(W, i, kernel, bias, bn, c->opt);
+        int rc = build_layer(W, i, kernel, bias, bn, c->opt, act_exp_in(W->act_exp, i), W->act_exp[i]);
         if (rc) { delete W; return rc; }
     }
     if (dtype == AVSE_F32_SPLIT) {
@@ -1190,6 +1264,12 @@ int avse_weights_load_shape(avse_ctx* c, const float* blob, int64_t n_floats, in
     return 0;
 }
 
+int avse_weights_act_exponents(const avse_weights* w, int* host_exp, int n) {
+    if (!w || !host_exp || n < 0) return fail(AVSE_ERR_INVALID, "bad act_exponents args");
+    for (int i = 0; i < n && i < kNumLayers; ++i) host_exp[i] = w->act_exp[i];
+    return 0;
+}
+
 void avse_weights_destroy(avse_weights* w) {
     if (!w) return;
     (void)hipSetDevice(w->device);
@@ -1200,8 +1280,9 @@ void avse_weights_destroy(avse_weights* w) {
 
 namespace {
 // Stage order of avse_forward_profile (include/avse.h AVSE_NUM_STAGES).
+// rflag: the split dtype's range-guard word the kernels report into (avse_ctx::range)
 int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const float* video, const float* vmean,
-                 const float* vstd, int64_t N, float* out, hipStream_t s, hipEvent_t* ev) {
+                 const float* vstd, int64_t N, float* out, hipStream_t s, hipEvent_t* ev, unsigned* rflag) {
     if (!c || !W || !audio || !out) return fail(AVSE_ERR_INVALID, "NULL argument");
     if ((vmean == nullptr) != (vstd == nullptr)) return fail(AVSE_ERR_INVALID, "vnorm_mean and vnorm_std must both be set or both NULL");
     if (!video && vmean) return fail(AVSE_ERR_INVALID, "video == NULL (all-zero video) takes no normaliser");
@@ -1220,8 +1301,12 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
     // (the next layer loads them as they are), except d_deconv5 (fused d_deconv6 -> float output, or fp32 unfused); the
     // layers fed by the fp32 preps (a_conv1, a generic v_conv1) split their fp32 input in the kernel
     const int cdt = split ? kConvSplit : gdt;
-    auto pairs = [&](ConvArgs& a, bool in_pairs, bool out_pairs) -> int {
+    // li: the layer's index in the plan (its range-guard bit)
+    auto pairs = [&](ConvArgs& a, bool in_pairs, bool out_pairs, int li) -> int {
         if (!split) return gdt;
+        a.range_flag = rflag;
+        a.range_bit = 1u << li;
+        a.range_in_bit = li == 0 ? kRangeAudioIn : kRangeVideoIn;   // the fp32 input split on load (a_conv1, v_conv1)
         if (in_pairs) {
             a.Ci *= 2;
             a.in_clip_stride *= 2;
@@ -1266,11 +1351,13 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
         g.counters = c->gemm_counters;
         return launch_gemm(g, mode, s);
     };
-    auto ksplit = [&](ConvArgs& a) {   // dense layers / v_conv6: split-K when the grid is small
+    // dense layers / v_conv6: split-K when the grid is small, partials at the split-K offset of the arena layout the
+    // launch's activations use (the N = 1 zero-video encoder has its own layout: its v_conv6 splits 36 ways)
+    auto ksplit = [&](ConvArgs& a, size_t partial_off) {
         if (a.nphase != 1) return;
         const int64_t M = (int64_t)a.N * a.Hq * a.Wq;
         a.ksplit = choose_ksplit(M, a.Co, a.ph[0].kpad, dt, a.ph[0].ntaps == 1, &a.ksplit_slabs);
-        a.partial = reinterpret_cast<float*>(c->arena + off[B_COUNT]);
+        a.partial = reinterpret_cast<float*>(c->arena + partial_off);
     };
     auto L = [&](int i) -> const GpuLayer& { return W->layers[i]; };
     int stage = 0;
@@ -1298,6 +1385,9 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
                     // a next split layer, fp32 for a generic one (weights_load keeps the split layers a prefix)
                     // every consumer (the next split layer or the generic v_conv6) takes the pair layout
                     h.split = 1;
+                    h.range_flag = rflag;
+                    h.range_bit = 1u << (5 + i);
+                    h.range_in_bit = kRangeVideoIn;
                     if (G.halo != HALO_V1) h.Ci = 2 * G.def.cin;
                     h.out_mode = OUT_S16;
                     h.out_clip_stride *= 2;
@@ -1316,8 +1406,8 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
             }
             ConvArgs a = (i < 5) ? conv_args(G, vb(v_in[i]), in_cs, vb(v_in[i + 1]), (long long)G.ho * G.wo * G.def.cout, G.def.cout, 0, n)
                                  : conv_args(G, vb(v_in[i]), in_cs, cat, CAT, G.def.cout, AEMB, n);  // concat[aemb:]
-            if (i == 5) ksplit(a);
-            const int dti = pairs(a, i > 0, true);   // v_conv1 generic: fp32 video-prep input
+            if (i == 5) ksplit(a, o[B_COUNT]);
+            const int dti = pairs(a, i > 0, true, 5 + i);   // v_conv1 generic: fp32 video-prep input
             if ((rc = launch_conv(a, split ? dti : cdt, s)) || (rc = mark())) return rc;
         }
         return 0;
@@ -1344,15 +1434,21 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
                 size_t o1[B_COUNT + 1];
                 arena_bytes(1, dt, opt, o1, P);
                 hipEvent_t* keep = ev;
+                unsigned* keep_flag = rflag;
                 const int keep_stage = stage;
                 ev = nullptr;   // the one-off N = 1 encoder is not a profiled stage
+                rflag = c->range + 2;   // its own range word: the bits are kept with the cached embedding
+                if (split) AVSE_HIP_CHECK(hipMemsetAsync(rflag, 0, sizeof(unsigned), s));
                 rc = video_encoder(c->zero_video, nullptr, nullptr, 1, o1, c->arena + o1[B_CAT]);
                 ev = keep;
+                rflag = keep_flag;
                 stage = keep_stage;
                 if (rc) { (void)hipFree(emb); return rc; }
                 AVSE_HIP_CHECK(hipMemcpyAsync(emb, c->arena + o1[B_CAT] + AEMB * es, 2048 * es, hipMemcpyDeviceToDevice, s));
+                if (split) AVSE_HIP_CHECK(hipMemcpyAsync(c->range_host + 2, c->range + 2, sizeof(unsigned), hipMemcpyDeviceToHost, s));
                 // one-time: the embedding is complete before any stream can see the pointer
                 AVSE_HIP_CHECK(hipStreamSynchronize(s));
+                W->vzero_range = split ? c->range_host[2] : 0u;
                 W->vzero_emb.store(emb, std::memory_order_release);
             }
         }
@@ -1411,7 +1507,7 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
         const long long in_cs = (long long)G.def.hin * G.def.win * (i == 0 ? G.cin_pad : G.def.cin);
         ConvArgs a = (i < 4) ? conv_args(G, buf(a_in[i]), in_cs, buf(a_in[i + 1]), (long long)G.ho * G.wo * G.def.cout, G.def.cout, 0, N)
                              : conv_args(G, buf(a_in[i]), in_cs, buf(B_CAT), CAT, G.def.cout, 0, N);   // Flatten -> concat[0:aemb]
-        const int dti = pairs(a, i > 0, true);   // a_conv1: fp32 audio-prep input
+        const int dti = pairs(a, i > 0, true, i);   // a_conv1: fp32 audio-prep input
         if ((rc = launch_conv(a, split ? dti : cdt, sa)) || (rc = mark())) return rc;
     }
     if (concurrent) AVSE_HIP_CHECK(hipEventRecord(c->join, sa));
@@ -1421,6 +1517,8 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
         // all-zero video: broadcast the constant embedding computed above
         const size_t es = dt == AVSE_BF16 ? 2 : 4;
         if ((rc = launch_broadcast_row(W->vzero_emb.load(std::memory_order_acquire), (char*)buf(B_CAT) + AEMB * es, N, 2048 * es, CAT * es, s))) return rc;
+        // an embedding that left the pair range reports it in every forward that broadcasts it
+        if (split && W->vzero_range && rflag && (rc = launch_flag_or(rflag, W->vzero_range, s))) return rc;
         for (int k = 0; k < 6; ++k)
             if ((rc = mark())) return rc;   // v_conv1..v_conv6 stages (the broadcast shows as v_conv1)
     }
@@ -1432,16 +1530,16 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
         if ((rc = gemm(L(13), buf(B_E2), EMB, buf(B_E3), AEMB, 0, 0, N)) || (rc = mark())) return rc;
     } else {
         ConvArgs a = conv_args(L(11), buf(B_CAT), CAT, buf(B_E1), EMB, EMB, 0, N);
-        ksplit(a);
-        int dti = pairs(a, true, true);
+        ksplit(a, off[B_COUNT]);
+        int dti = pairs(a, true, true, 11);
         if ((rc = launch_conv(a, split ? dti : cdt, s)) || (rc = mark())) return rc;
         a = conv_args(L(12), buf(B_E1), EMB, buf(B_E2), EMB, EMB, 0, N);
-        ksplit(a);
-        dti = pairs(a, true, true);
+        ksplit(a, off[B_COUNT]);
+        dti = pairs(a, true, true, 12);
         if ((rc = launch_conv(a, split ? dti : cdt, s)) || (rc = mark())) return rc;
         a = conv_args(L(13), buf(B_E2), EMB, buf(B_E3), AEMB, AEMB, 0, N);
-        ksplit(a);
-        dti = pairs(a, true, true);
+        ksplit(a, off[B_COUNT]);
+        dti = pairs(a, true, true, 13);
         if ((rc = launch_conv(a, split ? dti : cdt, s)) || (rc = mark())) return rc;
     }
     // audio decoder (network.py:112-135)
@@ -1497,12 +1595,12 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
             a.fuse_w = W->d6_w;
             a.fuse_bias = W->d6_bias;
             a.fuse_out = out;
-            const int dti = pairs(a, true, false);
+            const int dti = pairs(a, true, false, 14 + i);
             if ((rc = launch_conv(a, split ? dti : cdt, s)) || (rc = mark())) return rc;
             continue;
         }
         ConvArgs a = conv_args(G, buf(d_in[i]), in_cs, buf(d_in[i + 1]), (long long)G.ho * G.wo * G.def.cout, G.def.cout, 0, N);
-        const int dti = pairs(a, true, i < 4 || !opt.unfused_tail);   // an unfused d_deconv5 feeds launch_out_conv fp32
+        const int dti = pairs(a, true, i < 4 || !opt.unfused_tail, 14 + i);   // an unfused d_deconv5 feeds launch_out_conv fp32
         if ((rc = launch_conv(a, split ? dti : cdt, s)) || (rc = mark())) return rc;
     }
     if (opt.unfused_tail) {
@@ -1524,23 +1622,81 @@ extern "C" {
 // 2.14 ms (tools/graph_probe.py), but replaying the forward alone inside the same step measured 2.234 vs 2.24-2.26 ms
 // direct (bench.py A/B, same box), so direct launches stay the default.
 static int forward_dispatch(avse_ctx* c, const avse_weights* W, const float* audio, const float* video,
-                            const float* vmean, const float* vstd, int64_t N, float* out, void* stream);
+                            const float* vmean, const float* vstd, int64_t N, float* out, void* stream,
+                            unsigned* rflag);
 
 int avse_forward(avse_ctx* c, const avse_weights* W, const float* audio, const float* video, const float* vmean,
                  const float* vstd, int64_t N, float* out, void* stream) {
-    if (int rc = forward_dispatch(c, W, audio, video, vmean, vstd, N, out, stream)) return rc;
+    if (int rc = forward_dispatch(c, W, audio, video, vmean, vstd, N, out, stream, c ? c->range : nullptr)) return rc;
+    return avse::debug_poll(stream);
+}
+
+int avse_range_status(avse_ctx* c, void* stream, uint32_t* host_bits) {
+    if (!c || !host_bits) return fail(AVSE_ERR_INVALID, "NULL argument");
+    AVSE_HIP_CHECK(hipSetDevice(c->device));
+    hipStream_t s = (hipStream_t)stream;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    AVSE_HIP_CHECK(hipStreamIsCapturing(s, &cs));
+    if (cs != hipStreamCaptureStatusNone) return fail(AVSE_ERR_INVALID, "avse_range_status waits for its stream: not inside a capture");
+    AVSE_HIP_CHECK(hipMemcpyAsync(c->range_host, c->range, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+    AVSE_HIP_CHECK(hipMemsetAsync(c->range, 0, sizeof(unsigned), s));
+    AVSE_HIP_CHECK(hipStreamSynchronize(s));
+    *host_bits = c->range_host[0];
+    return 0;
+}
+
+int avse_forward_checked(avse_ctx* c, const avse_weights* W, const float* audio, const float* video, const float* vmean,
+                         const float* vstd, int64_t N, float* out, void* stream, int mode, uint32_t* host_bits) {
+    if (host_bits) *host_bits = 0;
+    if (!c || !W) return fail(AVSE_ERR_INVALID, "NULL argument");
+    if (mode != AVSE_RANGE_RECOMPUTE && mode != AVSE_RANGE_ERROR) return fail(AVSE_ERR_INVALID, "bad range mode");
+    if (W->dtype != AVSE_F32_SPLIT || N <= 0) return avse_forward(c, W, audio, video, vmean, vstd, N, out, stream);
+    AVSE_HIP_CHECK(hipSetDevice(c->device));
+    hipStream_t s = (hipStream_t)stream;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    AVSE_HIP_CHECK(hipStreamIsCapturing(s, &cs));
+    if (cs != hipStreamCaptureStatusNone)
+        return fail(AVSE_ERR_INVALID, "avse_forward_checked waits for its stream: capture avse_forward instead");
+    unsigned* flag = c->range + 1;
+    AVSE_HIP_CHECK(hipMemsetAsync(flag, 0, sizeof(unsigned), s));
+    // (option graph: the forward itself replays its hipGraph, so the launches after each wait are one graph launch)
+    if (int rc = forward_dispatch(c, W, audio, video, vmean, vstd, N, out, stream, flag)) return rc;
+    AVSE_HIP_CHECK(hipMemcpyAsync(c->range_host + 1, flag, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+    AVSE_HIP_CHECK(hipStreamSynchronize(s));
+    const unsigned bits = c->range_host[1];
+    if (host_bits) *host_bits = bits;
+    if (!bits) return avse::debug_poll(stream);
+    if (mode == AVSE_RANGE_ERROR)
+        return fail(AVSE_ERR_RANGE, "AVSE_F32_SPLIT: an activation left the f16 pair range (range bits 0x" +
+                                        [](unsigned b) { char t[16]; std::snprintf(t, sizeof(t), "%x", b); return std::string(t); }(bits) +
+                                        "): the outputs are not float32-accurate");
+    // recompute the batch on the exact-fp32 network (the same kernels as AVSE_F32 weights), built once from the blob
+    const avse_weights* twin = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(W->twin_mu);
+        if (!W->f32_twin) {
+            avse_weights* t = nullptr;
+            if (int rc = avse_weights_load_shape(c, W->blob.data(), (int64_t)W->blob.size(), AVSE_F32, W->plan.T, W->plan.F, &t))
+                return rc;
+            W->f32_twin = t;
+        }
+        twin = W->f32_twin;
+    }
+    if (int rc = forward_impl(c, twin, audio, video, vmean, vstd, N, out, s, nullptr, nullptr)) return rc;
     return avse::debug_poll(stream);
 }
 
 static int forward_dispatch(avse_ctx* c, const avse_weights* W, const float* audio, const float* video,
-                            const float* vmean, const float* vstd, int64_t N, float* out, void* stream) {
+                            const float* vmean, const float* vstd, int64_t N, float* out, void* stream,
+                            unsigned* rflag) {
     if (!c || !W || N <= 0 || !c->opt.graph)
-        return forward_impl(c, W, audio, video, vmean, vstd, N, out, (hipStream_t)stream, nullptr);
+        return forward_impl(c, W, audio, video, vmean, vstd, N, out, (hipStream_t)stream, nullptr, rflag);
     AVSE_HIP_CHECK(hipSetDevice(c->device));
     if (W->device != c->device) return fail(AVSE_ERR_INVALID, "weights and context are on different devices");
     int rc = ensure_arena(c, N, W->dtype, W->plan, (hipStream_t)stream);   // no allocation inside the capture
     if (rc) return rc;
-    const void* key[8] = {(const void*)W->serial, audio, video, vmean, vstd, out, c->arena, (const void*)c->arena_bytes};
+    const void* key[9] = {(const void*)W->serial, audio, video, vmean, vstd, out, c->arena, (const void*)c->arena_bytes,
+                          rflag};
     avse_ctx::Graph* hit = nullptr;
     for (auto& g : c->graphs)
         if (g.n == N && std::memcmp(&g.opt, &c->opt, sizeof(Options)) == 0 && std::memcmp(g.key, key, sizeof(key)) == 0)
@@ -1562,11 +1718,11 @@ static int forward_dispatch(avse_ctx* c, const avse_weights* W, const float* aud
         g.opt = c->opt;
         g.exec = nullptr;
         c->graphs.push_back(g);
-        return forward_impl(c, W, audio, video, vmean, vstd, N, out, (hipStream_t)stream, nullptr);
+        return forward_impl(c, W, audio, video, vmean, vstd, N, out, (hipStream_t)stream, nullptr, rflag);
     }
     if (!c->cap) AVSE_HIP_CHECK(hipStreamCreateWithFlags(&c->cap, hipStreamNonBlocking));
     AVSE_HIP_CHECK(hipStreamBeginCapture(c->cap, hipStreamCaptureModeRelaxed));
-    rc = forward_impl(c, W, audio, video, vmean, vstd, N, out, c->cap, nullptr);
+    rc = forward_impl(c, W, audio, video, vmean, vstd, N, out, c->cap, nullptr, rflag);
     hipGraph_t graph = nullptr;
     const hipError_t ce = hipStreamEndCapture(c->cap, &graph);
     if (rc || ce != hipSuccess) {
@@ -1588,7 +1744,7 @@ int avse_forward_profile(avse_ctx* c, const avse_weights* W, const float* audio,
     if (c) AVSE_HIP_CHECK(hipSetDevice(c->device));
     hipEvent_t ev[AVSE_NUM_STAGES + 1];
     for (int i = 0; i <= AVSE_NUM_STAGES; ++i) AVSE_HIP_CHECK(hipEventCreate(&ev[i]));
-    int rc = forward_impl(c, W, audio, video, vmean, vstd, N, out, (hipStream_t)stream, ev);
+    int rc = forward_impl(c, W, audio, video, vmean, vstd, N, out, (hipStream_t)stream, ev, c ? c->range : nullptr);
     if (!rc) {
         AVSE_HIP_CHECK(hipEventSynchronize(ev[AVSE_NUM_STAGES]));
         for (int i = 0; i < AVSE_NUM_STAGES; ++i) {

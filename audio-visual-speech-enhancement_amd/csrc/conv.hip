@@ -45,16 +45,18 @@ template <> __device__ __forceinline__ float from_f<float>(float v) { return v; 
 
 // one output value at element rowbase + n of a layer output: OutT (bf16 / fp32), or with a.out_s16 the split pair
 // layout (include/avse.h AVSE_F32_SPLIT: per pixel and 16 channels [h(16) | l(16)] f16; rowbase in halves)
+// Returns true when a pair cannot hold x (pair_out_of_range: the caller folds it into one range report).
 template <typename OutT>
-__device__ __forceinline__ void store_val(const ConvArgs& a, long long rowbase, int n, float x) {
+__device__ __forceinline__ bool store_val(const ConvArgs& a, long long rowbase, int n, float x) {
     if (a.out_s16) {
         _Float16* o = reinterpret_cast<_Float16*>(a.out) + rowbase + 32 * (n >> 4) + (n & 15);
         const _Float16 h = (_Float16)x;
         o[0] = h;
         o[16] = (_Float16)(x - (float)h);
-    } else {
-        reinterpret_cast<OutT*>(a.out)[rowbase + n] = from_f<OutT>(x);
+        return pair_out_of_range(x);
     }
+    reinterpret_cast<OutT*>(a.out)[rowbase + n] = from_f<OutT>(x);
+    return false;
 }
 
 struct RowInfo {
@@ -262,6 +264,7 @@ __global__ __launch_bounds__(256, (conv_occupancy<T, BN, FAST, S16>())) void k_c
         kc += SLAB;
         while (kc >= a.Ci) { kc -= a.Ci; ++kj; }
     };
+    bool in_bad = false;   // S16 on an fp32 input: an input value the pair split cannot hold (range guard)
     auto store_slab = [&](int buf, const i32x4 (&ra)[2], const i32x4 (&rb)[BCH]) {
         if constexpr (FAST && (KABL & 2)) {
             if (ra[0][0] == 0x7fffffff && rb[0][0] == 0x7fffffff) *reinterpret_cast<int*>(AS(buf)) = 1;
@@ -278,6 +281,7 @@ __global__ __launch_bounds__(256, (conv_occupancy<T, BN, FAST, S16>())) void k_c
                 for (int e = 0; e < 4; ++e) {
                     hi[e] = (_Float16)x[e];
                     lo[e] = (_Float16)(x[e] - (float)hi[e]);
+                    in_bad |= pair_out_of_range(x[e]);
                 }
                 char* rp = AS(buf) + row * 64 + (g & 1) * 8;
                 *reinterpret_cast<f16x4*>(rp + (((g >> 1) ^ swz(row)) << 4)) = hi;
@@ -387,6 +391,7 @@ __global__ __launch_bounds__(256, (conv_occupancy<T, BN, FAST, S16>())) void k_c
 
 #undef AS
 #undef BS
+    if constexpr (S16 && !PAIRS) range_report(a.range_flag, a.range_in_bit, in_bad);
     if constexpr (sizeof(T) == 4 || S16) {
 #pragma unroll
         for (int i = 0; i < NI; ++i)
@@ -481,6 +486,7 @@ __global__ __launch_bounds__(256, (conv_occupancy<T, BN, FAST, S16>())) void k_c
             return;
         }
     }
+    bool bad = false;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
         const int n = n0 + wn * WN + 16 * j + fr;
@@ -495,18 +501,19 @@ __global__ __launch_bounds__(256, (conv_occupancy<T, BN, FAST, S16>())) void k_c
                 if (orow[i][0] < 0) continue;
                 float x = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
                 if (a.act) x = x >= 0.f ? x : LRELU * x;
-                store_val<OutT>(a, orow[i][0], n, x);
+                bad |= store_val<OutT>(a, orow[i][0], n, x);
             } else {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     if (orow[i][r] < 0) continue;
                     float x = v[r];
                     if (a.act) x = x >= 0.f ? x : LRELU * x;
-                    store_val<OutT>(a, orow[i][r], n, x);
+                    bad |= store_val<OutT>(a, orow[i][r], n, x);
                 }
             }
         }
     }
+    if constexpr (S16) range_report(a.range_flag, a.range_bit, bad);
 }
 
 // split-K tail for k_conv's MFMA-native partials: one thread per f32x4 unit (4 rows of one column of one
@@ -519,6 +526,7 @@ __global__ void k_splitk_reduce_tiles(ConvArgs a) {
     const int mtiles = (M + BM - 1) / BM, tiles = mtiles * ((a.Co + BN - 1) / BN);
     const long long total = (long long)tiles * NIJ * 256;
     const f32x4* part = reinterpret_cast<const f32x4*>(a.partial);
+    bool bad = false;
     for (long long u = blockIdx.x * (long long)blockDim.x + threadIdx.x; u < total; u += (long long)gridDim.x * blockDim.x) {
         const int tid = (int)(u & 255), ij = (int)((u >> 8) % NIJ), tile = (int)((u >> 8) / NIJ);
         const int bx = tile % mtiles, by = tile / mtiles, i = ij / NJ, j = ij % NJ;
@@ -534,17 +542,18 @@ __global__ void k_splitk_reduce_tiles(ConvArgs a) {
             if (a.act) x = x >= 0.f ? x : LRELU * x;
             const int p = mb >> 2, pw = a.Wq >> 1, phh = a.Hq >> 1;
             const int clip = p / (phh * pw), rr = p - clip * phh * pw;
-            store_val<T>(a, clip * a.out_clip_stride + (long long)rr * a.out_pix_stride + a.out_c_off, n, x);
+            bad |= store_val<T>(a, clip * a.out_clip_stride + (long long)rr * a.out_pix_stride + a.out_c_off, n, x);
         } else {
             for (int r = 0; r < 4 && mb + r < M; ++r) {
                 float x = acc[r] * sc + sh;
                 if (a.act) x = x >= 0.f ? x : LRELU * x;
                 const int m = mb + r, clip = m / (a.Hq * a.Wq), rr = m - clip * a.Hq * a.Wq;
                 const int oy = (rr / a.Wq) * a.oys, ox = (rr % a.Wq) * a.oxs;
-                store_val<T>(a, clip * a.out_clip_stride + (long long)(oy * a.Wo + ox) * a.out_pix_stride + a.out_c_off, n, x);
+                bad |= store_val<T>(a, clip * a.out_clip_stride + (long long)(oy * a.Wo + ox) * a.out_pix_stride + a.out_c_off, n, x);
             }
         }
     }
+    range_report(a.range_flag, a.range_bit, bad);
 }
 
 // video [N][128][128][F] f32 -> (x - mean) / std -> T [N][128][128][8] (channels F..7 zero; F <= 8)
@@ -725,6 +734,17 @@ __global__ void k_broadcast_row(const char* __restrict__ src, char* __restrict__
         if (vec == 16) *reinterpret_cast<i32x4*>(dst + r * stride + j) = *reinterpret_cast<const i32x4*>(src + j);
         else dst[r * stride + j] = src[j];
     }
+}
+
+// range guard of a forward whose cached all-zero-video embedding was out of the pair range (capi.hip)
+__global__ void k_flag_or(unsigned* flag, unsigned bits) {
+    if (threadIdx.x == 0) atomicOr(flag, bits);
+}
+
+int launch_flag_or(unsigned* flag, unsigned bits, hipStream_t s) {
+    hipLaunchKernelGGL(k_flag_or, dim3(1), dim3(64), 0, s, flag, bits);
+    AVSE_HIP_CHECK(hipGetLastError());
+    return 0;
 }
 
 int launch_broadcast_row(const void* src, void* dst, int64_t rows, int64_t row_bytes, int64_t stride_bytes, hipStream_t s) {

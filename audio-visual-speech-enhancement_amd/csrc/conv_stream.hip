@@ -421,6 +421,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
         // output element (pooled pixel p, channel co): OUT_BF16 / OUT_F32 at p * out_pix_stride + out_c_off + co;
         // OUT_S16 (the next stream layer's split input, out_pix_stride = 2 Co) h at p * out_pix_stride + out_c_off +
         // 32 (co / 16) + co % 16 and l 16 halves further
+        bool range_bad = false;   // OUT_S16: range guard over all tiles (avse_common.h pair_out_of_range), reported once
         auto epilogue_m = [&](auto modec, int clip0, int oy0, int ox0) {
             constexpr int OM = decltype(modec)::value;
             constexpr int ES = OM == OUT_F32 ? 4 : 2;
@@ -444,6 +445,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
                     } else if constexpr (OM == OUT_S16) {
                         const _Float16 h = (_Float16)x;
                         const _Float16 l = (_Float16)(x - (float)h);
+                        range_bad |= pair_out_of_range(x);
                         __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, h), ors,
                                                               (pbase + 32 * j) * 2, 0, 0);
                         __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, l), ors,
@@ -608,6 +610,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
                 unsigned long long* pr = a.prof + ((size_t)blockIdx.x * 8 + wave) * 4;
                 pr[0] = p_work; pr[1] = p_wait; pr[2] = p_bar; pr[3] = (unsigned long long)t;
             }
+        if constexpr (S16) range_report(a.range_flag, a.range_bit, range_bad);
         return;
     }
     // fragment geometry (v_mfma_f32_32x32x16_bf16: lane l holds row/column l & 31 and k-half hi = l >> 5).

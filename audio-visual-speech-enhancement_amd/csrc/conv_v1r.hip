@@ -444,6 +444,7 @@ __global__ __launch_bounds__(64 * (CW + 4), 1) void k_conv_v1s(HaloArgs a) {
             }
         };
         // VideoNormalizer ((v - mean) / std: an IEEE division, the reference's numpy op), 'same' zero padding, split
+        bool in_bad = false;   // range guard of the split video input (avse_common.h pair_out_of_range)
         auto win_store = [&](auto set, int hs) {
             constexpr int Q = decltype(set)::value;
 #pragma unroll
@@ -461,6 +462,7 @@ __global__ __launch_bounds__(64 * (CW + 4), 1) void k_conv_v1s(HaloArgs a) {
                 for (int i = 0; i < 6; ++i) {
                     h[i] = (_Float16)f[i];
                     l[i] = (_Float16)(f[i] - (float)h[i]);
+                    in_bad |= pair_out_of_range(f[i]);
                 }
                 const int wy = P / HW, wx = P - wy * HW;
                 unsigned* dh = reinterpret_cast<unsigned*>(halo + hs * SSLOT + (wy * HWP + wx) * PB);
@@ -498,6 +500,7 @@ __global__ __launch_bounds__(64 * (CW + 4), 1) void k_conv_v1s(HaloArgs a) {
             iter(Q0{}, k);
             if (k + 1 < nmine) iter(Q1{}, k + 1);
         }
+        range_report(a.range_flag, a.range_in_bit, in_bad);
         return;
     }
 
@@ -573,6 +576,7 @@ __global__ __launch_bounds__(64 * (CW + 4), 1) void k_conv_v1s(HaloArgs a) {
     };
     const int Wp = a.Wc / 2;
     const long long cbytes = a.out_clip_stride * 2;
+    bool bad = false;   // range guard of the stored pairs
     auto epilogue = [&](int k) {
         int clip, oy0, ox0;
         tile_origin(k, clip, oy0, ox0);
@@ -590,6 +594,7 @@ __global__ __launch_bounds__(64 * (CW + 4), 1) void k_conv_v1s(HaloArgs a) {
                 x = fmaxf(x, LRELU * x);
                 const _Float16 h = (_Float16)x;
                 const _Float16 l = (_Float16)(x - (float)h);
+                bad |= pair_out_of_range(x);
                 if constexpr (V1S_ABL & 1) {
                     if (x == 12345.f) __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, h), ors, 0, 0, 0);
                     continue;
@@ -619,6 +624,7 @@ __global__ __launch_bounds__(64 * (CW + 4), 1) void k_conv_v1s(HaloArgs a) {
         tile(k, fa, fb, na, nb);
         if (k + 1 < nmine) tile(k + 1, na, nb, fa, fb);
     }
+    range_report(a.range_flag, a.range_bit, bad);
 }
 
 }  // namespace

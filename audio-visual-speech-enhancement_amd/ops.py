@@ -116,6 +116,7 @@ class DeviceWeights:
         self.dtype = DTYPES[dtype] if isinstance(dtype, str) else int(dtype)
         self.ctx = _lib.context(device)
         self.T, self.F = model.T, model.F
+        self.last_range_bits = 0
         blob = model.to_blob()
         # the CDLL is held here: at interpreter exit the module globals may be gone before this object
         self._cdll = _lib.load()
@@ -129,6 +130,12 @@ class DeviceWeights:
     @property
     def audio_shape(self):
         return (80, self.T)
+
+    def act_exponents(self):
+        """avse_weights_act_exponents: per plan layer, the power-of-two exponent its split-pair activations carry."""
+        e = (ctypes.c_int * 20)()
+        _lib.check(self._cdll.avse_weights_act_exponents(self.handle, e, 20), "avse_weights_act_exponents")
+        return dict(zip(_lib.LAYER_NAMES, list(e)))
 
     def __del__(self):
         h, lib = getattr(self, "handle", None), getattr(self, "_cdll", None)
@@ -158,13 +165,18 @@ def _check_forward_args(weights, audio, video, vnorm_mean, vnorm_std):
     return N
 
 
-def forward(weights, audio, video, vnorm_mean=None, vnorm_std=None, out=None):
+def forward(weights, audio, video, vnorm_mean=None, vnorm_std=None, out=None, checked=None, on_range="recompute"):
     """K2-K5: network forward.  audio [N, 80, 20], video [N, 128, 128, 5] float32 device tensors
     (video un-normalised when vnorm_* are given).  Returns [N, 80, 20] float32.  ([N, 80, T] / [N, 128, 128, F]
     for weights of another network shape, e.g. T = 24 at 29.97 fps.)
 
     video=None means an all-zero video input (BASELINE configs[2], the audio branch alone): the video
-    encoder's output is then one constant vector, computed once per weights object and broadcast."""
+    encoder's output is then one constant vector, computed once per weights object and broadcast.
+
+    checked (default: True for float32_split weights): avse_forward_checked — waits for the stream and, when an
+    activation left the f16 pair range, recomputes the batch on the exact-fp32 kernels (on_range="recompute") or raises
+    _lib.RangeError (on_range="error").  weights.last_range_bits holds the guard bits of the last checked call (0: every
+    pair in range).  checked=False: plain asynchronous avse_forward (read the guard later with Context.range_status)."""
     N = _check_forward_args(weights, audio, video, vnorm_mean, vnorm_std)
     if out is None:
         out = torch.empty((N, 80, weights.T), dtype=torch.float32, device=audio.device)
@@ -173,10 +185,25 @@ def forward(weights, audio, video, vnorm_mean=None, vnorm_std=None, out=None):
         raise ValueError(f"out must be [N, 80, {weights.T}] on the inputs' device")
     if N == 0:
         return out
+    if checked is None:
+        checked = weights.dtype == _lib.AVSE_F32_SPLIT
     with torch.cuda.device(audio.device):
-        _lib.check(_lib.load().avse_forward(weights.ctx.handle, weights.handle, _lib.ptr(audio), _lib.ptr(video),
-                                            _lib.ptr(vnorm_mean), _lib.ptr(vnorm_std), N, _lib.ptr(out),
-                                            _lib.stream_handle(audio.device)), "avse_forward")
+        if checked:
+            mode = {"recompute": _lib.AVSE_RANGE_RECOMPUTE, "error": _lib.AVSE_RANGE_ERROR}[on_range]
+            bits = ctypes.c_uint32()
+            rc = _lib.load().avse_forward_checked(weights.ctx.handle, weights.handle, _lib.ptr(audio), _lib.ptr(video),
+                                                  _lib.ptr(vnorm_mean), _lib.ptr(vnorm_std), N, _lib.ptr(out),
+                                                  _lib.stream_handle(audio.device), mode, ctypes.byref(bits))
+            weights.last_range_bits = bits.value
+            _lib.check(rc, "avse_forward_checked")
+            if bits.value:
+                import warnings
+                warnings.warn(f"float32_split forward of {N} clips: {_lib.range_bit_names(bits.value)} left the f16 pair "
+                              "range; the batch was recomputed on the exact-fp32 kernels", RuntimeWarning, stacklevel=2)
+        else:
+            _lib.check(_lib.load().avse_forward(weights.ctx.handle, weights.handle, _lib.ptr(audio), _lib.ptr(video),
+                                                _lib.ptr(vnorm_mean), _lib.ptr(vnorm_std), N, _lib.ptr(out),
+                                                _lib.stream_handle(audio.device)), "avse_forward")
     return out
 
 

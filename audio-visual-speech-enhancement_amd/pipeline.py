@@ -29,6 +29,7 @@ class Enhancer:
         self.sr = int(sample_rate)
         self.slice_ms = slice_duration_ms
         self.chunk = int(chunk)
+        self.range_bits = 0
 
     def geometry(self, n_video_slices):
         return data_processor.frame_geometry(self.sr, self.slice_ms, n_video_slices, self.fps)
@@ -63,9 +64,11 @@ class Enhancer:
         clips = mel.view(n, data_processor.N_MELS, spf)
         frames = video.reshape((n,) + tuple(video.shape[2:]))
         pred = torch.empty_like(clips)
+        self.range_bits = 0     # float32_split: range-guard bits of this call's chunks (recomputed on exact fp32)
         for a in range(0, n, self.chunk):
             b = min(n, a + self.chunk)
             ops.forward(self.weights, clips[a:b], frames[a:b], vmean, vstd, out=pred[a:b])
+            self.range_bits |= getattr(self.weights, "last_range_bits", 0)
         if ev:
             ev[2].record()
         out = ops.istft(pred.view(U, S, data_processor.N_MELS, spf), stft, sample_rate=self.sr, n_fft=g["n_fft"],

@@ -281,19 +281,30 @@ def predict_samples(samples, predictor, run_dir, world=1, rank=0, write=write_pr
     return losses
 
 
-def _launch_ranks(n):
-    """`predict -g N` outside a launcher: one rank per GPU as a child torch.distributed.run (rendezvous on
-    127.0.0.1), same arguments; nothing in this process has touched the GPU."""
+# the reference-shaped command line (repo root speech_enhancer.py): what every rank of `predict -g N` runs
+ENTRY_SCRIPT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "speech_enhancer.py")
+
+
+def rank_command(n, argv, port):
+    """The torch.distributed.run command line of `predict -g N`: one rank per GPU (rendezvous on 127.0.0.1), each
+    running the entry script with the same arguments `main` parsed (argv, not sys.argv: main(argv) may be called
+    programmatically, or the CLI run as a module)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}", "--master-addr",
+            "127.0.0.1", "--master-port", str(port), ENTRY_SCRIPT] + list(argv)
+
+
+def _launch_ranks(n, argv):
+    """`predict -g N` outside a launcher: the ranks as a child process group; nothing in this process has touched the
+    GPU."""
     with socket.socket() as sk:
         sk.bind(("127.0.0.1", 0))
         port = sk.getsockname()[1]
-    return subprocess.call([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
-                            "--master-addr", "127.0.0.1", "--master-port", str(port), sys.argv[0]] + sys.argv[1:])
+    return subprocess.call(rank_command(n, argv, port))
 
 
 def predict(args):
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        sys.exit(_launch_ranks(args.gpus))
+        sys.exit(_launch_ranks(args.gpus, args.argv))
     world, rank = int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0"))
     layout = Layout(args.base_dir)
     model_path, keras_path = layout.model_file(args.model), layout.keras_model_file(args.model)
@@ -362,7 +373,9 @@ def main(argv=None):
     q.add_argument("--per-sample", action="store_true", help="one forward / STFT / ISTFT per sample (unbatched)")
     q.set_defaults(func=predict)
 
+    argv = sys.argv[1:] if argv is None else list(argv)
     args = parser.parse_args(argv)
+    args.argv = argv
     args.func(args)
 
 

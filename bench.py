@@ -378,7 +378,7 @@ def run_e2e(args, world, rank, dev, model):
     res = {"metric": "clips/sec end-to-end predict (STFT -> fusion CNN -> ISTFT) on 200-ms@16kHz segments",
            "value": round(clips * args.steps / elapsed, 1), "unit": "clips/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True,
-           "scaling": "strong", "vs_baseline": None, "dtype": "bf16" if args.dtype == "bf16" else "fp32",
+           "scaling": "strong", "vs_baseline": None, "dtype": args.dtype,
            "arithmetic": ARITHMETIC[args.dtype],
            "data": "synthetic on device: int16-scale noise+tone 3-s utterances, uint8-valued mouth crops; "
                    "random-init Keras-layout weights",
@@ -415,6 +415,10 @@ def main():
     ap.add_argument("--dtype", default="fp32_split", choices=["fp32_split", "fp32", "bf16"],
                     help="headline compute dtype (fp32_split / fp32 meet the north star's 1e-4 RMS; bf16 does not)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--graph", action="store_true", help="the forward replays a hipGraph per argument set (option graph)")
+    ap.add_argument("--checked", action="store_true",
+                    help="fp32_split: avse_forward_checked per step (default: avse_forward, the sticky range guard read "
+                         "once after the timed steps)")
     ap.add_argument("--no-legs", action="store_true", help="skip the configs[1] / configs[2] legs")
     ap.add_argument("--profile-reps", type=int, default=5)
     ap.add_argument("--e2e", action="store_true", help="BASELINE configs[4]: end-to-end predict, utterance-sharded")
@@ -479,9 +483,18 @@ def main():
     padded = torch.zeros((per, 80, 20), dtype=torch.float32, device=dev)
     gathered = torch.empty((world * per, 80, 20), dtype=torch.float32, device=dev) if world > 1 else None
 
+    # fp32_split range guard: every kernel of every timed step reports an out-of-range pair into the context's sticky
+    # guard word, read once after the timed region (range_guard.bits: 0 = every timed output fp32-accurate).  --checked
+    # runs avse_forward_checked per step instead (a stream wait per step, the per-batch contract of the CLI / predict
+    # path; its throughput is reported as range_guard.checked_per_step_clips_per_s either way)
+    checked = args.checked
+    dw.ctx.range_status()
+    if args.graph:
+        dw.ctx.set_option("graph", 1)
+
     def step():
         ops.spectrogram(audio, frames_per_slice=20, out=mel)          # [B, 1, 80, 20]
-        ops.forward(dw, mel.view(B, 80, 20), video, mean, std, out=out)
+        ops.forward(dw, mel.view(B, 80, 20), video, mean, std, out=out, checked=checked)
         if world > 1:
             padded[:B].copy_(out)
             dist.all_gather_into_tensor(gathered, padded)
@@ -508,6 +521,28 @@ def main():
     value = global_batch * args.steps / elapsed
     ms_per_step = 1e3 * elapsed / args.steps
     timed_out = out.cpu().numpy()
+    bits = dw.ctx.range_status() | (dw.last_range_bits if checked else 0)
+    if world > 1:
+        every = [0] * world
+        dist.all_gather_object(every, bits)
+        bits = 0
+        for b in every:
+            bits |= b
+    range_guard = {"checked_every_step": bool(checked and args.dtype == "fp32_split"), "bits": bits,
+                   "layers_out_of_range": _lib.range_bit_names(bits),
+                   "read": "per step (avse_forward_checked)" if checked else
+                           "sticky guard word of all timed steps, read after the timed region (avse_range_status)",
+                   "act_exponents_nonzero": {k: v for k, v in dw.act_exponents().items() if v}}
+    if args.dtype == "fp32_split" and world == 1 and not checked:
+        # the per-batch checked path (what speech_enhancer predict / pipeline.Enhancer run), same batch, 20 steps
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(20):
+            ops.spectrogram(audio, frames_per_slice=20, out=mel)
+            ops.forward(dw, mel.view(B, 80, 20), video, mean, std, out=out, checked=True)
+        torch.cuda.synchronize()
+        range_guard["checked_per_step_clips_per_s"] = round(B * 20 / (time.perf_counter() - t1), 1)
+        range_guard["checked_per_step_bits"] = dw.last_range_bits
 
     # ---- live per-kernel durations (HIP events on the launch stream) for the roofline ----
     stage_ms = {}
@@ -529,7 +564,10 @@ def main():
     peak = PEAK_TFLOPS[args.dtype]
     pmc_file, pmc, pmc_status = pmc_summary(B, args.dtype)
     kp = (pmc or {}).get("kernels", {}).get(dom, {})
-    ksym, rp_ms = kernel_stat((pmc or {}).get("kernel_stats_avg_ms"), args.dtype)
+    # rocprof average over the headline-batch launches of the profiled run (kernel trace filtered by grid: the --stats
+    # average also counts the configs[2] leg's one-clip zero-video launch; tools/pmc_summary.py)
+    ksym, rp_ms = kernel_stat((pmc or {}).get("kernel_trace_headline_avg_ms"), args.dtype)
+    _, rp_all_ms = kernel_stat((pmc or {}).get("kernel_stats_avg_ms"), args.dtype)
     fwd_ms = sum(stage_ms.values())
     kdesc = {"bf16": "k_conv_stream<5,16,16,1> bf16: persistent warp-specialised implicit GEMM M=4096/clip N=128 "
                      "K=3200, fused BN+LReLU+2x2 maxpool",
@@ -548,8 +586,9 @@ def main():
         "higher_is_better": True,
         "scaling": "strong" if args.strong else "weak",
         "vs_baseline": None,
-        "dtype": "bf16" if args.dtype == "bf16" else "fp32",
+        "dtype": args.dtype,
         "arithmetic": ARITHMETIC[args.dtype],
+        "range_guard": range_guard,
         "data": "synthetic: seeded int16-scale noise+harmonic audio (3200 samples/clip), uint8-valued 128x128x5 "
                 "mouth crops, random-init Keras-layout weights with randomised BN; inputs resident in HBM",
         "config": {"workload": "STFT (n_fft 640, hop 160, 80 mel, dB) + full audio-visual fusion forward "
@@ -565,10 +604,15 @@ def main():
                      "source_digest": _lib.source_digest(),
                      "per_launch_flop": FLOP_V_CONV2 * B, "avg_launch_ms": round(stage_ms[dom], 4),
                      "timing": "avg_launch_ms: HIP events on the launch stream in this run; avg_launch_ms_rocprof / "
-                               "frac_rocprof: rocprofv3 --kernel-trace --stats average of the same source tree "
-                               "(profiles/<tag>_kernel_stats.csv, a separate profiled run)",
+                               "frac_rocprof: rocprofv3 --kernel-trace average of the same source tree's B = 512 "
+                               "launches (profiles/<tag>_pmc.json kernel_trace_headline_avg_ms, a separate profiled "
+                               "run); avg_launch_ms_rocprof_stats: the --stats average over every launch of the symbol "
+                               "(profiles/<tag>_kernel_stats.csv), which also counts the configs[2] leg's N = 1 launch",
                      "avg_launch_ms_rocprof": rp_ms,
                      "frac_rocprof": round(FLOP_V_CONV2 * B / (rp_ms * 1e-3) / 1e12 / peak, 4) if rp_ms else None,
+                     "avg_launch_ms_rocprof_stats": rp_all_ms,
+                     "frac_pmc_profiled": (round(FLOP_V_CONV2 * B / (kp["profiled_ns"] * 1e-9) / 1e12 / peak, 4)
+                                           if kp.get("profiled_ns") else None),
                      "achieved_vs_fp32_mfma_peak": round(achieved / PEAK_TFLOPS["fp32"], 4)},
         "breakdown": {
             "stft_ms": round(stft_ms, 4),

@@ -29,8 +29,10 @@ extern "C" {
 #endif
 
 /* 2: compute dtype AVSE_F32_SPLIT, avse_ctx_reserve_weights; option names tile_alt / aud_side removed (round 3);
- *    status AVSE_ERR_CHECK (checked build) */
-#define AVSE_ABI_VERSION 2
+ *    status AVSE_ERR_CHECK (checked build)
+ * 3: AVSE_F32_SPLIT range guard (avse_forward_checked, avse_range_status, status AVSE_ERR_RANGE), per-layer activation
+ *    exponents (avse_weights_act_exponents, option no_act_scale) */
+#define AVSE_ABI_VERSION 3
 
 enum avse_status {
     AVSE_OK = 0,
@@ -38,7 +40,8 @@ enum avse_status {
     AVSE_ERR_HIP = 2,          /* HIP runtime error (message in avse_last_error)       */
     AVSE_ERR_UNSUPPORTED = 3,  /* configuration outside what the kernels implement      */
     AVSE_ERR_OOM = 4,          /* device allocation failed                             */
-    AVSE_ERR_CHECK = 5         /* checked build only: a device-side protocol / bounds check fired */
+    AVSE_ERR_CHECK = 5,        /* checked build only: a device-side protocol / bounds check fired */
+    AVSE_ERR_RANGE = 6         /* avse_forward_checked(AVSE_RANGE_ERROR): a split-f16 activation left the f16 range */
 };
 
 /* Compute dtypes of avse_weights_load (inputs, outputs and accumulation are float32 in all three):
@@ -53,8 +56,12 @@ enum avse_status {
  *                   (about 22 significant bits; the float32 network inputs are split on load, the decoder's last
  *                   output is float32): whole-network error measured 1.3x AVSE_F32's (6.8e-5 vs
  *                   5.1e-5 absolute RMS on dB-scale outputs, tests/test_gpu_split.py), inside the north star's 1e-4.
- *                   Activations of these layers must stay below 65504 in magnitude (f16 range; BatchNormalization
- *                   keeps a trained network's far below). */
+ *                   Range: a pair holds |x| < 65520 (f16 overflow) at ~22 bits from 2^-3 up.  Each layer stores the
+ *                   pairs of x 2^e_L with a power-of-two exponent e_L from its BatchNormalization parameters (0 for
+ *                   layers whose |beta| + |gamma| lies in [2^-2, 2^8]; avse_weights_act_exponents), and every kernel
+ *                   that stores a pair (or splits an fp32 input) reports a value outside the range into a range guard:
+ *                   avse_forward_checked recomputes such a batch on the exact-fp32 kernels (or fails with
+ *                   AVSE_ERR_RANGE); after plain avse_forward calls avse_range_status tells whether any did. */
 enum avse_dtype { AVSE_F32 = 0, AVSE_BF16 = 1, AVSE_F32_SPLIT = 2 };
 enum avse_pad_mode { AVSE_PAD_REFLECT = 0, AVSE_PAD_CONSTANT = 1 };
 
@@ -83,6 +90,7 @@ void avse_ctx_destroy(avse_ctx* ctx);
  *   graph (AVSE_GRAPH)               avse_forward replays a hipGraph per argument set
  *   gemm_ksplit_cap (AVSE_GEMM_KSPLIT) cap on k_gemm's split-K factor (0 = none)
  *   dense_istft (AVSE_DENSE_ISTFT)   avse_istft through the dense pinv + frame scratch + overlap-add pass
+ *   no_act_scale (AVSE_NO_ACT_SCALE) AVSE_F32_SPLIT weights loaded afterwards keep every activation exponent 0
  * Unknown names return AVSE_ERR_INVALID. */
 int avse_ctx_set_option(avse_ctx* ctx, const char* name, int value);
 int avse_ctx_get_option(avse_ctx* ctx, const char* name, int* value);
@@ -186,6 +194,28 @@ void avse_weights_destroy(avse_weights* w);
 int avse_forward(avse_ctx* ctx, const avse_weights* w, const float* audio, const float* video,
                  const float* vnorm_mean, const float* vnorm_std, int64_t N, float* out,
                  void* stream);
+
+/* avse_forward for AVSE_F32_SPLIT weights with the range guard read back: waits for `stream` after the forward (not
+ * capturable) and, when a stored activation or a split input left the f16 pair range (|x| >= 65520 or NaN; bit i of
+ * *host_bits = plan layer i, a_conv1 = 0 .. d_deconv5 = 18; bit 24 the audio input, bit 25 the video input):
+ *   mode AVSE_RANGE_RECOMPUTE  recomputes the whole batch on the exact-fp32 kernels (the AVSE_F32 path of the same
+ *                              network, built once per weights object from the blob they were loaded from) into `out`
+ *                              and returns AVSE_OK — the outputs are then the AVSE_F32 forward's;
+ *   mode AVSE_RANGE_ERROR      returns AVSE_ERR_RANGE (outputs not float32-accurate).
+ * host_bits (nullable) receives the bits (0: every pair was in range).  Other dtypes: avse_forward, *host_bits = 0. */
+enum avse_range_mode { AVSE_RANGE_RECOMPUTE = 0, AVSE_RANGE_ERROR = 1 };
+int avse_forward_checked(avse_ctx* ctx, const avse_weights* w, const float* audio, const float* video,
+                         const float* vnorm_mean, const float* vnorm_std, int64_t N, float* out, void* stream,
+                         int mode, uint32_t* host_bits);
+
+/* Range-guard bits (as avse_forward_checked's) raised by the AVSE_F32_SPLIT forwards of plain avse_forward /
+ * avse_forward_profile calls on this context since the last avse_range_status; waits for `stream` (the stream those
+ * forwards ran on) and clears them. */
+int avse_range_status(avse_ctx* ctx, void* stream, uint32_t* host_bits);
+
+/* AVSE_F32_SPLIT: the activation exponent e_L of each plan layer (host_exp[0..n), n <= 20; layer L stores the pairs of
+ * x 2^e_L); 0 for every layer of the other dtypes. */
+int avse_weights_act_exponents(const avse_weights* w, int* host_exp, int n);
 
 /* Stages of the forward pass, in launch order (avse_forward_profile). */
 #define AVSE_NUM_STAGES 22

@@ -84,7 +84,9 @@ def scratch(dw, N, clips=None, names=None):
             # split-pair layout (include/avse.h AVSE_F32_SPLIT): per pixel and 16 channels [h(16) | l(16)] f16
             shp = BUF_SHAPES[name]
             hl = t.view(torch.float16).float().cpu().numpy().reshape((len(clips),) + shp[:-1] + (shp[-1] // 16, 2, 16))
-            out[name] = (hl[..., 0, :].astype(np.float64) + hl[..., 1, :]).reshape((len(clips),) + shp)
+            # the pairs hold x 2^e of the producing layer (avse_weights_act_exponents; concat: a_conv5 = v_conv6)
+            e = dw.act_exponents()["a_conv5" if name == "concat" else name]
+            out[name] = np.ldexp((hl[..., 0, :].astype(np.float64) + hl[..., 1, :]).reshape((len(clips),) + shp), -e)
         else:
             out[name] = t.float().cpu().numpy().reshape((len(clips),) + BUF_SHAPES[name])
     return out

@@ -80,3 +80,29 @@ def test_enhancer_rejects_mismatched_geometry(gpu):
     sig = torch.zeros((2, 48000), device="cuda")
     with pytest.raises(ValueError):
         enh(sig, torch.zeros((3, 15, 128, 128, 5), device="cuda"))
+
+
+def test_enhancer_split_1024_chunks_many_utterances(gpu):
+    """The credited dtype end to end at the bench's e2e geometry (bench.py --e2e: forward chunks of 1024 clips): 72
+    3-s utterances (1,080 clips: one full 1024-clip chunk and a ragged 56-clip one) through K1 -> split forward ->
+    K6 in one Enhancer call; utterances on both sides of the chunk boundary and at the ends against the oracle pipeline
+    (speech_enhancer.py:61-88 per sample, float64 forward)."""
+    from avse_amd import ops
+    from avse_amd.model import KerasModel
+    from avse_amd.pipeline import Enhancer
+    U, S = 72, 15
+    rng = np.random.default_rng(72)
+    x = synth_audio(rng, U, 48000)
+    video = synth_video(rng, U * S).reshape(U, S, 128, 128, 5)
+    mean, std = R.video_normalizer_fit(video.reshape(U * S, 128, 128, 5))
+    model = KerasModel.init(seed=21, randomize=True)
+    dw = ops.DeviceWeights(model, "float32_split")
+    enh = Enhancer(dw, chunk=1024)
+    got = enh(ops.to_device(x), ops.to_device(video), ops.to_device(mean), ops.to_device(std)).cpu().numpy()
+    assert got.shape == (U, 160 * (S * 20 - 1)) and np.isfinite(got).all()
+    assert enh.range_bits == 0
+    for u in (0, 1, 1023 // S, 1024 // S, 1025 // S, U - 1):     # utterance 68 straddles clips 1020..1034
+        ref, _ = oracle_enhance(model, x[u], video[u], mean, std)
+        err = rel_rms(got[u], ref)
+        print(f"split e2e utterance {u}: waveform rel RMS {err:.3e}")
+        assert err <= 1e-4, (u, err)

@@ -45,10 +45,11 @@ def test_split_intermediates(gpu):
             assert rel_rms(sc[k], inter[k]) <= FP32_REL, (k, rel_rms(sc[k], inter[k]))
 
 
-@pytest.mark.parametrize("N", [5, 301, 512])
+@pytest.mark.parametrize("N", [5, 301, 512, 1024])
 def test_split_bench_batch_matches_oracle(gpu, N):
     """The launch bench.py times in the split dtype (its inputs, normaliser, 512 clips; N = 301 and 5 leave ragged
-    4-clip v_conv5 tiles): output and every materialised layer of spread clips against the float64 oracle."""
+    4-clip v_conv5 tiles; N = 1024 is the forward chunk of the end-to-end configs[4] run, pipeline.Enhancer): output and
+    every materialised layer of spread clips against the float64 oracle."""
     import bench
     from avse_amd import ops
     from avse_amd.model import KerasModel
@@ -65,7 +66,8 @@ def test_split_bench_batch_matches_oracle(gpu, N):
     inter = {}
     vn = R.video_normalize(video_np[clips], mean_np, std_np).astype(np.float32)
     ref = K.forward(model.layer_dict(), mel_np, vn, intermediates=inter)
-    names = ["v_conv1", "v_conv2", "v_conv3", "v_conv4", "v_conv5", "concat"]
+    names = ["v_conv1", "v_conv2", "v_conv3", "v_conv4", "v_conv5", "concat", "enc_dense", "dec_dense1", "dec_dense2",
+             "d_deconv1", "d_deconv2", "d_deconv3", "d_deconv4"]
     sc = scratch(dw, N, clips, names)
     layers = {k: rel_rms(sc[k], inter[k]) for k in names}
     ae = abs_rms(out[clips], ref)
@@ -75,6 +77,42 @@ def test_split_bench_batch_matches_oracle(gpu, N):
     assert rel_rms(out[clips], ref) <= FP32_REL
     for k, e in layers.items():
         assert e <= FP32_REL, (k, e)
+
+
+@pytest.mark.parametrize("N", [120, 256])
+def test_split_zero_video_batches(gpu, N):
+    """video = None at the sizes the bench and the workspace plan care about: N = 256 is BASELINE configs[2]'s
+    audio-branch batch (bench leg audio_fp32_split_b256); N = 120 sizes the split-K workspace for the dense layers only,
+    while the one-clip zero-video encoder's v_conv6 splits 36 ways (it must use its own arena layout: ADVICE r4)."""
+    from avse_amd import ops
+    from avse_amd.model import KerasModel
+    model = db_scale(KerasModel.init(seed=12, randomize=True))
+    rng = np.random.default_rng(N)
+    mel = rng.normal(-40, 15, (N, 80, 20)).astype(np.float32)
+    dw = ops.DeviceWeights(model, SPLIT)
+    got = ops.forward(dw, ops.to_device(mel), None).cpu().numpy()
+    clips = spread_clips(N, k=12)
+    ref = K.forward(model.layer_dict(), mel[clips], None)
+    ae, re = abs_rms(got[clips], ref), rel_rms(got[clips], ref)
+    print(f"split zero video N={N}: abs {ae:.3e} rel {re:.3e}")
+    assert np.isfinite(got).all() and ae <= FP32_ABS and re <= FP32_REL
+    assert dw.last_range_bits == 0
+
+
+def test_fp32_zero_video_large_batch(gpu):
+    """AVSE_F32 with video = None at N = 4096: no layer splits K at that batch, so the forward's own split-K workspace
+    is empty, while the one-clip zero-video encoder's v_conv6 splits (it wrote past the arena)."""
+    from avse_amd import ops
+    from avse_amd.model import KerasModel
+    N = 4096
+    model = KerasModel.init(seed=13, randomize=True)
+    rng = np.random.default_rng(4096)
+    mel = rng.normal(-40, 15, (N, 80, 20)).astype(np.float32)
+    dw = ops.DeviceWeights(model, "float32")
+    got = ops.forward(dw, ops.to_device(mel), None).cpu().numpy()
+    clips = spread_clips(N, k=8)
+    ref = K.forward(model.layer_dict(), mel[clips], None)
+    assert np.isfinite(got).all() and rel_rms(got[clips], ref) <= FP32_REL
 
 
 def test_split_zero_video(gpu):

@@ -42,7 +42,7 @@ def test_abi_version_and_blob_size():
     from avse_amd import _lib
     from avse_amd.model import blob_floats
     lib = _lib.load()
-    assert lib.avse_abi_version() == _lib.ABI_VERSION == 2
+    assert lib.avse_abi_version() == _lib.ABI_VERSION == 3
     assert lib.avse_weights_blob_floats() == blob_floats()
 
 
@@ -52,6 +52,12 @@ def test_null_arguments_are_rejected_without_gpu_work():
     rc = lib.avse_ctx_create(0, None)
     assert rc == 1 and b"NULL" in lib.avse_last_error()
     rc = lib.avse_forward(None, None, None, None, None, None, 1, None, None)
+    assert rc == 1
+    rc = lib.avse_forward_checked(None, None, None, None, None, None, 1, None, None, 0, None)
+    assert rc == 1
+    rc = lib.avse_range_status(None, None, None)
+    assert rc == 1
+    rc = lib.avse_weights_act_exponents(None, None, 0)
     assert rc == 1
 
 
@@ -201,3 +207,16 @@ def test_checked_build_harness_host_part():
 def test_release_and_checked_build_flags():
     from avse_amd import _lib
     assert _lib.load().avse_build_flags() == (1 if "debug" in os.path.basename(_lib.LIB_PATH) else 0)
+
+
+def test_predict_rank_command_threads_argv():
+    """`predict -g N` relaunches the reference-shaped entry script with the arguments main() parsed (it used
+    sys.argv, wrong for main(argv) and for module invocations)."""
+    import os
+    from avse_amd import speech_enhancer as se
+    argv = ["-bd", "/tmp/base", "predict", "-mn", "m", "-dn", "d", "-g", "2"]
+    cmd = se.rank_command(2, argv, 12345)
+    assert cmd[cmd.index("--nproc-per-node=2")] and "--master-port" in cmd and cmd[cmd.index("--master-port") + 1] == "12345"
+    i = cmd.index(se.ENTRY_SCRIPT)
+    assert cmd[i + 1:] == argv
+    assert os.path.isfile(se.ENTRY_SCRIPT) and os.path.basename(se.ENTRY_SCRIPT) == "speech_enhancer.py"
