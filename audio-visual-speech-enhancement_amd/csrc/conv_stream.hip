@@ -63,8 +63,18 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, lo
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, nrec, 0x00020000);
 }
 
-__device__ __forceinline__ i32x4 ld16(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
-    return __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0);
+// cache-policy bits of the loaders' global loads (gfx950 buffer aux: 1 = sc0, 2 = nt, 16 = sc1), A/B switches
+#ifndef AVSE_HALO_AUX
+#define AVSE_HALO_AUX 0
+#endif
+#ifndef AVSE_WGT_AUX
+#define AVSE_WGT_AUX 0
+#endif
+__device__ __forceinline__ i32x4 ld16(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {   // input window pieces
+    return __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, AVSE_HALO_AUX);
+}
+__device__ __forceinline__ i32x4 ld16w(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {  // weight slices
+    return __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, AVSE_WGT_AUX);
 }
 __device__ __forceinline__ void st16(char* p, i32x4 v) { *reinterpret_cast<i32x4*>(p) = v; }
 
@@ -249,12 +259,12 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
 #pragma unroll
         for (int s = 0; s <= BP; ++s)
 #pragma unroll
-            for (int u = 0; u < 2; ++u) st16(wdst + s * WSLOT + 1024 * u, ld16(wrs, wvoff[u], (s % spt) * wslice));
+            for (int u = 0; u < 2; ++u) st16(wdst + s * WSLOT + 1024 * u, ld16w(wrs, wvoff[u], (s % spt) * wslice));
         i32x4 rw[LAT][2], rp[LAT];
         [&]<int... S>(std::integer_sequence<int, S...>) {
             ([&] {
-                 rw[S][0] = ld16(wrs, wvoff[0], ((S + BP + 1) % spt) * wslice);
-                 rw[S][1] = ld16(wrs, wvoff[1], ((S + BP + 1) % spt) * wslice);
+                 rw[S][0] = ld16w(wrs, wvoff[0], ((S + BP + 1) % spt) * wslice);
+                 rw[S][1] = ld16w(wrs, wvoff[1], ((S + BP + 1) % spt) * wslice);
                  constexpr int vt = NTAP - LAT + S;   // tap of virtual step S - LAT
                  if constexpr (vt < HPW && !(ABL & 1)) rp[S] = ld16(cur_rs, vo_cur[vt < HPW ? vt : 0], 64);
              }(), ...);
@@ -324,8 +334,8 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
                 piece_store(std::integral_constant<int, (tl < HPW ? tl : 0)>{}, lprev ? pd_prev : pd_cur, rp[S]);
             // 2. this step's loads
             if constexpr (!(ABL & 2)) {
-                rw[S][0] = ld16(wrs, wvoff[0], woff);
-                rw[S][1] = ld16(wrs, wvoff[1], woff);
+                rw[S][0] = ld16w(wrs, wvoff[0], woff);
+                rw[S][1] = ld16w(wrs, wvoff[1], woff);
             }
             if constexpr (tap < HPW && !(ABL & 1)) rp[S] = ld16(prs, vsel[tap < HPW ? tap : 0], psoff);
             woff += wslice;

@@ -89,16 +89,18 @@ def test_keras_h5_shape_mismatch_is_an_error(tmp_path):
 
 @needs_h5py
 @pytest.mark.gpu
-def test_converted_keras_h5_runs_forward_against_oracle(tmp_path, gpu):
+@pytest.mark.parametrize("dtype", ["float32", "float32_split"])
+def test_converted_keras_h5_runs_forward_against_oracle(tmp_path, gpu, dtype):
     """SpeechEnhancementNetwork.load of a Keras model file (network.py:222-226), end to end: a Keras-2-layout
-    HDF5 file -> tools/keras_h5_to_avse.py -> KerasModel.load -> libavse fp32 forward, against the float64
-    oracle run on the ORIGINAL tensors (so a mis-mapped layer shows up as a forward error, not only as a
-    tensor mismatch)."""
+    HDF5 file -> tools/keras_h5_to_avse.py -> KerasModel.load -> libavse forward (exact fp32 and the credited
+    float32_split dtype, the output layer at dB scale), against the float64 oracle run on the ORIGINAL tensors (so a
+    mis-mapped layer shows up as a forward error, not only as a tensor mismatch)."""
     import torch
     from avse_amd import ops
     from avse_amd.model import KerasModel
     from oracle import keras_ref as K
-    m = KerasModel.init(seed=5, randomize=True)
+    from test_gpu_forward import db_scale
+    m = db_scale(KerasModel.init(seed=5, randomize=True))
     npz, h5, st = tmp_path / "w.npz", tmp_path / "model.h5py", tmp_path / "model.safetensors"
     _write_npz(m, npz)
     assert _run("make_keras_h5.py", str(npz), str(h5), "--offset", "4").returncode == 0
@@ -109,9 +111,11 @@ def test_converted_keras_h5_runs_forward_against_oracle(tmp_path, gpu):
     mel = rng.normal(-40, 12, (3, 80, 20)).astype(np.float32)
     video = rng.integers(0, 256, (3, 128, 128, 5)).astype(np.float32)
     ref = K.forward(m.layer_dict(), mel, video)
-    dw = ops.DeviceWeights(loaded, "float32")
+    dw = ops.DeviceWeights(loaded, dtype)
     got = ops.forward(dw, torch.from_numpy(mel).to(gpu), torch.from_numpy(video).to(gpu)).cpu().numpy()
     err = float(np.sqrt(np.mean((got.astype(np.float64) - ref) ** 2)))
+    print(f"HDF5 model, {dtype}: output RMS {np.sqrt(np.mean(ref ** 2)):.3g}, abs RMS err {err:.3e}")
+    assert dw.last_range_bits == 0
     # the fp32 forward's bounds (tests/test_gpu_forward.py): absolute RMS 1e-4 (north star) and relative 1e-5
     assert err <= 1e-4, err
     assert err <= 1e-5 * float(np.sqrt(np.mean(ref ** 2))) + 1e-12, err

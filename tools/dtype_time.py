@@ -35,7 +35,7 @@ def main():
 
         def step():
             ops.spectrogram(audio, frames_per_slice=20, out=mel)
-            ops.forward(dw, mel.view(B, 80, 20), video, mean, std, out=out)
+            ops.forward(dw, mel.view(B, 80, 20), video, mean, std, out=out, checked=False)
         for _ in range(3):
             step()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
