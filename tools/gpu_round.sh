@@ -6,7 +6,7 @@ TAG=${1:-r02}
 OUT=gpurun_out
 mkdir -p $OUT
 # -rP: every passing test's captured output (the measured errors each tolerance is set against) stays in the log
-timeout -k 10 900 python -u -m pytest tests -m gpu -v -rP --timeout 300 --timeout-method thread > $OUT/gputest_$TAG.log 2>&1
+timeout -k 10 1100 python -u -m pytest tests -m gpu -v -rP --timeout 300 --timeout-method thread > $OUT/gputest_$TAG.log 2>&1
 rc=$?
 echo "pytest rc=$rc"
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
