@@ -395,10 +395,13 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
         // the Bl half (2 + (kg & 1)); the per-16-lane address pattern is the bf16 one (same conflict-free image)
         const int bo16 = r16 * 64 + (((S16 ? (kg & 1) : kg) ^ wswz<true>(r16)) << 4);
         const int bo16l = r16 * 64 + (((2 + (kg & 1)) ^ wswz<true>(r16)) << 4);
+        // ABL & 256 (harness only): B fragments of column blocks 4..7 reuse blocks 0..3 (the LDS fragment reads per MFMA of
+        // a 128 x 128 wave tile; results meaningless)
         auto frags_lo = [&](int ws, i32x4 (&fb)[8]) {
             const char* wp = wring + ws * WSLOT + bo16l;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) fb[j] = *reinterpret_cast<const i32x4*>(wp + 1024 * j);
+            for (int j = 0; j < 8; ++j)
+                fb[j] = ((ABL & 256) && j >= 4) ? fb[j - 4] : *reinterpret_cast<const i32x4*>(wp + 1024 * j);
         };
         auto frags = [&](int hs, int tap, int ws, i32x4 (&fa)[4], i32x4 (&fb)[8]) {
             const int ky = tap / KS, kx = tap % KS;
@@ -408,7 +411,8 @@ __global__ __launch_bounds__(512, 1) void k_conv_stream(HaloArgs a) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) fa[i] = *reinterpret_cast<const i32x4*>(hp + boff_of(i));
 #pragma unroll
-            for (int j = 0; j < 8; ++j) fb[j] = *reinterpret_cast<const i32x4*>(wp + 1024 * j);
+            for (int j = 0; j < 8; ++j)
+                fb[j] = ((ABL & 256) && j >= 4) ? fb[j - 4] : *reinterpret_cast<const i32x4*>(wp + 1024 * j);
         };
         // BN scale / shift of this column block in LDS (past the rings), read in the epilogue: 16 VGPRs held
         // for the whole tile would spill the 256-register budget (128 accumulators + 2 x 12 fragments)

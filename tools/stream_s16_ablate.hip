@@ -71,6 +71,9 @@ int main() {
         std::printf("%-40s %8.4f ms  %7.1f TF/s (fp32 MAC)\n", name, ms, flop / (ms * 1e-3) / 1e12);
     };
     rep("full", run<0>(a, reps));
+    rep("half the B fragment reads (256)", run<256>(a, reps));
+    rep("full", run<0>(a, reps));
+    rep("half the B fragment reads (256)", run<256>(a, reps));
     rep("no halo pieces (1)", run<1>(a, reps));
     rep("no weight streaming (2)", run<2>(a, reps));
     rep("no loads (3)", run<3>(a, reps));
