@@ -40,6 +40,7 @@ struct Options {
     int gemm_ksplit_cap = 0;  // AVSE_GEMM_KSPLIT: cap k_gemm's split-K factor (0 = no cap)
     int dense_istft = 0;      // AVSE_DENSE_ISTFT: ISTFT through the dense pinv + scratch frames + k_ola (not fused)
     int no_act_scale = 0;     // AVSE_NO_ACT_SCALE: split weights loaded without per-layer activation exponents
+    int no_win = 0;           // AVSE_NO_WIN: split stride-1 gather layers on k_conv, not the windowed conv_win.hip
 };
 
 #define AVSE_HIP_CHECK(expr)                                                                   \
@@ -237,6 +238,13 @@ constexpr int kFp32Block = 8;
 // kConvSplitPairs the same on an input already in the split pair layout (Ci, strides, kpad, w_off in halves)
 constexpr int kConvSplit = 2, kConvSplitPairs = 3;
 int launch_conv(const ConvArgs& a, int dtype, hipStream_t s);
+
+// conv_win.hip: the split-pair layers whose every phase is a stride-1 gather over the input grid (the decoder's
+// transposed convolutions, the stride-1 audio conv): k_conv's arithmetic with the A operand read from a per-tile input
+// window staged once per 16-channel chunk in LDS (k_conv gathers every tap's im2col rows from global memory).
+// htaps: host copy of a.taps.  Returns 0 when launched, -1 when the layer does not fit the kernel (the caller runs
+// launch_conv), else an error status.
+int launch_conv_win(const ConvArgs& a, const int2* htaps, hipStream_t s);
 
 // fused decoder tail d_deconv4 -> d_deconv5 -> d_deconv6, one workgroup per clip (conv_dec.hip, bf16)
 struct DecTailArgs {

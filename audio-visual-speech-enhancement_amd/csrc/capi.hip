@@ -197,6 +197,7 @@ const OptionName kOptionNames[] = {
     {"gemm_ksplit_cap", "AVSE_GEMM_KSPLIT", &Options::gemm_ksplit_cap},
     {"dense_istft", "AVSE_DENSE_ISTFT", &Options::dense_istft},
     {"no_act_scale", "AVSE_NO_ACT_SCALE", &Options::no_act_scale},
+    {"no_win", "AVSE_NO_WIN", &Options::no_win},
 };
 
 struct avse_weights {
@@ -1323,6 +1324,15 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
         }
         return in_pairs ? kConvSplitPairs : kConvSplit;
     };
+    // a generic layer launch: split-pair stride-1 gather layers on the windowed kernel (conv_win.hip) when it takes
+    // their shape (option no_win: always k_conv)
+    auto conv = [&](const ConvArgs& a, int dti, const GpuLayer& G, hipStream_t st) -> int {
+        if (split && dti == kConvSplitPairs && !c->opt.no_win) {
+            const int rw = launch_conv_win(a, G.htaps, st);
+            if (rw != -1) return rw;
+        }
+        return launch_conv(a, split ? dti : cdt, st);
+    };
     size_t off[B_COUNT + 1];
     arena_bytes(N, dt, c->opt, off, P);
     const long long CAT = P.cat, AEMB = P.aemb, EMB = P.emb;
@@ -1508,7 +1518,7 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
         ConvArgs a = (i < 4) ? conv_args(G, buf(a_in[i]), in_cs, buf(a_in[i + 1]), (long long)G.ho * G.wo * G.def.cout, G.def.cout, 0, N)
                              : conv_args(G, buf(a_in[i]), in_cs, buf(B_CAT), CAT, G.def.cout, 0, N);   // Flatten -> concat[0:aemb]
         const int dti = pairs(a, i > 0, true, i);   // a_conv1: fp32 audio-prep input
-        if ((rc = launch_conv(a, split ? dti : cdt, sa)) || (rc = mark())) return rc;
+        if ((rc = conv(a, dti, G, sa)) || (rc = mark())) return rc;
     }
     if (concurrent) AVSE_HIP_CHECK(hipEventRecord(c->join, sa));
     if (video) {
@@ -1596,12 +1606,12 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
             a.fuse_bias = W->d6_bias;
             a.fuse_out = out;
             const int dti = pairs(a, true, false, 14 + i);
-            if ((rc = launch_conv(a, split ? dti : cdt, s)) || (rc = mark())) return rc;
+            if ((rc = conv(a, dti, G, s)) || (rc = mark())) return rc;
             continue;
         }
         ConvArgs a = conv_args(G, buf(d_in[i]), in_cs, buf(d_in[i + 1]), (long long)G.ho * G.wo * G.def.cout, G.def.cout, 0, N);
         const int dti = pairs(a, true, i < 4 || !opt.unfused_tail, 14 + i);   // an unfused d_deconv5 feeds launch_out_conv fp32
-        if ((rc = launch_conv(a, split ? dti : cdt, s)) || (rc = mark())) return rc;
+        if ((rc = conv(a, dti, G, s)) || (rc = mark())) return rc;
     }
     if (opt.unfused_tail) {
         if ((rc = launch_out_conv(buf(B_D5), W->d6_w, W->d6_bias, out, N * kMels * P.T, gdt, s)) || (rc = mark())) return rc;

@@ -91,6 +91,8 @@ void avse_ctx_destroy(avse_ctx* ctx);
  *   gemm_ksplit_cap (AVSE_GEMM_KSPLIT) cap on k_gemm's split-K factor (0 = none)
  *   dense_istft (AVSE_DENSE_ISTFT)   avse_istft through the dense pinv + frame scratch + overlap-add pass
  *   no_act_scale (AVSE_NO_ACT_SCALE) AVSE_F32_SPLIT weights loaded afterwards keep every activation exponent 0
+ *   no_win (AVSE_NO_WIN)             AVSE_F32_SPLIT stride-1 gather layers (decoder phases, a_conv2) on the generic
+ *                                    k_conv instead of the windowed kernel
  * Unknown names return AVSE_ERR_INVALID. */
 int avse_ctx_set_option(avse_ctx* ctx, const char* name, int value);
 int avse_ctx_get_option(avse_ctx* ctx, const char* name, int* value);

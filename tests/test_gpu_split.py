@@ -184,3 +184,30 @@ def test_fp32_forward_is_batch_invariant(gpu, dtype):
         assert np.array_equal(one.reshape(full[c].shape), full[c]), (c, float(np.abs(one.reshape(full[c].shape) - full[c]).max()))
     part = ops.forward(dw, mel[290:297].contiguous(), video[290:297].contiguous(), mean, std).cpu().numpy()
     assert np.array_equal(part, full[290:297])
+
+
+@pytest.mark.parametrize("N", [3, 37])
+def test_split_windowed_layers_match_kconv_and_oracle(gpu, N):
+    """conv_win.hip (the split single-phase 16-tap gather layers: d_deconv4, a_conv2) against the same layers on k_conv
+    (option no_win) and the float64 oracle, layer by layer: another K order over the same products (chunk-outer,
+    tap-inner), so the two agree within fp32 rounding; N = 37 puts tile boundaries inside clips and tiles over two."""
+    from avse_amd import _lib
+    from avse_amd.model import KerasModel
+    from avse_amd import ops
+    model = db_scale(KerasModel.init(seed=31, randomize=True))
+    mel, video = make_inputs(N, 131)
+    inter = {}
+    ref = K.forward(model.layer_dict(), mel, video, intermediates=inter)
+    names = ["a_conv2", "d_deconv1", "d_deconv2", "d_deconv3", "d_deconv4"]
+    dw = ops.DeviceWeights(model, SPLIT)
+    got = ops.forward(dw, ops.to_device(mel), ops.to_device(video)).cpu().numpy()
+    sc = scratch(dw, N, names=names)
+    with _lib.context().options(no_win=1):
+        got_k = ops.forward(dw, ops.to_device(mel), ops.to_device(video)).cpu().numpy()
+        sck = scratch(dw, N, names=names)
+    for k in names:
+        print(f"{k}: window vs oracle {rel_rms(sc[k], inter[k]):.2e}, vs k_conv {rel_rms(sc[k], sck[k]):.2e}")
+        assert rel_rms(sc[k], inter[k]) <= FP32_REL and rel_rms(sc[k], sck[k]) <= 1e-6, k
+    ae, aek = abs_rms(got, ref), abs_rms(got_k, ref)
+    print(f"output abs RMS: windowed {ae:.3e}, k_conv {aek:.3e}")
+    assert ae <= FP32_ABS and rel_rms(got, got_k) <= 1e-6
