@@ -72,6 +72,7 @@ SIGNATURES = {
     "avse_forward_checked": (_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _c_void_p,
                                     _c_void_p, _int, ctypes.POINTER(ctypes.c_uint32)]),
     "avse_range_status": (_int, [_c_void_p, _c_void_p, ctypes.POINTER(ctypes.c_uint32)]),
+    "avse_range_snapshot": (_int, [_c_void_p, _c_void_p, _c_void_p]),
     "avse_weights_act_exponents": (_int, [_c_void_p, ctypes.POINTER(_int), _int]),
     "avse_forward_profile": (_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64,
                                     _c_void_p, _c_void_p, ctypes.POINTER(_flt)]),

@@ -1655,6 +1655,15 @@ int avse_range_status(avse_ctx* c, void* stream, uint32_t* host_bits) {
     return 0;
 }
 
+int avse_range_snapshot(avse_ctx* c, void* stream, uint32_t* host_word) {
+    if (!c || !host_word) return fail(AVSE_ERR_INVALID, "NULL argument");
+    AVSE_HIP_CHECK(hipSetDevice(c->device));
+    hipStream_t s = (hipStream_t)stream;
+    AVSE_HIP_CHECK(hipMemcpyAsync(host_word, c->range, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+    AVSE_HIP_CHECK(hipMemsetAsync(c->range, 0, sizeof(unsigned), s));
+    return 0;
+}
+
 int avse_forward_checked(avse_ctx* c, const avse_weights* W, const float* audio, const float* video, const float* vmean,
                          const float* vstd, int64_t N, float* out, void* stream, int mode, uint32_t* host_bits) {
     if (host_bits) *host_bits = 0;

@@ -207,6 +207,54 @@ def forward(weights, audio, video, vnorm_mean=None, vnorm_std=None, out=None, ch
     return out
 
 
+class RangePipeline:
+    """Deferred range verification of unchecked float32_split forwards (avse_range_snapshot): after each forward,
+    `submit(recompute)` enqueues a snapshot of the context's range guard into a pinned host word and an event; the
+    snapshot of batch k is read once the stream has passed it — at the `depth`-th later submit, or at `drain()` — so the
+    host never waits for the batch it just enqueued (avse_forward_checked waits for every batch before the next is
+    launched).  A batch whose bits are set is recomputed by its `recompute` callable (e.g. ops.forward(...,
+    checked=True) into the same output, which must then still hold that batch's inputs); `bits` accumulates every
+    batch's guard bits and `recomputed` counts the batches redone."""
+
+    def __init__(self, ctx, depth=2):
+        self.ctx = ctx
+        self.depth = max(1, int(depth))
+        self.words = torch.zeros(self.depth, dtype=torch.int32, pin_memory=True)
+        self.events = [torch.cuda.Event() for _ in range(self.depth)]
+        self.pending = []
+        self.k = 0
+        self.bits = 0
+        self.recomputed = 0
+
+    def submit(self, recompute=None):
+        slot = self.k % self.depth
+        if len(self.pending) == self.depth:
+            self._retire()
+        dev = torch.device("cuda", self.ctx.device_index)
+        with torch.cuda.device(dev):
+            _lib.check(_lib.load().avse_range_snapshot(self.ctx.handle, _lib.stream_handle(dev),
+                                                       ctypes.c_void_p(self.words.data_ptr() + 4 * slot)),
+                       "avse_range_snapshot")
+            self.events[slot].record()
+        self.pending.append((slot, recompute))
+        self.k += 1
+
+    def _retire(self):
+        slot, recompute = self.pending.pop(0)
+        self.events[slot].synchronize()
+        b = int(self.words[slot].item()) & 0xFFFFFFFF
+        if b:
+            self.bits |= b
+            if recompute is not None:
+                recompute()
+                self.recomputed += 1
+
+    def drain(self):
+        while self.pending:
+            self._retire()
+        return self.bits
+
+
 def forward_profile(weights, audio, video, vnorm_mean=None, vnorm_std=None, out=None):
     """forward() with HIP events between kernel launches (synchronises); returns (out, {stage: ms})."""
     N = _check_forward_args(weights, audio, video, vnorm_mean, vnorm_std)

@@ -17,7 +17,7 @@ Every utterance is independent (top_db is per utterance), so a multi-GPU run sha
 """
 import torch
 
-from . import data_processor, ops
+from . import _lib, data_processor, ops
 
 
 class Enhancer:
@@ -64,16 +64,33 @@ class Enhancer:
         clips = mel.view(n, data_processor.N_MELS, spf)
         frames = video.reshape((n,) + tuple(video.shape[2:]))
         pred = torch.empty_like(clips)
-        self.range_bits = 0     # float32_split: range-guard bits of this call's chunks (recomputed on exact fp32)
+        # float32_split: each chunk's range guard is verified one chunk later (ops.RangePipeline), so the chunks'
+        # forwards queue back to back; a flagged chunk is recomputed on the exact-fp32 kernels
+        split = self.weights.dtype == _lib.AVSE_F32_SPLIT
+        pipe = ops.RangePipeline(self.weights.ctx) if split else None
+        if split:
+            self.weights.ctx.range_status()
+
+        def chunk(a, b, checked):
+            ops.forward(self.weights, clips[a:b], frames[a:b], vmean, vstd, out=pred[a:b], checked=checked)
+
         for a in range(0, n, self.chunk):
             b = min(n, a + self.chunk)
-            ops.forward(self.weights, clips[a:b], frames[a:b], vmean, vstd, out=pred[a:b])
-            self.range_bits |= getattr(self.weights, "last_range_bits", 0)
+            chunk(a, b, False)
+            if split:
+                pipe.submit(lambda a=a, b=b: chunk(a, b, True))
         if ev:
             ev[2].record()
-        out = ops.istft(pred.view(U, S, data_processor.N_MELS, spf), stft, sample_rate=self.sr, n_fft=g["n_fft"],
-                        hop_length=g["hop_length"], n_mels=data_processor.N_MELS, fmin=data_processor.MEL_FMIN,
-                        fmax=data_processor.MEL_FMAX)
+        def istft():
+            return ops.istft(pred.view(U, S, data_processor.N_MELS, spf), stft, sample_rate=self.sr, n_fft=g["n_fft"],
+                             hop_length=g["hop_length"], n_mels=data_processor.N_MELS, fmin=data_processor.MEL_FMIN,
+                             fmax=data_processor.MEL_FMAX)
+        out = istft()
+        self.range_bits = 0
+        if split:
+            self.range_bits = pipe.drain()
+            if pipe.recomputed:      # a chunk was redone after the ISTFT had been queued: redo the ISTFT after it
+                out = istft()
         if ev:
             ev[3].record()
             ev[3].synchronize()

@@ -483,18 +483,25 @@ def main():
     padded = torch.zeros((per, 80, 20), dtype=torch.float32, device=dev)
     gathered = torch.empty((world * per, 80, 20), dtype=torch.float32, device=dev) if world > 1 else None
 
-    # fp32_split range guard: every kernel of every timed step reports an out-of-range pair into the context's sticky
-    # guard word, read once after the timed region (range_guard.bits: 0 = every timed output fp32-accurate).  --checked
-    # runs avse_forward_checked per step instead (a stream wait per step, the per-batch contract of the CLI / predict
-    # path; its throughput is reported as range_guard.checked_per_step_clips_per_s either way)
+    # fp32_split range guard, per batch: every kernel reports an out-of-range pair into the context's guard word, and
+    # after each step's forward a snapshot of it is queued (ops.RangePipeline, avse_range_snapshot) and read one step
+    # later, while the next step runs; a batch with bits set would be recomputed on the exact-fp32 kernels (its
+    # recompute callable).  --checked runs avse_forward_checked instead (the forward, then a wait for its guard word
+    # before the next step is launched: the blocking form the CLI predict path uses per batch)
     checked = args.checked
     dw.ctx.range_status()
+    pipe = ops.RangePipeline(dw.ctx)
     if args.graph:
         dw.ctx.set_option("graph", 1)
+
+    def recompute():
+        ops.forward(dw, mel.view(B, 80, 20), video, mean, std, out=out, checked=True)
 
     def step():
         ops.spectrogram(audio, frames_per_slice=20, out=mel)          # [B, 1, 80, 20]
         ops.forward(dw, mel.view(B, 80, 20), video, mean, std, out=out, checked=checked)
+        if not checked and args.dtype == "fp32_split":
+            pipe.submit(recompute)
         if world > 1:
             padded[:B].copy_(out)
             dist.all_gather_into_tensor(gathered, padded)
@@ -510,6 +517,7 @@ def main():
         win.mark(i)
         step()
     win.mark(args.steps)
+    pipe.drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -521,17 +529,18 @@ def main():
     value = global_batch * args.steps / elapsed
     ms_per_step = 1e3 * elapsed / args.steps
     timed_out = out.cpu().numpy()
-    bits = dw.ctx.range_status() | (dw.last_range_bits if checked else 0)
+    bits = pipe.bits | dw.ctx.range_status() | (dw.last_range_bits if checked else 0)
     if world > 1:
         every = [0] * world
         dist.all_gather_object(every, bits)
         bits = 0
         for b in every:
             bits |= b
-    range_guard = {"checked_every_step": bool(checked and args.dtype == "fp32_split"), "bits": bits,
-                   "layers_out_of_range": _lib.range_bit_names(bits),
-                   "read": "per step (avse_forward_checked)" if checked else
-                           "sticky guard word of all timed steps, read after the timed region (avse_range_status)",
+    range_guard = {"checked_every_step": args.dtype == "fp32_split", "bits": bits,
+                   "layers_out_of_range": _lib.range_bit_names(bits), "batches_recomputed": pipe.recomputed,
+                   "read": "per step, blocking (avse_forward_checked)" if checked else
+                           "per step, one step later (ops.RangePipeline: avse_range_snapshot + event, read while the "
+                           "next step runs; a flagged batch is recomputed on the exact-fp32 kernels)",
                    "act_exponents_nonzero": {k: v for k, v in dw.act_exponents().items() if v}}
     if args.dtype == "fp32_split" and world == 1 and not checked:
         # the per-batch checked path (what speech_enhancer predict / pipeline.Enhancer run), same batch, 20 steps
@@ -541,8 +550,8 @@ def main():
             ops.spectrogram(audio, frames_per_slice=20, out=mel)
             ops.forward(dw, mel.view(B, 80, 20), video, mean, std, out=out, checked=True)
         torch.cuda.synchronize()
-        range_guard["checked_per_step_clips_per_s"] = round(B * 20 / (time.perf_counter() - t1), 1)
-        range_guard["checked_per_step_bits"] = dw.last_range_bits
+        range_guard["blocking_checked_per_step_clips_per_s"] = round(B * 20 / (time.perf_counter() - t1), 1)
+        range_guard["blocking_checked_per_step_bits"] = dw.last_range_bits
 
     # ---- live per-kernel durations (HIP events on the launch stream) for the roofline ----
     stage_ms = {}

@@ -215,6 +215,12 @@ int avse_forward_checked(avse_ctx* ctx, const avse_weights* w, const float* audi
  * forwards ran on) and clears them. */
 int avse_range_status(avse_ctx* ctx, void* stream, uint32_t* host_bits);
 
+/* Stream-ordered, non-blocking form of avse_range_status for pipelines (verify batch k while batch k + 1 runs): enqueues
+ * on `stream` a copy of the guard bits raised so far into *host_word (pinned host memory, e.g. hipHostMalloc; valid
+ * once the stream has reached this point: record an event after the call and wait for it) and a reset of the guard, so
+ * the bits of the forwards enqueued between two snapshots land in the later one. */
+int avse_range_snapshot(avse_ctx* ctx, void* stream, uint32_t* host_word);
+
 /* AVSE_F32_SPLIT: the activation exponent e_L of each plan layer (host_exp[0..n), n <= 20; layer L stores the pairs of
  * x 2^e_L); 0 for every layer of the other dtypes. */
 int avse_weights_act_exponents(const avse_weights* w, int* host_exp, int n);

@@ -203,3 +203,34 @@ def test_trained_model_split_parity(gpu):
     assert dw.last_range_bits == 0
     assert ae <= FP32_ABS and ae <= 1.5 * ae32 + 1e-6
     torch.cuda.synchronize()
+
+
+def test_range_pipeline_recomputes_flagged_batches(gpu):
+    """ops.RangePipeline (avse_range_snapshot): unchecked forwards queued back to back, each batch's guard read one batch
+    later; the flagged batches (the overflowing model) are recomputed on exact fp32 into their own outputs, the clean
+    ones (the same model's weights at O(1) scale) are not."""
+    from avse_amd import _lib, ops
+    from avse_amd.model import KerasModel
+    bad = KerasModel.init(seed=6, randomize=True)
+    bad.tensors["v_conv2/kernel"] = (bad.tensors["v_conv2/kernel"] * np.float32(3000.0)).astype(np.float32)
+    good = KerasModel.init(seed=6, randomize=True)
+    mel, video = make_inputs(3, 66)
+    m, v = ops.to_device(mel), ops.to_device(video)
+    dws = {"bad": ops.DeviceWeights(bad, SPLIT), "good": ops.DeviceWeights(good, SPLIT)}
+    ref32 = {k: ops.forward(ops.DeviceWeights(x, "float32"), m, v).cpu().numpy() for k, x in (("bad", bad), ("good", good))}
+    ctx = _lib.context()
+    ctx.range_status()
+    pipe = ops.RangePipeline(ctx)
+    outs = {}
+    for name in ("good", "bad", "good", "bad"):
+        out = outs.setdefault(name, [])
+        o = ops.forward(dws[name], m, v, checked=False)
+        out.append(o)
+        pipe.submit(lambda dw=dws[name], o=o: ops.forward(dw, m, v, out=o, checked=True))
+    bits = pipe.drain()
+    assert bits >> 6 & 1 and pipe.recomputed == 2, (hex(bits), pipe.recomputed)
+    for o in outs["bad"]:
+        assert np.array_equal(o.cpu().numpy(), ref32["bad"])
+    ref = K.forward(good.layer_dict(), mel, video)
+    for o in outs["good"]:
+        assert rel_rms(o.cpu().numpy(), ref) <= FP32_REL
