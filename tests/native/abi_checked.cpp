@@ -121,8 +121,8 @@ static void gpu_part() {
     // the all-zero-video path, and the training step
     const avse::NetPlan p = avse::make_plan(20, 5);
     const std::vector<float> blob = random_blob(p, 3);
-    for (int dtype : {AVSE_BF16, AVSE_F32}) {
-        const int N = dtype == AVSE_BF16 ? 300 : 4;
+    for (int dtype : {AVSE_BF16, AVSE_F32, AVSE_F32_SPLIT}) {
+        const int N = dtype == AVSE_BF16 ? 300 : dtype == AVSE_F32_SPLIT ? 37 : 4;
         avse_weights* w = nullptr;
         CALL(avse_weights_load(c, blob.data(), (int64_t)blob.size(), dtype, &w));
         if (!w) continue;
@@ -139,6 +139,26 @@ static void gpu_part() {
         EXPECT(all_finite(dout, (size_t)N * 1600), "forward finite (dtype %d)", dtype);
         CALL(avse_forward(c, w, da, nullptr, nullptr, nullptr, N, dout, nullptr));
         EXPECT(all_finite(dout, (size_t)N * 1600), "zero-video forward finite (dtype %d)", dtype);
+        if (dtype == AVSE_F32_SPLIT) {
+            // the range guard: in range for these weights (read and cleared), checked forward, snapshot into pinned memory
+            uint32_t bits = 1;
+            CALL(avse_range_status(c, nullptr, &bits));
+            EXPECT(bits == 0, "split forwards in range (bits 0x%x)", bits);
+            CALL(avse_forward_checked(c, w, da, dv, dm, ds, N, dout, nullptr, AVSE_RANGE_ERROR, &bits));
+            EXPECT(bits == 0 && all_finite(dout, (size_t)N * 1600), "checked forward (bits 0x%x)", bits);
+            uint32_t* pinned = nullptr;
+            EXPECT(hipHostMalloc((void**)&pinned, sizeof(uint32_t), hipHostMallocDefault) == hipSuccess, "pinned");
+            if (pinned) {
+                *pinned = 7;
+                CALL(avse_forward(c, w, da, dv, dm, ds, N, dout, nullptr));
+                CALL(avse_range_snapshot(c, nullptr, pinned));
+                EXPECT(hipDeviceSynchronize() == hipSuccess && *pinned == 0, "snapshot (0x%x)", *pinned);
+                (void)hipHostFree(pinned);
+            }
+            int ex[20] = {};
+            CALL(avse_weights_act_exponents(w, ex, 20));
+            EXPECT(avse_forward_checked(c, w, da, dv, dm, ds, N, dout, nullptr, 7, &bits) == AVSE_ERR_INVALID, "bad mode");
+        }
         if (dtype == AVSE_F32) {
             avse_trainer* t = nullptr;
             CALL(avse_trainer_create(c, blob.data(), (int64_t)blob.size(), N, &t));
