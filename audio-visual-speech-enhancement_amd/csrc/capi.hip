@@ -751,8 +751,8 @@ int build_layer(avse_weights* W, int li, const float* kernel, const float* bias,
     // Split dtype: the same kernels on split-f16 operands (see below).
     if ((W->dtype == AVSE_BF16 || split) && L.kind == CONV && L.pool && L.hin >= 8 && !opt.no_halo) {
         const int ntap = L.kh * L.kw;
-        if (L.cin == 5 && L.kh == 5) G.halo = HALO_V1;   // conv_v1r.hip: 5 frames (25 / 29.97 fps)
-        else if (L.cin % 128) G.halo = HALO_NONE;         // 6 frames (30 fps): generic k_conv
+        if ((L.cin == 5 || L.cin == 6) && L.kh == 5) G.halo = HALO_V1;   // conv_v1r.hip: 5 (25 / 29.97 fps) or 6 frames (30)
+        else if (L.cin % 128) G.halo = HALO_NONE;
         else if (L.kh == 5) G.halo = HALO_K5;
         else if (L.hin >= 16) G.halo = HALO_K3_16;
         else G.halo = HALO_K3_8;
@@ -819,7 +819,7 @@ int build_layer(avse_weights* W, int li, const float* kernel, const float* bias,
         if ((rc = upload(W, scale_h, &G.scale_h))) return rc;
         std::vector<uint16_t> hp;
         if (G.halo == HALO_V1) {
-            // conv_v1r.hip: slice ky, k = kx * 6 + frame (frame 5 and k = 30, 31 zero)
+            // conv_v1r.hip: slice ky, k = kx * 6 + frame (k = 30, 31 zero; frame 5 too with 5 frames)
             hp.assign((size_t)L.kh * L.cout * 32, 0);
             for (int ky = 0; ky < L.kh; ++ky)
                 for (int n = 0; n < L.cout; ++n)
@@ -1254,7 +1254,7 @@ int avse_weights_load_shape(avse_ctx* c, const float* blob, int64_t n_floats, in
     }
     if (dtype == AVSE_F32_SPLIT) {
         // the split layers pass split-pair activations to each other: they must be a prefix v_conv1 .. of the video
-        // encoder (a 6-frame v_conv1 runs generic: then every video layer does)
+        // encoder (a v_conv1 on the generic kernel makes every video layer generic; no_halo: all of them)
         bool prefix = true;
         for (int i = 5; i < 11; ++i) {
             if (W->layers[i].halo == HALO_NONE) prefix = false;

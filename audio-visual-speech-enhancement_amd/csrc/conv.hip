@@ -96,7 +96,7 @@ constexpr int FP32_BLOCK = kFp32Block;
 constexpr int KABL = AVSE_KCONV_ABL;   // avse_common.h (train.hip's block-exact split-K plans on it)
 
 // S16 (AVSE_F32_SPLIT's generic layers): split-f16 products on the 16-bit matrix cores.  The LDS A slab row is
-// [h(16) | l(16)] f16 of 16 real k (h = f16(x), l = f16(x - h)): with T = float (fp32 input: a_conv1, a 6-frame
+// [h(16) | l(16)] f16 of 16 real k (h = f16(x), l = f16(x - h)): with T = float (fp32 input: a_conv1, a no_halo
 // v_conv1) store_slab splits the loaded floats into those 64 bytes; with T = _Float16 the input already holds the pairs
 // in that layout (written by the producing layer's epilogue, a.out_s16) and a slab is copied as is — Ci, strides, kpad
 // and w_off then count halves.  The host packs each weight slab row as [Bh(16) | Bl(16)] (per-channel power-of-two

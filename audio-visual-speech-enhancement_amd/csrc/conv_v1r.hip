@@ -39,7 +39,9 @@ __device__ __forceinline__ void barrier_raw() { asm volatile("s_barrier" ::: "me
 // B-operand lane groups, tools/lds_swizzle_search.py)
 __device__ __forceinline__ int wsw(int co) { return 2 * ((co >> 2) & 1); }
 
-constexpr int TH = 16, TW = 16, KS = 5, PAD = 2, NF = 5;
+// NF (template): video frames per clip, 5 (25 / 29.97 fps) or 6 (30 fps: the 12-byte window pixel's sixth half
+// holds a real frame instead of the zero, and the weights' k = kx * 6 + 5 rows are the sixth frame's)
+constexpr int TH = 16, TW = 16, KS = 5, PAD = 2;
 constexpr int HH = TH + KS - 1, HW = TW + KS - 1, HPIX = HH * HW;   // 20 x 20 window
 constexpr int PB = 12;                                              // bytes per window pixel
 // LDS row pitch 24 pixels (20 used): 20 gave 2-way bank conflicts on the A-fragment ds_read2_b32, 24 none
@@ -61,8 +63,9 @@ static_assert(HSLOT % 16 == 0 && LDS_BYTES <= 160 * 1024, "LDS");
 
 // ABL: ablation mask for tools/v1r_ablate.hip only (0 in the library): 1 = loaders skip the output pass,
 // 2 = loaders skip the per-tile window work, 4 = no MFMAs, 8 = no barrier in the tile loop
-template <int ABL = 0>
+template <int ABL = 0, int NF = 5>
 __global__ __launch_bounds__(512, 1) void k_conv_v1r(HaloArgs a) {
+    static_assert(NF == 5 || NF == 6, "frames");
     extern __shared__ __attribute__((aligned(1024))) char lds[];
     char* const wimg = lds;
     char* const halo = lds + WIMG;                  // [NWS][HSLOT]
@@ -117,7 +120,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_v1r(HaloArgs a) {
         // two register sets: window k+2 is loaded two tiles ahead, so the vmcnt wait for it never waits on
         // output stores younger than two tiles (vmcnt retires in issue order, stores included)
         f32x4 v4[2][PPL];
-        float v1[2][PPL], pm[2][PPL], ps[2][PPL];
+        float v1[2][PPL], v5[2][PPL], pm[2][PPL], ps[2][PPL];
         int pok[2][PPL];
         auto win_load = [&](auto set, int k) {
             constexpr int Q = decltype(set)::value;
@@ -135,6 +138,8 @@ __global__ __launch_bounds__(512, 1) void k_conv_v1r(HaloArgs a) {
                 const int voff = ok ? pix * NF * 4 : kOOB, moff = ok ? pix * 4 : kOOB;
                 v4[Q][e] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(vrs, voff, 0, 0));
                 v1[Q][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(vrs, voff, 16, 0));
+                if constexpr (NF == 6)
+                    v5[Q][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(vrs, voff, 20, 0));
                 pm[Q][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(mrs, moff, 0, 0));
                 ps[Q][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(srs, moff, 0, 0));
                 pok[Q][e] = ok;
@@ -149,7 +154,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_v1r(HaloArgs a) {
                 if (P >= HPIX) continue;
                 // v_rcp_f32 (1 ulp) and packed conversions: the loader shares its SIMD's issue with the MFMA wave
                 const float rs = __builtin_amdgcn_rcpf(ps[Q][e]);
-                float f[NF] = {v4[Q][e][0], v4[Q][e][1], v4[Q][e][2], v4[Q][e][3], v1[Q][e]};
+                float f[6] = {v4[Q][e][0], v4[Q][e][1], v4[Q][e][2], v4[Q][e][3], v1[Q][e], NF == 6 ? v5[Q][e] : 0.f};
 #pragma unroll
                 for (int i = 0; i < NF; ++i) {
                     const float n = norm ? (f[i] - pm[Q][e]) * rs : f[i];
@@ -159,7 +164,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_v1r(HaloArgs a) {
                 unsigned* d = reinterpret_cast<unsigned*>(halo + hs * HSLOT + (wy * HWP + wx) * PB);
                 d[0] = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){f[0], f[1]}, bf16x2));
                 d[1] = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){f[2], f[3]}, bf16x2));
-                d[2] = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){f[4], 0.f}, bf16x2));
+                d[2] = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){f[4], f[5]}, bf16x2));
             }
         };
         // output pass of tile k: BN (|scale|, shift) + LeakyReLU(0.3) on the pooled raw maxima the compute
@@ -366,9 +371,10 @@ typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 // CW compute waves + 4 loader waves.  CW = 4: compute wave w owns conv rows 4w .. 4w+3 x all 128 channels (one
 // compute wave per SIMD); CW = 8: rows 4 (w & 3) .. x channels 64 (w >> 2) .. +63 — two compute waves per SIMD, so one
 // wave's MFMAs cover the other's LDS waits (half the accumulators, the A fragments read by both)
-template <int CW>
+template <int CW, int NF = 5>
 __global__ __launch_bounds__(64 * (CW + 4), 1) void k_conv_v1s(HaloArgs a) {
     static_assert(CW == 4 || CW == 8, "compute waves");
+    static_assert(NF == 5 || NF == 6, "frames");
     constexpr int NJ = 32 / CW;                      // 16-channel column blocks per compute wave
     extern __shared__ __attribute__((aligned(1024))) char lds[];
     char* const wimg = lds;                          // [2 pieces][5 rows][128 co][64 B]
@@ -420,7 +426,7 @@ __global__ __launch_bounds__(64 * (CW + 4), 1) void k_conv_v1s(HaloArgs a) {
         const __amdgpu_buffer_rsrc_t mrs = make_rsrc(norm ? a.vmean : a.video, (long long)a.Hc * a.Wc * 4);
         const __amdgpu_buffer_rsrc_t srs = make_rsrc(norm ? a.vstd : a.video, (long long)a.Hc * a.Wc * 4);
         f32x4 v4[2][PPL];
-        float v1[2][PPL], pm[2][PPL], ps[2][PPL];
+        float v1[2][PPL], v5[2][PPL], pm[2][PPL], ps[2][PPL];
         int pok[2][PPL];
         auto win_load = [&](auto set, int k) {
             constexpr int Q = decltype(set)::value;
@@ -438,6 +444,8 @@ __global__ __launch_bounds__(64 * (CW + 4), 1) void k_conv_v1s(HaloArgs a) {
                 const int voff = ok ? pix * NF * 4 : kOOB, moff = ok ? pix * 4 : kOOB;
                 v4[Q][e] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(vrs, voff, 0, 0));
                 v1[Q][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(vrs, voff, 16, 0));
+                if constexpr (NF == 6)
+                    v5[Q][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(vrs, voff, 20, 0));
                 pm[Q][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(mrs, moff, 0, 0));
                 ps[Q][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(srs, moff, 0, 0));
                 pok[Q][e] = ok;
@@ -451,7 +459,7 @@ __global__ __launch_bounds__(64 * (CW + 4), 1) void k_conv_v1s(HaloArgs a) {
             for (int e = 0; e < PPL; ++e) {
                 const int P = L + 256 * e;
                 if (P >= HPIX) continue;
-                float f[6] = {v4[Q][e][0], v4[Q][e][1], v4[Q][e][2], v4[Q][e][3], v1[Q][e], 0.f};
+                float f[6] = {v4[Q][e][0], v4[Q][e][1], v4[Q][e][2], v4[Q][e][3], v1[Q][e], NF == 6 ? v5[Q][e] : 0.f};
 #pragma unroll
                 for (int i = 0; i < NF; ++i) {
                     const float n = norm ? (f[i] - pm[Q][e]) / ps[Q][e] : f[i];
@@ -635,8 +643,9 @@ __global__ __launch_bounds__(64 * (CW + 4), 1) void k_conv_v1s(HaloArgs a) {
 int launch_conv_v1r(const HaloArgs& a, hipStream_t s) {
     if (a.split) {
         constexpr int CW = AVSE_V1S_CW;
-        if (int rc = ensure_lds_attr((const void*)k_conv_v1s<CW>, LDS_S)) return rc;
-        if (a.Hc % TH || a.Wc % TW || a.Co != 128 || a.Ci != NF || !a.w || a.out_mode != OUT_S16) {
+        const void* kf = a.Ci == 6 ? (const void*)k_conv_v1s<CW, 6> : (const void*)k_conv_v1s<CW, 5>;
+        if (int rc = ensure_lds_attr(kf, LDS_S)) return rc;
+        if (a.Hc % TH || a.Wc % TW || a.Co != 128 || (a.Ci != 5 && a.Ci != 6) || !a.w || a.out_mode != OUT_S16) {
             set_error("v_conv1 split kernel: unexpected layer shape, packing or output format");
             return 3;
         }
@@ -646,12 +655,14 @@ int launch_conv_v1r(const HaloArgs& a, hipStream_t s) {
         const int tiles = a.N * (a.Hc / TH) * (a.Wc / TW);
         int gx = ncu >= 8 ? ncu / 8 * 8 : ncu;
         if (gx > tiles) gx = tiles;
-        hipLaunchKernelGGL(k_conv_v1s<CW>, dim3(gx), dim3(64 * (CW + 4)), LDS_S, s, a);
+        if (a.Ci == 6) hipLaunchKernelGGL((k_conv_v1s<CW, 6>), dim3(gx), dim3(64 * (CW + 4)), LDS_S, s, a);
+        else hipLaunchKernelGGL((k_conv_v1s<CW, 5>), dim3(gx), dim3(64 * (CW + 4)), LDS_S, s, a);
         AVSE_HIP_CHECK(hipGetLastError());
         return 0;
     }
-    if (int rc = ensure_lds_attr((const void*)k_conv_v1r<0>, LDS_LAUNCH)) return rc;
-    if (a.Hc % TH || a.Wc % TW || a.Co != 128 || a.Ci != NF || !a.w) {
+    const void* kf = a.Ci == 6 ? (const void*)k_conv_v1r<0, 6> : (const void*)k_conv_v1r<0, 5>;
+    if (int rc = ensure_lds_attr(kf, LDS_LAUNCH)) return rc;
+    if (a.Hc % TH || a.Wc % TW || a.Co != 128 || (a.Ci != 5 && a.Ci != 6) || !a.w) {
         set_error("v_conv1 row-run kernel: unexpected layer shape or missing packing");
         return 3;
     }
@@ -661,7 +672,8 @@ int launch_conv_v1r(const HaloArgs& a, hipStream_t s) {
     const int tiles = a.N * (a.Hc / TH) * (a.Wc / TW);
     int gx = ncu >= 8 ? ncu / 8 * 8 : ncu;
     if (gx > tiles) gx = tiles;
-    hipLaunchKernelGGL(k_conv_v1r<0>, dim3(gx), dim3(512), LDS_LAUNCH, s, a);
+    if (a.Ci == 6) hipLaunchKernelGGL((k_conv_v1r<0, 6>), dim3(gx), dim3(512), LDS_LAUNCH, s, a);
+    else hipLaunchKernelGGL((k_conv_v1r<0, 5>), dim3(gx), dim3(512), LDS_LAUNCH, s, a);
     AVSE_HIP_CHECK(hipGetLastError());
     return 0;
 }

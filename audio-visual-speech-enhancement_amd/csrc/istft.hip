@@ -9,8 +9,8 @@
 // k_istft640 (n_fft 640): one 64-lane block per 3 frames of one utterance.  The 321-bin one-sided
 // spectrum is folded into a 320-point complex sequence (E[k] + i O[k]) and inverted with the same
 // in-register 20 x 16 DFTs as K1 through the conjugation identity IDFT(Z) = conj(DFT(conj Z)) / 320;
-// each lane then writes two windowed output samples per frame.  k_istft_dft handles other sizes
-// (n_fft = 2 (n_bins - 1), e.g. 532 at 29.97 fps) with a direct inverse DFT.  k_ola sums the <= 4
+// each lane then writes two windowed output samples per frame.  k_istft532 (532 = 2 (267 - 1), the inverse at
+// 29.97 / 30 fps) is a 28 x 19 prime-factor DFT; k_istft_dft handles other sizes with a direct inverse DFT.  k_ola sums the <= 4
 // overlapping frames of each output sample in increasing frame order (librosa's order), divides by
 // the window sum-square where it exceeds float32 tiny, and drops n_fft/2 samples at both ends.
 #include <algorithm>
@@ -502,6 +502,169 @@ __global__ __launch_bounds__(64 * IWAVES) AVSE_ISTFT_ATTR void k_istft_fused(Ist
     }
 }
 
+// ------------------------------------------------------------------------------------------------------------
+// k_istft532: the inverse for n_fft 533's 267 bins (N = 2 (267 - 1) = 532 = 28 x 19, librosa.istft's n_fft at 29.97 /
+// 30 fps) by the Good-Thomas prime-factor algorithm over the Hermitian-complete spectrum Xf:
+//   input map  k = (19 k1 + 28 k2) mod 532,  output map  n = (57 n1 + 476 n2) mod 532
+//   (57 = 19 (19^-1 mod 28), 476 = 28 (28^-1 mod 19)), so that e^{+2 pi i k n / 532} = V28^{k1 n1} V19^{k2 n2}:
+//   stage A: item (frame, k1 in 0..14): Z[k1][n2] = sum_k2 Xf V19^{k2 n2}, folded over k2 <-> 19 - k2, n2 <-> 19 - n2
+//            (Z[28 - k1][n2] = conj Z[k1][n2] by Hermitian symmetry, so k1 = 15..27 are not computed);
+//   stage B: item (frame, n2): x[n1, n2] = Re sum_k1 Z[k1][n2] V28^{k1 n1}, folded over k1 <-> 28 - k1 and
+//            n1 <-> 28 - n1; x / 532 times the window goes to the frame scratch for k_ola (as k_istft_dft's output).
+// Before the stages: amplitudes from the mel dB, the pinv(mel) projection to 267 bins for a chunk of frames per
+// thread (the pinv rows read once per block, coalesced) and the mixture's unit phase.  One 256-thread block per
+// (utterance, chunk of 16 frames); ~20K pinv + ~11K DFT multiply-adds per frame against the direct inverse's ~300K.
+constexpr int I532_CH = 16;
+constexpr int I532_THREADS = 256;
+constexpr int I532_XS = 272;                           // float2 bin row pitch
+constexpr int I532_LDS = 4 * I532_CH * 80 + 8 * I532_CH * I532_XS + 8 * I532_CH * 15 * 19;
+
+__device__ constexpr float kCos19[19] = {
+    1.000000000e+00f, 9.458172321e-01f, 7.891405225e-01f, 5.469481349e-01f, 2.454854846e-01f, -8.257934451e-02f,
+    -4.016954303e-01f, -6.772815585e-01f, -8.794737458e-01f, -9.863613248e-01f, -9.863613248e-01f, -8.794737458e-01f,
+    -6.772815585e-01f, -4.016954303e-01f, -8.257934451e-02f, 2.454854846e-01f, 5.469481349e-01f, 7.891405225e-01f,
+    9.458172321e-01f};
+__device__ constexpr float kSin19[19] = {
+    0.000000000e+00f, 3.246994615e-01f, 6.142126918e-01f, 8.371664882e-01f, 9.694002867e-01f, 9.965844750e-01f,
+    9.157733321e-01f, 7.357239127e-01f, 4.759473801e-01f, 1.645945907e-01f, -1.645945907e-01f, -4.759473801e-01f,
+    -7.357239127e-01f, -9.157733321e-01f, -9.965844750e-01f, -9.694002867e-01f, -8.371664882e-01f, -6.142126918e-01f,
+    -3.246994615e-01f};
+__device__ constexpr float kCos28[28] = {
+    1.000000000e+00f, 9.749279022e-01f, 9.009688497e-01f, 7.818315029e-01f, 6.234897971e-01f, 4.338837266e-01f,
+    2.225209326e-01f, 0.0f, -2.225209326e-01f, -4.338837266e-01f, -6.234897971e-01f, -7.818315029e-01f,
+    -9.009688497e-01f, -9.749279022e-01f, -1.000000000e+00f, -9.749279022e-01f, -9.009688497e-01f, -7.818315029e-01f,
+    -6.234897971e-01f, -4.338837266e-01f, -2.225209326e-01f, 0.0f, 2.225209326e-01f, 4.338837266e-01f,
+    6.234897971e-01f, 7.818315029e-01f, 9.009688497e-01f, 9.749279022e-01f};
+__device__ constexpr float kSin28[28] = {
+    0.000000000e+00f, 2.225209326e-01f, 4.338837266e-01f, 6.234897971e-01f, 7.818315029e-01f, 9.009688497e-01f,
+    9.749279022e-01f, 1.000000000e+00f, 9.749279022e-01f, 9.009688497e-01f, 7.818315029e-01f, 6.234897971e-01f,
+    4.338837266e-01f, 2.225209326e-01f, 0.0f, -2.225209326e-01f, -4.338837266e-01f, -6.234897971e-01f,
+    -7.818315029e-01f, -9.009688497e-01f, -9.749279022e-01f, -1.000000000e+00f, -9.749279022e-01f, -9.009688497e-01f,
+    -7.818315029e-01f, -6.234897971e-01f, -4.338837266e-01f, -2.225209326e-01f};
+
+__global__ __launch_bounds__(I532_THREADS) void k_istft532(IstftArgs a, int n_chunks) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    float* const amp = sm;                                                         // [CH][80]
+    float2* const Xs = reinterpret_cast<float2*>(sm + I532_CH * 80);                // [CH][XS] bins 0..266
+    float2* const Z = Xs + I532_CH * I532_XS;                                       // [CH][15][19]
+    float* const fo = reinterpret_cast<float*>(Xs);                                 // [CH][532] (stage B: aliases Xs)
+    const int tid = threadIdx.x;
+    const long long u = blockIdx.x / n_chunks;
+    const int t0 = (int)(blockIdx.x - u * n_chunks) * I532_CH;
+    const int nt = min(I532_CH, a.T - t0);
+
+    for (int it = tid; it < nt * a.n_mels; it += I532_THREADS) {
+        const int f = it / a.n_mels, m = it - f * a.n_mels;
+        amp[f * 80 + m] = sqrtf(exp10f(0.1f * mel_at(a, u, m, t0 + f)));
+    }
+    __syncthreads();
+    // bins: thread k, all frames of the chunk (pinv row element read once per block)
+    for (int k = tid; k < 267; k += I532_THREADS) {
+        float acc[I532_CH];
+#pragma unroll
+        for (int f = 0; f < I532_CH; ++f) acc[f] = 0.f;
+        for (int m = 0; m < a.n_mels; ++m) {
+            const float p = a.pinvT[m * 267 + k];
+#pragma unroll
+            for (int f = 0; f < I532_CH; ++f) acc[f] = fmaf(p, amp[f * 80 + m], acc[f]);
+        }
+        const float2* d = a.stft + (u * 267 + k) * (long long)a.stft_frames + t0;
+#pragma unroll
+        for (int f = 0; f < I532_CH; ++f) {
+            if (f >= nt) break;
+            const float2 ph = unit_phase(d[f]);
+            float2 x = make_float2(acc[f] * ph.x, acc[f] * ph.y);
+            if (k == 0 || k == 266) x.y = 0.f;   // irfft ignores the DC / Nyquist imaginary parts
+            Xs[f * I532_XS + k] = x;
+        }
+    }
+    __syncthreads();
+    // stage A: item (f, k1 in 0..14)
+    if (tid < nt * 15) {
+        const int f = tid / 15, k1 = tid - 15 * f;
+        const float2* xr = Xs + f * I532_XS;
+        float2 y[19];
+#pragma unroll
+        for (int k2 = 0; k2 < 19; ++k2) {
+            int k = 19 * k1 + 28 * k2;
+            k = k >= 532 ? k - 532 : k;
+            k = k >= 532 ? k - 532 : k;
+            const float2 v = xr[k <= 266 ? k : 532 - k];
+            y[k2] = k <= 266 ? v : make_float2(v.x, -v.y);
+        }
+        float pr[10], pi[10], mr[10], mi[10];
+        float z0r = y[0].x, z0i = y[0].y;
+#pragma unroll
+        for (int k2 = 1; k2 <= 9; ++k2) {
+            pr[k2] = y[k2].x + y[19 - k2].x;
+            pi[k2] = y[k2].y + y[19 - k2].y;
+            mr[k2] = y[k2].x - y[19 - k2].x;
+            mi[k2] = y[k2].y - y[19 - k2].y;
+            z0r += pr[k2];
+            z0i += pi[k2];
+        }
+        float2* zo = Z + (f * 15 + k1) * 19;
+        zo[0] = make_float2(z0r, z0i);
+#pragma unroll
+        for (int n2 = 1; n2 <= 9; ++n2) {
+            // V = c + i s: Y V + Y' conj V = (Pr c - Mi s) + i (Pi c + Mr s); n2 -> 19 - n2 flips s
+            float A = y[0].x, B = 0.f, C = y[0].y, D = 0.f;
+#pragma unroll
+            for (int k2 = 1; k2 <= 9; ++k2) {
+                const float c = kCos19[(k2 * n2) % 19], s = kSin19[(k2 * n2) % 19];
+                A = fmaf(pr[k2], c, A);
+                B = fmaf(mi[k2], s, B);
+                C = fmaf(pi[k2], c, C);
+                D = fmaf(mr[k2], s, D);
+            }
+            zo[n2] = make_float2(A - B, C + D);
+            zo[19 - n2] = make_float2(A + B, C - D);
+        }
+    }
+    __syncthreads();
+    // stage B: item (f, n2); Z[28 - k1][n2] = conj Z[k1][n2] (Hermitian Xf), so the pair k1, 28 - k1 adds
+    // 2 Re(Z[k1][n2] V28^{k1 n1}); k1 = 0 and 14 are their own partners (real: V28^{14 n1} = (-1)^n1)
+    const float scale = 1.f / 532.f;
+    for (int it = tid; it < nt * 19; it += I532_THREADS) {
+        const int f = it / 19, n2 = it - 19 * f;
+        const float2* zf = Z + f * 15 * 19;
+        float sr[15], si[15];
+        const float z0 = zf[n2].x;
+        const float2 z14 = zf[14 * 19 + n2];
+#pragma unroll
+        for (int k1 = 1; k1 <= 13; ++k1) {
+            const float2 p = zf[k1 * 19 + n2];
+            sr[k1] = 2.f * p.x;
+            si[k1] = 2.f * p.y;
+        }
+        float xo[28];
+#pragma unroll
+        for (int n1 = 0; n1 <= 14; ++n1) {
+            float E = z0 + ((n1 & 1) ? -z14.x : z14.x), O = 0.f;
+#pragma unroll
+            for (int k1 = 1; k1 <= 13; ++k1) {
+                E = fmaf(sr[k1], kCos28[(k1 * n1) % 28], E);
+                O = fmaf(si[k1], kSin28[(k1 * n1) % 28], O);
+            }
+            xo[n1] = E - O;
+            if (n1 >= 1 && n1 <= 13) xo[28 - n1] = E + O;
+        }
+        float* fr = fo + f * 532;
+#pragma unroll
+        for (int n1 = 0; n1 < 28; ++n1) {
+            int n = 57 * n1 + 476 * n2;
+            n %= 532;
+            fr[n] = xo[n1] * scale;
+        }
+    }
+    __syncthreads();
+    // windowed frames to the scratch for k_ola
+    for (int it = tid; it < nt * 532; it += I532_THREADS) {
+        const int f = it / 532, n = it - 532 * f;
+        a.frames[((u * a.T) + t0 + f) * 532LL + n] = fo[f * 532 + n] * a.window[n];
+    }
+}
+
 // direct inverse real DFT, one 256-thread block per (frame, utterance); N = 2 (nb - 1)
 __global__ __launch_bounds__(256) void k_istft_dft(IstftArgs a) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -589,6 +752,15 @@ int launch_istft(const IstftArgs& a, hipStream_t s) {
     }
     if (a.N == 640) {
         hipLaunchKernelGGL(k_istft640, dim3((a.T + FPG - 1) / FPG, (unsigned)a.n_utt), dim3(64), 0, s, a);
+    } else if (a.N == 532 && a.nb == 267 && a.n_mels <= 80) {
+        const int n_chunks = (a.T + I532_CH - 1) / I532_CH;
+        const long long items = (long long)n_chunks * a.n_utt;
+        if (items > INT32_MAX) {
+            set_error("istft batch too large");
+            return 3;   // AVSE_ERR_UNSUPPORTED
+        }
+        if (int rc = ensure_lds_attr((const void*)k_istft532, I532_LDS)) return rc;
+        hipLaunchKernelGGL(k_istft532, dim3((unsigned)items), dim3(I532_THREADS), I532_LDS, s, a, n_chunks);
     } else {
         const size_t shm = sizeof(float) * 80 + sizeof(float2) * a.nb;
         hipLaunchKernelGGL(k_istft_dft, dim3(a.T, (unsigned)a.n_utt), dim3(256), shm, s, a);

@@ -18,7 +18,8 @@
 // [80, T] array, including the frame the slicing later drops) happens in-kernel; otherwise each
 // chunk publishes its max with an ordered-uint atomicMax and a clamp kernel follows.
 //
-// Other n_fft (e.g. 533 at 29.97 fps) use k_spec_dft: a direct DFT, one block per frame.
+// n_fft = 533 (29.97 / 30 fps) runs k_spec533 (a Good-Thomas 13 x 41 prime-factor DFT); other n_fft use k_spec_dft,
+// a direct DFT, one block per frame.
 #include <algorithm>
 
 #include "avse_common.h"
@@ -661,7 +662,224 @@ __global__ __launch_bounds__(64 * WAVES) AVSE_WPE4 void k_spec_seg(SpecArgs a) {
     }
 }
 
-// Direct DFT fallback for n_fft != 640: one 256-thread block per (frame, utterance).
+// ------------------------------------------------------------------------------------------------------------
+// k_spec533: n_fft = 533 (int(16000 / 29.97) and int(16000 / 30), data_processor.py:44) by the Good-Thomas prime
+// factor algorithm, 533 = 13 x 41 (coprime: no twiddle factors between the stages):
+//   input map  n = (41 n1 + 13 n2) mod 533,  output map  k = (287 k1 + 247 k2) mod 533
+//   (287 = 41 (41^-1 mod 13), 247 = 13 (13^-1 mod 41)), so that W533^{nk} = W13^{n1 k1} W41^{n2 k2}:
+//   stage 1: item (frame t, n1): the real 41-point DFT of x[(41 n1 + 13 n2) mod 533] (windowed), k2 = 0..20 only
+//            (real input: k2 and 41 - k2 are conjugate), folded over n2 <-> 41 - n2 (20 cos + 20 sin FMAs per k2);
+//   stage 2: item (t, k2 in 0..20): the complex 13-point DFT over n1, folded over n1 <-> 13 - n1 and k1 <-> 13 - k1.
+// The 13 x 21 outputs of a frame are its 267 bins once each: (k1, k2) with k2 >= 1 gives bin k or, when k > 266, bin
+// 533 - k as conj(X) (the (-k1, -k2) partner has k2 >= 21 and is not computed); k2 = 0 pairs k1 with 13 - k1, of
+// which the one with k <= 266 is kept.  14.5K FMAs per frame against the direct DFT's 285K; the cos / sin of both
+// DFT lengths are compile-time constants (float32 of the exact values), so no table is read in the stages.
+// One 384-thread block per (utterance, chunk of up to 25 frames: the 200-ms segment's 25 frames in one block, whose
+// top_db clamp then happens in-kernel as k_spec640's); the padded sample span and the window are staged in LDS.
+constexpr int P533_CH = 25;                           // frames per block
+constexpr int P533_THREADS = 384;
+constexpr int P533_HOPMAX = 160;
+constexpr int P533_SPAN = (P533_CH - 1) * P533_HOPMAX + 533;
+constexpr int P533_MAGP = 300;                        // magnitude row pitch (267 bins + band-read overrun, zeroed)
+constexpr int P533_MW = 32;                           // mel row width staged in LDS (host rows are padded to >= 24)
+constexpr int P533_UNION = (P533_SPAN + 536) > P533_CH * P533_MAGP ? (P533_SPAN + 536) : P533_CH * P533_MAGP;
+constexpr int P533_LDS = 4 * P533_UNION + 8 * P533_CH * 13 * 21 + 4 * 80 * P533_MW + 8 * 80 + 4 * 8;
+
+__device__ constexpr float kCos41[41] = {
+    1.000000000e+00f, 9.882804155e-01f, 9.533963799e-01f, 8.961655498e-01f, 8.179293871e-01f, 7.205215693e-01f,
+    6.062254310e-01f, 4.777198136e-01f, 3.380168676e-01f, 1.903911084e-01f, 3.830273449e-02f, -1.146834269e-01f,
+    -2.649815083e-01f, -4.090686440e-01f, -5.435675383e-01f, -6.653257012e-01f, -7.714892030e-01f, -8.595696092e-01f,
+    -9.275024533e-01f, -9.736953974e-01f, -9.970657825e-01f, -9.970657825e-01f, -9.736953974e-01f, -9.275024533e-01f,
+    -8.595696092e-01f, -7.714892030e-01f, -6.653257012e-01f, -5.435675383e-01f, -4.090686440e-01f, -2.649815083e-01f,
+    -1.146834269e-01f, 3.830273449e-02f, 1.903911084e-01f, 3.380168676e-01f, 4.777198136e-01f, 6.062254310e-01f,
+    7.205215693e-01f, 8.179293871e-01f, 8.961655498e-01f, 9.533963799e-01f, 9.882804155e-01f};
+__device__ constexpr float kSin41[41] = {
+    0.000000000e+00f, 1.526492834e-01f, 3.017205894e-01f, 4.437198341e-01f, 5.753186345e-01f, 6.934325099e-01f,
+    7.952928543e-01f, 8.785122633e-01f, 9.411400557e-01f, 9.817083478e-01f, 9.992662072e-01f, 9.934020638e-01f,
+    9.642534852e-01f, 9.125036001e-01f, 8.393654227e-01f, 7.465532422e-01f, 6.362424493e-01f, 5.110186934e-01f,
+    3.738170862e-01f, 2.278535068e-01f, 7.654925436e-02f, -7.654925436e-02f, -2.278535068e-01f, -3.738170862e-01f,
+    -5.110186934e-01f, -6.362424493e-01f, -7.465532422e-01f, -8.393654227e-01f, -9.125036001e-01f, -9.642534852e-01f,
+    -9.934020638e-01f, -9.992662072e-01f, -9.817083478e-01f, -9.411400557e-01f, -8.785122633e-01f, -7.952928543e-01f,
+    -6.934325099e-01f, -5.753186345e-01f, -4.437198341e-01f, -3.017205894e-01f, -1.526492834e-01f};
+__device__ constexpr float kCos13[13] = {1.000000000e+00f, 8.854560256e-01f, 5.680647492e-01f, 1.205366775e-01f,
+                                         -3.546048999e-01f, -7.485107780e-01f, -9.709418416e-01f, -9.709418416e-01f,
+                                         -7.485107780e-01f, -3.546048999e-01f, 1.205366775e-01f, 5.680647492e-01f,
+                                         8.854560256e-01f};
+__device__ constexpr float kSin13[13] = {0.000000000e+00f, 4.647231698e-01f, 8.229838610e-01f, 9.927088618e-01f,
+                                         9.350162148e-01f, 6.631226540e-01f, 2.393156588e-01f, -2.393156588e-01f,
+                                         -6.631226540e-01f, -9.350162148e-01f, -9.927088618e-01f, -8.229838610e-01f,
+                                         -4.647231698e-01f};
+
+__global__ __launch_bounds__(P533_THREADS) void k_spec533(SpecArgs a, int n_chunks) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    float* const seg = sm;                                  // [P533_SPAN] padded samples of the chunk's frames
+    float* const win = sm + P533_SPAN;                      // [533] window   (seg / win: stages 0-1)
+    float* const mag = sm;                                  // [CH][MAGP]     (stage 2 on: aliases seg / win)
+    float2* const Y = reinterpret_cast<float2*>(sm + P533_UNION);                 // [CH][13][21]
+    float* const melw = sm + P533_UNION + 2 * P533_CH * 13 * 21;                  // [n_mels][P533_MW]
+    int* const mst = reinterpret_cast<int*>(melw + 80 * P533_MW);                 // [n_mels] band starts
+    int* const mwd = mst + 80;                                                    // [n_mels] band widths
+    float* const red = reinterpret_cast<float*>(mwd + 80);                        // [6] block max
+    const int tid = threadIdx.x;
+    const long long u = blockIdx.x / n_chunks;
+    const int t0 = (int)(blockIdx.x - u * n_chunks) * P533_CH;
+    const int nt = min(P533_CH, a.n_frames - t0);
+    const long long L = a.n_samples;
+    const float* sig = a.sig + u * L;
+    const int hop = a.hop;
+
+    // stage 0: the chunk's padded samples (reflect / zero centre padding), the window, the Slaney rows
+    const long long s0 = (long long)t0 * hop - 266;
+    const int span = (nt - 1) * hop + 533;
+    for (int j = tid; j < span; j += P533_THREADS) seg[j] = sample_at(sig, L, s0 + j, a.pad_mode);
+    for (int j = tid; j < 533; j += P533_THREADS) win[j] = a.window[j];
+    for (int j = tid; j < a.n_mels * P533_MW; j += P533_THREADS) {
+        const int m = j / P533_MW, i = j - m * P533_MW;
+        melw[j] = i < a.mel_max_width ? a.mel_weight[m * a.mel_max_width + i] : 0.f;
+    }
+    for (int m = tid; m < a.n_mels; m += P533_THREADS) {
+        mst[m] = a.mel_start[m];
+        mwd[m] = a.mel_width[m];
+    }
+    __syncthreads();
+
+    // stage 1: item (t, n1) -> Y[t][n1][k2], k2 = 0..20
+    if (tid < nt * 13) {
+        const int t = tid / 13, n1 = tid - 13 * t;
+        const float* xs = seg + t * hop;
+        float x[41];
+#pragma unroll
+        for (int n2 = 0; n2 < 41; ++n2) {
+            int n = 41 * n1 + 13 * n2;
+            n = n >= 533 ? n - 533 : n;
+            x[n2] = xs[n] * win[n];
+        }
+        float ps[21], ms[21];   // x[n2] + x[41 - n2], x[n2] - x[41 - n2]
+#pragma unroll
+        for (int n2 = 1; n2 <= 20; ++n2) {
+            ps[n2] = x[n2] + x[41 - n2];
+            ms[n2] = x[n2] - x[41 - n2];
+        }
+        float2* yo = Y + (t * 13 + n1) * 21;
+        float r0 = x[0];
+#pragma unroll
+        for (int n2 = 1; n2 <= 20; ++n2) r0 += ps[n2];
+        yo[0] = make_float2(r0, 0.f);
+#pragma unroll
+        for (int k2 = 1; k2 <= 20; ++k2) {
+            float re = x[0], im = 0.f;
+#pragma unroll
+            for (int n2 = 1; n2 <= 20; ++n2) {
+                re = fmaf(ps[n2], kCos41[(n2 * k2) % 41], re);
+                im = fmaf(ms[n2], -kSin41[(n2 * k2) % 41], im);
+            }
+            yo[k2] = make_float2(re, im);
+        }
+    }
+    __syncthreads();
+
+    // stage 2: item (t, k2) -> X(k1, k2), k1 = 0..12 -> |X| rows (and the complex STFT)
+    const int nb = 267;
+    for (int it = tid; it < nt * 21; it += P533_THREADS) {
+        const int t = it / 21, k2 = it - 21 * t;
+        const float2* yi = Y + t * 13 * 21 + k2;
+        float2 y[13];
+#pragma unroll
+        for (int n1 = 0; n1 < 13; ++n1) y[n1] = yi[n1 * 21];
+        float pr[7], pi[7], mr[7], mi[7];
+        float x0r = y[0].x, x0i = y[0].y;
+#pragma unroll
+        for (int n1 = 1; n1 <= 6; ++n1) {
+            pr[n1] = y[n1].x + y[13 - n1].x;
+            pi[n1] = y[n1].y + y[13 - n1].y;
+            mr[n1] = y[n1].x - y[13 - n1].x;
+            mi[n1] = y[n1].y - y[13 - n1].y;
+            x0r += pr[n1];
+            x0i += pi[n1];
+        }
+        float2 X[13];
+        X[0] = make_float2(x0r, x0i);
+#pragma unroll
+        for (int k1 = 1; k1 <= 6; ++k1) {
+            float A = y[0].x, B = 0.f, C = y[0].y, D = 0.f;
+#pragma unroll
+            for (int n1 = 1; n1 <= 6; ++n1) {
+                const float c = kCos13[(n1 * k1) % 13], s = kSin13[(n1 * k1) % 13];
+                A = fmaf(pr[n1], c, A);
+                B = fmaf(mi[n1], s, B);
+                C = fmaf(pi[n1], c, C);
+                D = fmaf(mr[n1], s, D);
+            }
+            X[k1] = make_float2(A + B, C - D);
+            X[13 - k1] = make_float2(A - B, C + D);
+        }
+        float* mrow = mag + t * P533_MAGP;
+#pragma unroll
+        for (int k1 = 0; k1 < 13; ++k1) {
+            int k = (287 * k1 + 247 * k2) % 533;
+            float2 v = X[k1];
+            if (k > 266) {
+                if (k2 == 0) continue;   // the k1 <-> 13 - k1 partner holds this bin
+                k = 533 - k;
+                v.y = -v.y;
+            }
+            mrow[k] = __builtin_amdgcn_sqrtf(v.x * v.x + v.y * v.y);
+            if (a.stft_ri) reinterpret_cast<float2*>(a.stft_ri)[(u * nb + k) * a.n_frames + t0 + t] = v;
+        }
+    }
+    // the rows' tails past bin 266 (read by the padded band dots) are zero
+    for (int j = tid; j < nt * (P533_MAGP - 267); j += P533_THREADS) {
+        const int t = j / (P533_MAGP - 267);
+        mag[t * P533_MAGP + 267 + (j - t * (P533_MAGP - 267))] = 0.f;
+    }
+    __syncthreads();
+
+    // stage 3: Slaney mel + dB, item (m, t); top_db in-kernel when the block holds the whole utterance
+    const bool whole = n_chunks == 1;
+    float vmax = -INFINITY;
+    constexpr int NIT = (80 * P533_CH + P533_THREADS - 1) / P533_THREADS;
+    float dbv[NIT];
+#pragma unroll
+    for (int r = 0; r < NIT; ++r) {
+        const int it = tid + r * P533_THREADS;
+        dbv[r] = -INFINITY;
+        if (it >= a.n_mels * nt) continue;
+        const int m = it / nt, t = it - m * nt;
+        const float* mf = mag + t * P533_MAGP + mst[m];
+        const float* wm = melw + m * P533_MW;
+        float acc = 0.f;
+        for (int j = 0; j < mwd[m]; ++j) acc = fmaf(mf[j], wm[j], acc);
+        const float db = acc > a.amin ? 20.0f * log10f(acc) : a.db_floor;
+        dbv[r] = db;
+        vmax = fmaxf(vmax, db);
+        if (!whole) {
+            const long long oi = out_index(a.spf, a.n_slices, a.n_mels, a.n_frames, u, m, t0 + t);
+            if (oi >= 0) a.mel_db[oi] = db;
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) vmax = fmaxf(vmax, __shfl_xor(vmax, o));
+    if (!whole) {
+        if ((tid & 63) == 0) atomicMax(a.umax + u, f2ord(vmax));
+        return;
+    }
+    if ((tid & 63) == 0) red[tid >> 6] = vmax;
+    __syncthreads();
+    vmax = red[0];
+#pragma unroll
+    for (int w = 1; w < P533_THREADS / 64; ++w) vmax = fmaxf(vmax, red[w]);
+    const float floor_db = a.top_db >= 0.f ? vmax - a.top_db : -INFINITY;
+#pragma unroll
+    for (int r = 0; r < NIT; ++r) {
+        const int it = tid + r * P533_THREADS;
+        if (it >= a.n_mels * nt) continue;
+        const int m = it / nt, t = it - m * nt;
+        const long long oi = out_index(a.spf, a.n_slices, a.n_mels, a.n_frames, u, m, t0 + t);
+        if (oi >= 0) a.mel_db[oi] = fmaxf(dbv[r], floor_db);
+    }
+}
+
+// Direct DFT fallback for n_fft != 640 / 533: one 256-thread block per (frame, utterance).
 __global__ __launch_bounds__(256) void k_spec_dft(SpecArgs a) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const int N = a.n_fft, nb = N / 2 + 1;
@@ -757,6 +975,23 @@ int launch_spectrogram(const SpecArgs& a, hipStream_t s) {
         else if (fast) hipLaunchKernelGGL((k_spec640<true, false>), grid, block, 0, s, a, n_chunks);
         else if (ri) hipLaunchKernelGGL((k_spec640<false, true>), grid, block, 0, s, a, n_chunks);
         else hipLaunchKernelGGL((k_spec640<false, false>), grid, block, 0, s, a, n_chunks);
+        AVSE_HIP_CHECK(hipGetLastError());
+        if (n_chunks > 1 && need_clamp_pass) {
+            hipLaunchKernelGGL(k_spec_clamp, dim3(1024), dim3(256), 0, s, a);
+            AVSE_HIP_CHECK(hipGetLastError());
+        }
+        return 0;
+    }
+    if (a.n_fft == 533 && a.hop <= P533_HOPMAX && a.n_mels <= 80 && a.mel_max_width <= P533_MW) {
+        const int n_chunks = (a.n_frames + P533_CH - 1) / P533_CH;
+        const long long items = (long long)n_chunks * a.n_utt;
+        if (items > INT32_MAX) {
+            set_error("spectrogram batch too large (n_utt * chunks must fit in int32)");
+            return 3;   // AVSE_ERR_UNSUPPORTED
+        }
+        if (int rc = ensure_lds_attr((const void*)k_spec533, P533_LDS)) return rc;
+        if (n_chunks > 1) AVSE_HIP_CHECK(hipMemsetAsync(a.umax, 0, sizeof(unsigned) * a.n_utt, s));
+        hipLaunchKernelGGL(k_spec533, dim3((unsigned)items), dim3(P533_THREADS), P533_LDS, s, a, n_chunks);
         AVSE_HIP_CHECK(hipGetLastError());
         if (n_chunks > 1 && need_clamp_pass) {
             hipLaunchKernelGGL(k_spec_clamp, dim3(1024), dim3(256), 0, s, a);

@@ -103,3 +103,27 @@ def test_fused_istft_matches_dense_path(gpu, n_samples):
     torch.cuda.synchronize()
     assert fused.shape == dense.shape
     assert rel_rms(fused.cpu().numpy(), dense.cpu().numpy()) < 1e-5
+
+
+@pytest.mark.parametrize("U,n_samples", [(24, 48000), (3, 3200)])
+def test_batched_istft_533_matches_oracle(gpu, U, n_samples):
+    """29.97 / 30 fps (analysis n_fft 533, hop 133: the inverse is 532 = 28 x 19, k_istft532) on a batch of 3-s
+    utterances (361 frames, 23 chunks of 16) and on 200-ms segments (25 frames, a partial chunk), perturbed
+    predictions, each utterance against the oracle's reconstruct_speech_signal."""
+    from avse_amd import ops
+    rng = np.random.default_rng(533 + U)
+    x = synth_audio(rng, U, n_samples)
+    xt = torch.from_numpy(x).to(gpu)
+    mel, D = ops.spectrogram(xt, n_fft=533, hop_length=133, frames_per_slice=24, return_stft=True)
+    pred = mel + torch.from_numpy(rng.normal(0, 1.0, tuple(mel.shape)).astype(np.float32)).to(gpu)
+    y = ops.istft(pred, D, n_fft=533, hop_length=133).cpu().numpy()
+    ns = n_samples // 3200
+    assert y.shape == (U, 133 * (24 * ns - 1))
+    pred_np = pred.cpu().numpy()
+    worst = 0.0
+    for u in range(U):
+        ref = R.reconstruct_speech_signal(x[u], 16000, pred_np[u], 29.97)
+        assert ref.shape == y[u].shape
+        worst = max(worst, rel_rms(y[u], ref))
+    print(f"ISTFT n_fft 533, {U} x {n_samples} samples: worst waveform rel RMS {worst:.3e}")
+    assert worst < 1e-4, worst

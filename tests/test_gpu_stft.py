@@ -93,8 +93,9 @@ def test_complex_stft_matches(gpu):
         assert err < 2e-6, err
 
 
-def test_29_97_fps_direct_dft(gpu):
-    """n_fft = int(16000/29.97) = 533 (prime) takes the direct-DFT kernel."""
+def test_29_97_fps_utterances(gpu):
+    """n_fft = int(16000/29.97) = 533 = 13 x 41 (k_spec533, the prime-factor kernel): 2-s utterances, 241 frames in
+    chunks of 25 (the atomicMax top_db path)."""
     ops = _ops()
     rng = np.random.default_rng(6)
     g = R.frame_geometry(16000, 200, 10, 29.97)
@@ -155,3 +156,54 @@ def test_segment_kernel_other_banks(gpu, n_mels, fmin, fmax, sr, top_db):
     for u in range(40):
         mag, _ = R.magphase(R.stft(x[u], 640, 160))
         _check_db(got[u], R.amplitude_to_db(fb @ mag, top_db=top_db))
+
+
+@pytest.mark.parametrize("pad_mode", ["reflect", "constant"])
+def test_533_segments_match_oracle(gpu, pad_mode):
+    """29.97 / 30 fps 200-ms segments: 3200 samples -> 25 frames of n_fft 533 / hop 133 in one k_spec533 block (top_db
+    in-kernel), unsliced and sliced to 24 frames (the dropped 25th frame still sets the top_db floor: it is made the
+    loudest)."""
+    ops = _ops()
+    rng = np.random.default_rng(12)
+    x = synth_audio(rng, 48, 3200)
+    x[:8, -200:] *= 8
+    d = torch.from_numpy(x).to(gpu)
+    got = ops.spectrogram(d, n_fft=533, hop_length=133, pad_mode=pad_mode).cpu().numpy()
+    sl = ops.spectrogram(d, n_fft=533, hop_length=133, pad_mode=pad_mode, frames_per_slice=24).cpu().numpy()
+    assert got.shape == (48, 80, 25) and sl.shape == (48, 1, 80, 24)
+    np.testing.assert_array_equal(sl[:, 0], got[:, :, :24])
+    for u in range(48):
+        ref, _ = R.signal_to_spectrogram(x[u], 16000, 533, 133, pad_mode=pad_mode)
+        _check_db(got[u], ref)
+        if pad_mode == "reflect":
+            _check_db(sl[u], R.preprocess_audio_signal(x[u], 16000, 200, 1, 29.97))
+
+
+def test_533_complex_stft_and_bench_batch(gpu):
+    """k_spec533's complex STFT (every one of the 267 bins: the 13 x 21 prime-factor outputs map onto them once) against
+    the oracle, on 3-s utterances (chunked); and 512 segments (the fps_time / bench batch) spread-checked."""
+    ops = _ops()
+    rng = np.random.default_rng(13)
+    x = synth_audio(rng, 3, 48000)
+    _, D = ops.spectrogram(torch.from_numpy(x).to(gpu), n_fft=533, hop_length=133, return_stft=True)
+    D = D.cpu().numpy()
+    for u in range(3):
+        ref = R.stft(x[u], 533, 133).astype(np.complex128)
+        assert D[u].shape == ref.shape == (267, 361)
+        err = np.abs(D[u] - ref).max() / np.abs(ref).max()
+        assert err < 2e-6, err
+    xb = synth_audio(rng, 512, 3200)
+    got = ops.spectrogram(torch.from_numpy(xb).to(gpu), n_fft=533, hop_length=133, frames_per_slice=24).cpu().numpy()
+    for u in range(0, 512, 37):
+        _check_db(got[u], R.preprocess_audio_signal(xb[u], 16000, 200, 1, 29.97))
+
+
+def test_other_n_fft_direct_dft(gpu):
+    """n_fft without a fast kernel (600, hop 150) runs the direct-DFT fallback."""
+    ops = _ops()
+    rng = np.random.default_rng(14)
+    x = synth_audio(rng, 3, 6400)
+    got = ops.spectrogram(torch.from_numpy(x).to(gpu), n_fft=600, hop_length=150).cpu().numpy()
+    for u in range(3):
+        ref, _ = R.signal_to_spectrogram(x[u], 16000, 600, 150)
+        _check_db(got[u], ref)
