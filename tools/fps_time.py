@@ -50,6 +50,12 @@ def main():
         std = torch.from_numpy(v.std(axis=(0, 3)).astype(np.float32)).to(dev)
         model = KerasModel.init(seed=0, randomize=True, audio_shape=(80, T), video_shape=(128, 128, F))
         out = torch.empty((B, 80, T), dtype=torch.float32, device=dev)
+        # ISTFT (K6) of 64 3-s utterances at this rate: analysis STFT with the complex output, then the inverse
+        xu = torch.from_numpy(rng.normal(0, 3000, (64, 48000)).astype(np.float32)).to(dev)
+        melu, D = ops.spectrogram(xu, n_fft=g["n_fft"], hop_length=g["hop_length"], frames_per_slice=T,
+                                  return_stft=True)
+        istft_ms = timed(lambda: ops.istft(melu, D, n_fft=g["n_fft"], hop_length=g["hop_length"]))
+        print(f"{fps:5.2f} fps n_fft {g['n_fft']} ISTFT of 64 x 3 s: {istft_ms:.4f} ms", flush=True)
         for dt in dtypes:
             dw = ops.DeviceWeights(model, dt, dev)
             dw.ctx.reserve_for(dw, B)
