@@ -85,6 +85,34 @@ def test_training_gradients_match_oracle(gpu, T, F):
     check_gradients(tr.gradients(), ref_g)
 
 
+@pytest.mark.parametrize("fps,F", [(29.97, 5), (30.0, 6)])
+def test_enhancer_split_at_other_rates(gpu, fps, F):
+    """The predict path in the default dtype at 29.97 / 30 fps: k_spec533 -> the [80, 24] network in AVSE_F32_SPLIT
+    (v_conv1's row-run kernel on 5 / 6 frames, the stream convolutions) -> k_istft532, against the oracle pipeline
+    per utterance (speech_enhancer.py:61-88): waveform relative RMS 1e-4 (the fp32 bound of test_enhancer_at_2997_fps)."""
+    from avse_amd import ops
+    from avse_amd.model import KerasModel
+    from avse_amd.pipeline import Enhancer
+    U, S = 3, 12
+    rng = np.random.default_rng(int(fps * 100))
+    x = synth_audio(rng, U, 3200 * S)
+    video = synth_video(rng, U * S, f=F).reshape(U, S, 128, 128, F)
+    mean, std = R.video_normalizer_fit(video.reshape(U * S, 128, 128, F))
+    model = KerasModel.init(seed=F, randomize=True, audio_shape=(80, 24), video_shape=(128, 128, F))
+    enh = Enhancer(ops.DeviceWeights(model, "float32_split"), video_frame_rate=fps, chunk=16)
+    got = enh(ops.to_device(x), ops.to_device(video), ops.to_device(mean), ops.to_device(std)).cpu().numpy()
+    assert enh.range_bits == 0
+    for u in range(U):
+        xu = R.fit_length(x[u], 3200 * S)
+        sl = R.preprocess_audio_signal(xu, 16000, 200, S, fps)
+        pred = K.forward(model.layer_dict(), sl.astype(np.float32),
+                         R.video_normalize(video[u], mean, std).astype(np.float32))
+        ref = R.reconstruct_speech_signal(xu, 16000, pred.astype(np.float32), fps)
+        err = rel_rms(got[u], ref)
+        print(f"{fps} fps split utterance {u}: waveform rel RMS {err:.2e}")
+        assert got.shape[1] == len(ref) and err <= 1e-4, (u, err)
+
+
 def test_enhancer_at_2997_fps(gpu):
     """The end-to-end predict path (pipeline.Enhancer) at 29.97 fps: K1 at n_fft 533 -> the [80, 24] network ->
     K6, against the oracle pipeline (speech_enhancer.py:61-88 per sample), fp32: waveform relative RMS 1e-4."""
