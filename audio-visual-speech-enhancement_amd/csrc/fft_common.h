@@ -73,16 +73,20 @@ __device__ __forceinline__ void dft16(float2 (&v)[16], const float2* __restrict_
 // helpers keep (re, im) together and fold the quarter turns into the op_sel / neg modifiers.
 typedef float v2f __attribute__((ext_vector_type(2)));
 
-// b + (-i) e = (b.x + e.y, b.y - e.x)
+// b + (-i) e = (b.x + e.y, b.y - e.x) as one v_pk_fma_f32: the swapped e times (1, -1) (inline 1.0, neg_hi) plus b.
+// Not v_pk_add_f32 with a half-swapping op_sel (op_sel:[0,1] op_sel_hi:[1,0]): on gfx950 that form returned wrong
+// values in lanes 48..63 whenever matrix-core work of another kernel shared the CU (tools/pk_probe.py: 12 of 12 runs,
+// every run of the STFT beside an MFMA loop; 0 runs alone), while v_pk_fma_f32 with op_sel and v_pk_add_f32 without it
+// measured clean.  (Round 5; the v_pk_add form is kept out of every kernel: DESIGN.md §3 K1.)
 __device__ __forceinline__ v2f pk_add_mi(v2f b, v2f e) {
     v2f r;
-    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(b), "v"(e));
+    asm("v_pk_fma_f32 %0, %1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[0,0,1] neg_hi:[0,1,0]" : "=v"(r) : "v"(e), "v"(b));
     return r;
 }
-// b - (-i) e = (b.x - e.y, b.y + e.x)
+// b - (-i) e = (b.x - e.y, b.y + e.x): the swapped e times (-1, 1) plus b
 __device__ __forceinline__ v2f pk_sub_mi(v2f b, v2f e) {
     v2f r;
-    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(b), "v"(e));
+    asm("v_pk_fma_f32 %0, %1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[0,0,1] neg_lo:[0,1,0]" : "=v"(r) : "v"(e), "v"(b));
     return r;
 }
 // b + conj(e), b - conj(e)
