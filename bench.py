@@ -319,7 +319,7 @@ def cpu_baseline(audio, video, mean, std, model, gpu_outs, budget_s=12.0, max_s=
 E2E_UTTERANCES, E2E_SLICES = 667, 15           # BASELINE configs[4]: 10,005 clips = 667 3-s utterances x 15
 
 
-def run_e2e(args, world, rank, dev, model):
+def run_e2e(args, world, rank, dev, model, dist_on):
     """BASELINE configs[4]: end-to-end predict (K1 STFT -> bf16 fusion CNN -> K6 ISTFT) of 667 synthetic 3-s
     utterances (10,005 clips), strong-scaled over the ranks at utterance granularity (top_db is per utterance),
     the enhanced signals all-gathered over RCCL.  Prints its own JSON line (workload 'e2e')."""
@@ -348,17 +348,17 @@ def run_e2e(args, world, rank, dev, model):
 
     for _ in range(args.warmup):
         step()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if dist_on:
         tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
@@ -389,8 +389,20 @@ def run_e2e(args, world, rank, dev, model):
            "forward_tflops": round(fwd_tf, 1),
            "istft_roofline": {"bound": "hbm", "achieved": round(istft_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                               "frac": round(istft_gbs / PEAK_HBM_GBS, 4), "bytes_per_launch": istft_bytes}}
+    if dist_on:
+        res["collectives"] = {"backend": dist.get_backend(), "world_size": dist.get_world_size(),
+                              "per_step": "gather_clips (all_gather_into_tensor) of the enhanced signals when world > 1",
+                              "once": "weight broadcast, barriers, max-over-ranks all_reduce"}
     if rank == 0:
         print(json.dumps(res), flush=True)
+
+
+def _local_store():
+    """A TCP rendezvous on 127.0.0.1 for a one-rank group started without a launcher (--rccl)."""
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return f"tcp://127.0.0.1:{sk.getsockname()[1]}"
 
 
 def launch_ranks(n):
@@ -424,6 +436,9 @@ def main():
     ap.add_argument("--e2e", action="store_true", help="BASELINE configs[4]: end-to-end predict, utterance-sharded")
     ap.add_argument("--utterances", type=int, default=E2E_UTTERANCES)
     ap.add_argument("--e2e-chunk", type=int, default=1024, help="clips per forward launch in --e2e")
+    ap.add_argument("--rccl", action="store_true",
+                    help="initialise RCCL and run the N > 1 collectives (weight broadcast, per-step all-gather, "
+                         "max-over-ranks timing, guard-bit gather) even at one rank: the distributed path on a 1-GPU box")
     args = ap.parse_args()
     if args.gpus < 1:
         ap.error("--gpus must be >= 1")
@@ -440,8 +455,10 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    dist_on = world > 1 or args.rccl
+    if dist_on:
+        dist.init_process_group("nccl", device_id=dev, **({} if "RANK" in os.environ else
+                                                           {"rank": 0, "world_size": 1, "init_method": _local_store()}))
     from avse_amd.parallel import shard_bounds
     if args.strong:
         lo, hi = shard_bounds(args.batch, world, rank)
@@ -451,7 +468,7 @@ def main():
 
     # weights: seeded Keras-layout init on rank 0, broadcast once over RCCL (not timed)
     blob = torch.from_numpy(KerasModel.init(seed=0, randomize=True).to_blob()).to(dev)
-    if world > 1:
+    if dist_on:
         dist.broadcast(blob, 0)
     host = blob.cpu().numpy()
     tensors, off = {}, 0
@@ -461,8 +478,8 @@ def main():
         off += n
     model = KerasModel(tensors)
     if args.e2e:
-        run_e2e(args, world, rank, dev, model)
-        if world > 1:
+        run_e2e(args, world, rank, dev, model, dist_on)
+        if dist_on:
             dist.destroy_process_group()
         return
     dw = ops.DeviceWeights(model, LIB_DTYPE[args.dtype], dev)
@@ -481,7 +498,7 @@ def main():
     mel = torch.empty((B, 1, 80, 20), dtype=torch.float32, device=dev)
     per = -(-global_batch // world)
     padded = torch.zeros((per, 80, 20), dtype=torch.float32, device=dev)
-    gathered = torch.empty((world * per, 80, 20), dtype=torch.float32, device=dev) if world > 1 else None
+    gathered = torch.empty((world * per, 80, 20), dtype=torch.float32, device=dev) if dist_on else None
 
     # fp32_split range guard, per batch: every kernel reports an out-of-range pair into the context's guard word, and
     # after each step's forward a snapshot of it is queued (ops.RangePipeline, avse_range_snapshot) and read one step
@@ -502,14 +519,14 @@ def main():
         ops.forward(dw, mel.view(B, 80, 20), video, mean, std, out=out, checked=checked)
         if not checked and args.dtype == "fp32_split":
             pipe.submit(recompute)
-        if world > 1:
+        if dist_on:
             padded[:B].copy_(out)
             dist.all_gather_into_tensor(gathered, padded)
 
     for _ in range(args.warmup):
         step()
     win = Windows(args.steps, 10)
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -519,10 +536,10 @@ def main():
     win.mark(args.steps)
     pipe.drain()
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if dist_on:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -530,7 +547,7 @@ def main():
     ms_per_step = 1e3 * elapsed / args.steps
     timed_out = out.cpu().numpy()
     bits = pipe.bits | dw.ctx.range_status() | (dw.last_range_bits if checked else 0)
-    if world > 1:
+    if dist_on:
         every = [0] * world
         dist.all_gather_object(every, bits)
         bits = 0
@@ -656,9 +673,13 @@ def main():
         for ldt in outs:
             if ldt != args.dtype and f"fwd_{ldt}_b512" in result.get("legs", {}):
                 result["legs"][f"fwd_{ldt}_b512"]["parity"] = parity[ldt]
+    if dist_on:
+        result["collectives"] = {"backend": dist.get_backend(), "world_size": dist.get_world_size(),
+                                 "per_step": "all_gather_into_tensor of the rank's [B, 80, 20] outputs",
+                                 "once": "weight broadcast, barrier, max-over-ranks all_reduce, guard-bit gather"}
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 
