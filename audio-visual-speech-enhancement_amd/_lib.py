@@ -151,15 +151,31 @@ class Context:
         self.device_index = device_index
         self._cdll = load()   # held for __del__: module globals may be torn down first at interpreter exit
         self.handle = _c_void_p()
+        self._set_aside = 0
         check(load().avse_ctx_create(device_index, ctypes.byref(self.handle)), "avse_ctx_create")
 
-    def range_status(self, stream=None):
-        """avse_range_status: the range-guard bits raised by unchecked split forwards since the last call (waits for
-        `stream`, default torch's current stream on this device, and clears them)."""
+    def _read_range(self, stream):
         bits = ctypes.c_uint32()
         check(load().avse_range_status(self.handle, stream if stream is not None else stream_handle(self.device_index),
                                        ctypes.byref(bits)), "avse_range_status")
         return bits.value
+
+    def range_status(self, stream=None):
+        """avse_range_status: the range-guard bits raised by unchecked split forwards since the last call (waits for
+        `stream`, default torch's current stream on this device, and clears them), plus any bits set_aside_range()
+        took out of the device word since then.
+
+        The guard word is one per context (include/avse.h): forwards of one context on several streams or threads OR
+        into the same word, so a reader cannot tell which of them raised a bit.  Give each concurrent pipeline its own
+        context (avse_ctx_create) when that matters."""
+        bits = self._read_range(stream) | self._set_aside
+        self._set_aside = 0
+        return bits
+
+    def set_aside_range(self, stream=None):
+        """Start a pipeline with a clean device guard word WITHOUT discarding what earlier forwards raised: their bits
+        move to the host side and the next range_status() still returns them (pipeline.Enhancer, bench.py)."""
+        self._set_aside |= self._read_range(stream)
 
     def reserve(self, max_clips, dtype):
         check(load().avse_ctx_reserve(self.handle, int(max_clips), int(dtype)), "avse_ctx_reserve")

@@ -9,7 +9,7 @@ train (network.py:177-206) runs Keras-semantics fit steps on libavse's training 
 import numpy as np
 import torch
 
-from . import ops
+from . import _lib, ops
 from .model import KerasModel, shape_supported
 
 
@@ -60,14 +60,18 @@ class SpeechEnhancementNetwork(object):
         self.__dw = None
         return history
 
-    def predict_device(self, mixed_spectrograms, video_samples, video_normalizer=None):
-        """Device-tensor forward: [N, 80, T] x [N, 128, 128, F] -> [N, 80, T] (no squeeze)."""
+    def predict_device(self, mixed_spectrograms, video_samples, video_normalizer=None, checked=None):
+        """Device-tensor forward: [N, 80, T] x [N, 128, 128, F] -> [N, 80, T] (no squeeze).  checked (default: on for
+        float32_split weights, whose range guard is then read before returning) as in ops.forward."""
         a = ops.to_device(mixed_spectrograms, self.__device)
         v = None if video_samples is None else ops.to_device(video_samples, a.device)   # None: all-zero video
         m = s = None
         if video_normalizer is not None:
             m, s = video_normalizer.device_stats(a.device)
-        return ops.forward(self.device_weights(), a, v, m, s)
+        dw = self.device_weights()
+        if checked is None:
+            checked = dw.dtype == _lib.AVSE_F32_SPLIT
+        return ops.forward(dw, a, v, m, s, checked=checked)
 
     def predict(self, mixed_spectrograms, video_samples, video_normalizer=None):
         """network.py:208-212.  video_normalizer (optional) fuses VideoNormalizer.normalize into the

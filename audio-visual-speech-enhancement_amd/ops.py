@@ -165,7 +165,7 @@ def _check_forward_args(weights, audio, video, vnorm_mean, vnorm_std):
     return N
 
 
-def forward(weights, audio, video, vnorm_mean=None, vnorm_std=None, out=None, checked=None, on_range="recompute"):
+def forward(weights, audio, video, vnorm_mean=None, vnorm_std=None, out=None, checked=False, on_range="recompute"):
     """K2-K5: network forward.  audio [N, 80, 20], video [N, 128, 128, 5] float32 device tensors
     (video un-normalised when vnorm_* are given).  Returns [N, 80, 20] float32.  ([N, 80, T] / [N, 128, 128, F]
     for weights of another network shape, e.g. T = 24 at 29.97 fps.)
@@ -173,10 +173,13 @@ def forward(weights, audio, video, vnorm_mean=None, vnorm_std=None, out=None, ch
     video=None means an all-zero video input (BASELINE configs[2], the audio branch alone): the video
     encoder's output is then one constant vector, computed once per weights object and broadcast.
 
-    checked (default: True for float32_split weights): avse_forward_checked — waits for the stream and, when an
-    activation left the f16 pair range, recomputes the batch on the exact-fp32 kernels (on_range="recompute") or raises
-    _lib.RangeError (on_range="error").  weights.last_range_bits holds the guard bits of the last checked call (0: every
-    pair in range).  checked=False: plain asynchronous avse_forward (read the guard later with Context.range_status)."""
+    checked=False (default): plain asynchronous avse_forward on torch's current stream, capturable in a graph; a
+    float32_split forward leaves its range-guard bits in the context for Context.range_status / RangePipeline.
+    checked=True: avse_forward_checked — BLOCKS the host until the stream has run the forward and, when an activation
+    left the f16 pair range, recomputes the batch on the exact-fp32 kernels (on_range="recompute") or raises
+    _lib.RangeError (on_range="error"); not allowed while the stream is capturing.  weights.last_range_bits holds the
+    guard bits of the last checked call (0: every pair in range).  The synchronous reference-shaped API
+    (network.SpeechEnhancementNetwork.predict / evaluate, the CLI predict) opts in for float32_split weights."""
     N = _check_forward_args(weights, audio, video, vnorm_mean, vnorm_std)
     if out is None:
         out = torch.empty((N, 80, weights.T), dtype=torch.float32, device=audio.device)
@@ -185,8 +188,6 @@ def forward(weights, audio, video, vnorm_mean=None, vnorm_std=None, out=None, ch
         raise ValueError(f"out must be [N, 80, {weights.T}] on the inputs' device")
     if N == 0:
         return out
-    if checked is None:
-        checked = weights.dtype == _lib.AVSE_F32_SPLIT
     with torch.cuda.device(audio.device):
         if checked:
             mode = {"recompute": _lib.AVSE_RANGE_RECOMPUTE, "error": _lib.AVSE_RANGE_ERROR}[on_range]

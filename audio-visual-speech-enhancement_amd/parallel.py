@@ -46,8 +46,12 @@ def gather_clips(local, n_total):
         dist.all_gather_into_tensor(out, pad)
         parts = list(out.split(per))
     else:
-        parts = [torch.empty_like(pad) for _ in range(world)]
-        dist.all_gather(parts, pad)
+        # gloo (CPU tests; several ranks sharing one GPU, where RCCL refuses duplicate devices): stage through host
+        # memory, then back onto the rank's device
+        host = pad.cpu()
+        parts = [torch.empty_like(host) for _ in range(world)]
+        dist.all_gather(parts, host)
+        parts = [p.to(local.device) for p in parts]
     return torch.cat([p[: (lambda ab: ab[1] - ab[0])(shard_bounds(n_total, world, r))] for r, p in enumerate(parts)])
 
 

@@ -69,7 +69,7 @@ class Enhancer:
         split = self.weights.dtype == _lib.AVSE_F32_SPLIT
         pipe = ops.RangePipeline(self.weights.ctx) if split else None
         if split:
-            self.weights.ctx.range_status()
+            self.weights.ctx.set_aside_range()   # earlier forwards' bits stay readable by range_status()
 
         def chunk(a, b, checked):
             ops.forward(self.weights, clips[a:b], frames[a:b], vmean, vstd, out=pred[a:b], checked=checked)

@@ -217,7 +217,7 @@ class BatchPredictor:
 
     def __call__(self, group):
         import torch
-        from . import ops
+        from . import _lib, ops
         dw = self.network.device_weights()
         dev = torch.device("cuda", dw.ctx.device_index)
         U = len(group)
@@ -233,7 +233,8 @@ class BatchPredictor:
         pred = torch.empty_like(clips)
         for a in range(0, n, self.chunk):
             b = min(n, a + self.chunk)
-            ops.forward(dw, clips[a:b], frames[a:b], m, s, out=pred[a:b])
+            # the CLI is synchronous anyway: a float32_split batch's range guard is read per chunk (avse_forward_checked)
+            ops.forward(dw, clips[a:b], frames[a:b], m, s, out=pred[a:b], checked=dw.dtype == _lib.AVSE_F32_SPLIT)
         pred = pred.view(U, S, nm, T)
         losses = [ops.mse(pred[u], speech[u]) for u in range(U)]
         sr, fps = group[0].mixed_signal.get_sample_rate(), group[0].video_frame_rate
@@ -314,9 +315,15 @@ def predict(args):
     if world > 1:
         import torch
         import torch.distributed as dist
+        # AVSE_DIST_BACKEND=gloo runs the ranks' collectives (run directory broadcast, loss gather) over gloo instead
+        # of RCCL, and then ranks may share a GPU (local rank modulo the visible devices): RCCL refuses two ranks on
+        # one device, which is all a one-GPU box can offer (tests/test_gpu_dist.py)
+        backend = os.environ.get("AVSE_DIST_BACKEND", "nccl")
         local = int(os.environ.get("LOCAL_RANK", "0"))
+        if backend != "nccl":
+            local %= max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group(backend, **({"device_id": torch.device("cuda", local)} if backend == "nccl" else {}))
         # one timestamped run directory for every rank: rank 0 creates it
         box = [str(layout.prediction_run_dir(args.model, args.data_name)) if rank == 0 else None]
         dist.broadcast_object_list(box, 0)

@@ -218,7 +218,12 @@ int avse_range_status(avse_ctx* ctx, void* stream, uint32_t* host_bits);
 /* Stream-ordered, non-blocking form of avse_range_status for pipelines (verify batch k while batch k + 1 runs): enqueues
  * on `stream` a copy of the guard bits raised so far into *host_word (pinned host memory, e.g. hipHostMalloc; valid
  * once the stream has reached this point: record an event after the call and wait for it) and a reset of the guard, so
- * the bits of the forwards enqueued between two snapshots land in the later one. */
+ * the bits of the forwards enqueued between two snapshots land in the later one.
+ *
+ * Contract of the three guard readers: the guard words belong to the context.  Unchecked forwards of one context on
+ * several streams (or threads) OR into the same word, and avse_forward_checked uses one word per context, so per-batch
+ * attribution holds only while ONE stream at a time drives the context; concurrent pipelines each create their own
+ * context (they may share the read-only avse_weights). */
 int avse_range_snapshot(avse_ctx* ctx, void* stream, uint32_t* host_word);
 
 /* AVSE_F32_SPLIT: the activation exponent e_L of each plan layer (host_exp[0..n), n <= 20; layer L stores the pairs of

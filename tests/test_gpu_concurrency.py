@@ -47,12 +47,20 @@ def _beside_mfma(gpu, fn):
     return bad
 
 
-@pytest.mark.parametrize("n_fft,hop,spf", [(640, 160, 20), (533, 133, 24)])
-def test_spectrogram_beside_matrix_core_work(gpu, n_fft, hop, spf):
+@pytest.mark.parametrize("n_fft,hop,spf,L,stft", [(640, 160, 20, 3200, False), (533, 133, 24, 3200, False),
+                                                 (640, 160, 20, 48000, True), (533, 133, 24, 48000, True)])
+def test_spectrogram_beside_matrix_core_work(gpu, n_fft, hop, spf, L, stft):
+    """200-ms segments (k_spec_seg / k_spec533 in one block) and 3-s utterances with the complex STFT (k_spec640 /
+    k_spec533 chunked + the top_db clamp pass)."""
     from avse_amd import ops
-    x = torch.from_numpy(synth_audio(np.random.default_rng(21), 512, 3200)).to(gpu)
-    bad = _beside_mfma(gpu, lambda: ops.spectrogram(x, n_fft=n_fft, hop_length=hop, frames_per_slice=spf))
-    print(f"n_fft {n_fft}: {bad} of {REPS} reps differ from the solo spectrogram")
+    x = torch.from_numpy(synth_audio(np.random.default_rng(21), 512 if L == 3200 else 32, L)).to(gpu)
+
+    def run():
+        r = ops.spectrogram(x, n_fft=n_fft, hop_length=hop, frames_per_slice=spf, return_stft=stft)
+        return torch.cat([r[0].flatten(), torch.view_as_real(r[1]).flatten()]) if stft else r
+
+    bad = _beside_mfma(gpu, run)
+    print(f"n_fft {n_fft}, {L} samples: {bad} of {REPS} reps differ from the solo spectrogram")
     assert bad == 0
 
 

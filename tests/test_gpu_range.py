@@ -23,11 +23,12 @@ pytestmark = pytest.mark.gpu
 SPLIT = "float32_split"
 
 
-def _run(model, mel, video, dtype=SPLIT, **kw):
+def _run(model, mel, video, dtype=SPLIT, checked=True, **kw):
+    """The checked forward (avse_forward_checked): the guard bits are read before it returns."""
     from avse_amd import ops
     dw = ops.DeviceWeights(model, dtype)
     v = None if video is None else ops.to_device(video)
-    return ops.forward(dw, ops.to_device(mel), v, **kw).cpu().numpy(), dw
+    return ops.forward(dw, ops.to_device(mel), v, checked=checked, **kw).cpu().numpy(), dw
 
 
 def _rescaled(model, layer, nxt, k):
@@ -63,7 +64,7 @@ def test_overflow_is_recomputed_on_exact_fp32(gpu):
     assert np.array_equal(got, f32)
     assert rel_rms(got, ref) <= FP32_REL
     with pytest.raises(_lib.RangeError):
-        ops.forward(dw, ops.to_device(mel), ops.to_device(video), on_range="error")
+        ops.forward(dw, ops.to_device(mel), ops.to_device(video), checked=True, on_range="error")
     with warnings.catch_warnings():
         warnings.simplefilter("error")
         ops.forward(dw, ops.to_device(mel), ops.to_device(video), checked=False)
@@ -106,7 +107,7 @@ def test_zero_video_embedding_overflow_reported_every_call(gpu):
     f32 = ops.forward(ops.DeviceWeights(model, "float32"), ops.to_device(mel), None).cpu().numpy()
     for _ in range(2):
         with pytest.warns(RuntimeWarning, match="v_conv6"):
-            got = ops.forward(dw, ops.to_device(mel), None).cpu().numpy()
+            got = ops.forward(dw, ops.to_device(mel), None, checked=True).cpu().numpy()
         assert dw.last_range_bits >> 10 & 1
         assert np.array_equal(got, f32)
     assert rel_rms(got, ref) <= FP32_REL

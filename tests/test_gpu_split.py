@@ -90,7 +90,7 @@ def test_split_zero_video_batches(gpu, N):
     rng = np.random.default_rng(N)
     mel = rng.normal(-40, 15, (N, 80, 20)).astype(np.float32)
     dw = ops.DeviceWeights(model, SPLIT)
-    got = ops.forward(dw, ops.to_device(mel), None).cpu().numpy()
+    got = ops.forward(dw, ops.to_device(mel), None, checked=True).cpu().numpy()
     clips = spread_clips(N, k=12)
     ref = K.forward(model.layer_dict(), mel[clips], None)
     ae, re = abs_rms(got[clips], ref), rel_rms(got[clips], ref)
@@ -129,8 +129,9 @@ def test_split_zero_video(gpu):
 
 @pytest.mark.parametrize("T,F", [(24, 5), (24, 6)])
 def test_split_other_frame_rates(gpu, T, F):
-    """29.97 fps (5 frames: the split video kernels) and 30 fps (6 frames: v_conv1 has no split kernel, so every video
-    layer runs the generic fp32 one) networks in the split dtype."""
+    """29.97 fps (T = 24, 5 frames) and 30 fps (T = 24, 6 frames) networks in the split dtype: the video encoder runs
+    the split row-run v_conv1 (k_conv_v1s<8, 5> / <8, 6>, conv_v1r.hip) and the split stream kernels at both rates;
+    the T = 24 audio / decoder layers run the generic split k_conv."""
     from avse_amd import ops
     from avse_amd.model import KerasModel
     from conftest import synth_video

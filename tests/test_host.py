@@ -220,3 +220,28 @@ def test_predict_rank_command_threads_argv():
     i = cmd.index(se.ENTRY_SCRIPT)
     assert cmd[i + 1:] == argv
     assert os.path.isfile(se.ENTRY_SCRIPT) and os.path.basename(se.ENTRY_SCRIPT) == "speech_enhancer.py"
+
+
+def test_forward_is_asynchronous_by_default_and_the_reference_api_checks():
+    """ops.forward stays the asynchronous, capturable avse_forward unless a caller opts in; the synchronous
+    reference-shaped API (SpeechEnhancementNetwork.predict_device / predict / evaluate) opts in for split weights."""
+    import inspect
+    from avse_amd import network, ops
+    assert inspect.signature(ops.forward).parameters["checked"].default is False
+    assert inspect.signature(network.SpeechEnhancementNetwork.predict_device).parameters["checked"].default is None
+
+
+def test_range_set_aside_keeps_earlier_bits():
+    """Context.set_aside_range moves the device word's bits to the host side; range_status still returns them once."""
+    from avse_amd import _lib
+
+    class Fake(_lib.Context):
+        def __init__(self):
+            self._set_aside, self.words = 0, [0x40, 0x2, 0]
+
+        def _read_range(self, stream):
+            return self.words.pop(0)
+
+    c = Fake()
+    c.set_aside_range()
+    assert c.range_status() == 0x42 and c.range_status() == 0

@@ -112,7 +112,7 @@ def test_converted_keras_h5_runs_forward_against_oracle(tmp_path, gpu, dtype):
     video = rng.integers(0, 256, (3, 128, 128, 5)).astype(np.float32)
     ref = K.forward(m.layer_dict(), mel, video)
     dw = ops.DeviceWeights(loaded, dtype)
-    got = ops.forward(dw, torch.from_numpy(mel).to(gpu), torch.from_numpy(video).to(gpu)).cpu().numpy()
+    got = ops.forward(dw, torch.from_numpy(mel).to(gpu), torch.from_numpy(video).to(gpu), checked=True).cpu().numpy()
     err = float(np.sqrt(np.mean((got.astype(np.float64) - ref) ** 2)))
     print(f"HDF5 model, {dtype}: output RMS {np.sqrt(np.mean(ref ** 2)):.3g}, abs RMS err {err:.3e}")
     assert dw.last_range_bits == 0

@@ -2,7 +2,8 @@
 // result when matrix-core work from another kernel shares its compute units?  k_pk_victim: 448 threads (7 waves, the
 // STFT kernels' shape) with a 72-KB LDS footprint (two blocks per CU, like k_spec_seg), each lane iterating
 // x = x * a + b on a float2 `iters` times — kind 0 as v_pk_fma_f32 (inline asm), kind 1 as two v_fma_f32 — and storing
-// x; k_mfma_busy: a grid of 256-thread workgroups issuing v_mfma_f32_16x16x32_f16 back to back.
+// x (kinds 16.. : one packed-FP32 op_sel / neg form each, every form the built library contains — the allow-list of
+// tests/test_isa_guard.py; `x = FORM(x / 2, a, b) + b`); k_mfma_busy: a grid of 256-thread workgroups issuing v_mfma_f32_16x16x32_f16 back to back.
 //   hipcc --offload-arch=gfx950 -O3 -shared -fPIC tools/pk_probe.hip -o tools/_stress/libpk_probe.so
 #include <hip/hip_runtime.h>
 
@@ -44,6 +45,131 @@ __global__ __launch_bounds__(448) void k_pk_victim(const float* in, float* out, 
             const v2f h = x * v2f{0.5f, 0.5f};
             asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0]" : "=v"(r) : "v"(h), "v"(b));
             x = r;
+        } else if constexpr (KIND == 16) {   // v_pk_fma_f32 op_sel_hi:[1,0,0]
+            v2f r;
+            const v2f h = x * v2f{0.5f, 0.5f};
+            asm volatile("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(h), "v"(a), "v"(b));
+            x = r + b;
+        } else if constexpr (KIND == 17) {   // v_pk_fma_f32 op_sel_hi:[1,0,1]
+            v2f r;
+            const v2f h = x * v2f{0.5f, 0.5f};
+            asm volatile("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,1]" : "=v"(r) : "v"(h), "v"(a), "v"(b));
+            x = r + b;
+        } else if constexpr (KIND == 18) {   // v_pk_fma_f32 op_sel_hi:[1,1,0]
+            v2f r;
+            const v2f h = x * v2f{0.5f, 0.5f};
+            asm volatile("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,1,0]" : "=v"(r) : "v"(h), "v"(a), "v"(b));
+            x = r + b;
+        } else if constexpr (KIND == 19) {   // v_pk_fma_f32 op_sel_hi:[0,1,1]
+            v2f r;
+            const v2f h = x * v2f{0.5f, 0.5f};
+            asm volatile("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1]" : "=v"(r) : "v"(h), "v"(a), "v"(b));
+            x = r + b;
+        } else if constexpr (KIND == 20) {   // v_pk_fma_f32 op_sel_hi:[0,1,0]
+            v2f r;
+            const v2f h = x * v2f{0.5f, 0.5f};
+            asm volatile("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,0]" : "=v"(r) : "v"(h), "v"(a), "v"(b));
+            x = r + b;
+        } else if constexpr (KIND == 21) {   // v_pk_fma_f32 op_sel:[1,0,0]
+            v2f r;
+            const v2f h = x * v2f{0.5f, 0.5f};
+            asm volatile("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0]" : "=v"(r) : "v"(h), "v"(a), "v"(b));
+            x = r + b;
+        } else if constexpr (KIND == 22) {   // v_pk_fma_f32 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]
+            v2f r;
+            const v2f h = x * v2f{0.5f, 0.5f};
+            asm volatile("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]" : "=v"(r) : "v"(h), "v"(a), "v"(b));
+            x = r + b;
+        } else if constexpr (KIND == 23) {   // v_pk_fma_f32 op_sel:[1,0,0] op_sel_hi:[0,0,1] neg_lo:[0,1,0]
+            v2f r;
+            const v2f h = x * v2f{0.5f, 0.5f};
+            asm volatile("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[0,0,1] neg_lo:[0,1,0]" : "=v"(r) : "v"(h), "v"(a), "v"(b));
+            x = r + b;
+        } else if constexpr (KIND == 24) {   // v_pk_fma_f32 op_sel:[1,0,0] op_sel_hi:[0,0,1] neg_hi:[0,1,0]
+            v2f r;
+            const v2f h = x * v2f{0.5f, 0.5f};
+            asm volatile("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[0,0,1] neg_hi:[0,1,0]" : "=v"(r) : "v"(h), "v"(a), "v"(b));
+            x = r + b;
+        } else if constexpr (KIND == 25) {   // v_pk_fma_f32 op_sel:[1,0,0] op_sel_hi:[1,0,1]
+            v2f r;
+            const v2f h = x * v2f{0.5f, 0.5f};
+            asm volatile("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,1]" : "=v"(r) : "v"(h), "v"(a), "v"(b));
+            x = r + b;
+        } else if constexpr (KIND == 26) {   // v_pk_fma_f32 op_sel:[1,0,0] op_sel_hi:[1,1,0]
+            v2f r;
+            const v2f h = x * v2f{0.5f, 0.5f};
+            asm volatile("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,1,0]" : "=v"(r) : "v"(h), "v"(a), "v"(b));
+            x = r + b;
+        } else if constexpr (KIND == 27) {   // v_pk_fma_f32 op_sel:[0,0,1] op_sel_hi:[1,1,0]
+            v2f r;
+            const v2f h = x * v2f{0.5f, 0.5f};
+            asm volatile("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,0,1] op_sel_hi:[1,1,0]" : "=v"(r) : "v"(h), "v"(a), "v"(b));
+            x = r + b;
+        } else if constexpr (KIND == 28) {   // v_pk_fma_f32 op_sel_hi:[1,1,0] neg_lo:[1,0,0] neg_hi:[1,0,0]
+            v2f r;
+            const v2f h = x * v2f{0.5f, 0.5f};
+            asm volatile("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,1,0] neg_lo:[1,0,0] neg_hi:[1,0,0]" : "=v"(r) : "v"(h), "v"(a), "v"(b));
+            x = r + b;
+        } else if constexpr (KIND == 29) {   // v_pk_fma_f32 op_sel_hi:[1,0,1] neg_lo:[0,0,1] neg_hi:[0,0,1]
+            v2f r;
+            const v2f h = x * v2f{0.5f, 0.5f};
+            asm volatile("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,1] neg_lo:[0,0,1] neg_hi:[0,0,1]" : "=v"(r) : "v"(h), "v"(a), "v"(b));
+            x = r + b;
+        } else if constexpr (KIND == 30) {   // v_pk_mul_f32 op_sel_hi:[1,0]
+            v2f r;
+            const v2f h = x * v2f{0.5f, 0.5f};
+            asm volatile("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(r) : "v"(h), "v"(a));
+            x = r + b;
+        } else if constexpr (KIND == 31) {   // v_pk_mul_f32 op_sel_hi:[0,1]
+            v2f r;
+            const v2f h = x * v2f{0.5f, 0.5f};
+            asm volatile("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(r) : "v"(h), "v"(a));
+            x = r + b;
+        } else if constexpr (KIND == 32) {   // v_pk_add_f32 op_sel_hi:[1,0] neg_lo:[0,1] neg_hi:[0,1]
+            v2f r;
+            const v2f h = x * v2f{0.5f, 0.5f};
+            asm volatile("v_pk_add_f32 %0, %1, %2 op_sel_hi:[1,0] neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(h), "v"(a));
+            x = r + b;
+        } else if constexpr (KIND == 33) {   // v_pk_add_f32 
+            v2f r;
+            const v2f h = x * v2f{0.5f, 0.5f};
+            asm volatile("v_pk_add_f32 %0, %1, %2 " : "=v"(r) : "v"(h), "v"(a));
+            x = r + b;
+        } else if constexpr (KIND == 34) {   // v_pk_add_f32 neg_hi:[0,1]
+            v2f r;
+            const v2f h = x * v2f{0.5f, 0.5f};
+            asm volatile("v_pk_add_f32 %0, %1, %2 neg_hi:[0,1]" : "=v"(r) : "v"(h), "v"(a));
+            x = r + b;
+        } else if constexpr (KIND == 35) {   // v_pk_add_f32 neg_lo:[0,1]
+            v2f r;
+            const v2f h = x * v2f{0.5f, 0.5f};
+            asm volatile("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1]" : "=v"(r) : "v"(h), "v"(a));
+            x = r + b;
+        } else if constexpr (KIND == 36) {   // v_pk_add_f32 neg_lo:[0,1] neg_hi:[0,1]
+            v2f r;
+            const v2f h = x * v2f{0.5f, 0.5f};
+            asm volatile("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(h), "v"(a));
+            x = r + b;
+        } else if constexpr (KIND == 37) {   // v_pk_add_f32 neg_lo:[1,1] neg_hi:[1,1]
+            v2f r;
+            const v2f h = x * v2f{0.5f, 0.5f};
+            asm volatile("v_pk_add_f32 %0, %1, %2 neg_lo:[1,1] neg_hi:[1,1]" : "=v"(r) : "v"(h), "v"(a));
+            x = r + b;
+        } else if constexpr (KIND == 38) {   // v_pk_fma_f32 
+            v2f r;
+            const v2f h = x * v2f{0.5f, 0.5f};
+            asm volatile("v_pk_fma_f32 %0, %1, %2, %3 " : "=v"(r) : "v"(h), "v"(a), "v"(b));
+            x = r + b;
+        } else if constexpr (KIND == 39) {   // v_pk_fma_f32 neg_lo:[0,0,1] neg_hi:[0,0,1]
+            v2f r;
+            const v2f h = x * v2f{0.5f, 0.5f};
+            asm volatile("v_pk_fma_f32 %0, %1, %2, %3 neg_lo:[0,0,1] neg_hi:[0,0,1]" : "=v"(r) : "v"(h), "v"(a), "v"(b));
+            x = r + b;
+        } else if constexpr (KIND == 40) {   // v_pk_mul_f32 
+            v2f r;
+            const v2f h = x * v2f{0.5f, 0.5f};
+            asm volatile("v_pk_mul_f32 %0, %1, %2 " : "=v"(r) : "v"(h), "v"(a));
+            x = r + b;
         } else if constexpr (KIND == 3) {
             // the STFT's op_sel / neg packed-fp32 helpers (fft_common.h): a rotation, a -i add and a conjugate add
             const v2f t = pk_cmul_t(x, a);
@@ -103,6 +229,31 @@ extern "C" int pk_victim(int kind, const float* in, float* out, int blocks, int 
     else if (kind == 6) hipLaunchKernelGGL(k_pk_victim<6>, dim3(blocks), dim3(448), 0, (hipStream_t)stream, in, out, iters);
     else if (kind == 7) hipLaunchKernelGGL(k_pk_victim<7>, dim3(blocks), dim3(448), 0, (hipStream_t)stream, in, out, iters);
     else if (kind == 8) hipLaunchKernelGGL(k_pk_victim<8>, dim3(blocks), dim3(448), 0, (hipStream_t)stream, in, out, iters);
+    else if (kind == 16) hipLaunchKernelGGL(k_pk_victim<16>, dim3(blocks), dim3(448), 0, (hipStream_t)stream, in, out, iters);
+    else if (kind == 17) hipLaunchKernelGGL(k_pk_victim<17>, dim3(blocks), dim3(448), 0, (hipStream_t)stream, in, out, iters);
+    else if (kind == 18) hipLaunchKernelGGL(k_pk_victim<18>, dim3(blocks), dim3(448), 0, (hipStream_t)stream, in, out, iters);
+    else if (kind == 19) hipLaunchKernelGGL(k_pk_victim<19>, dim3(blocks), dim3(448), 0, (hipStream_t)stream, in, out, iters);
+    else if (kind == 20) hipLaunchKernelGGL(k_pk_victim<20>, dim3(blocks), dim3(448), 0, (hipStream_t)stream, in, out, iters);
+    else if (kind == 21) hipLaunchKernelGGL(k_pk_victim<21>, dim3(blocks), dim3(448), 0, (hipStream_t)stream, in, out, iters);
+    else if (kind == 22) hipLaunchKernelGGL(k_pk_victim<22>, dim3(blocks), dim3(448), 0, (hipStream_t)stream, in, out, iters);
+    else if (kind == 23) hipLaunchKernelGGL(k_pk_victim<23>, dim3(blocks), dim3(448), 0, (hipStream_t)stream, in, out, iters);
+    else if (kind == 24) hipLaunchKernelGGL(k_pk_victim<24>, dim3(blocks), dim3(448), 0, (hipStream_t)stream, in, out, iters);
+    else if (kind == 25) hipLaunchKernelGGL(k_pk_victim<25>, dim3(blocks), dim3(448), 0, (hipStream_t)stream, in, out, iters);
+    else if (kind == 26) hipLaunchKernelGGL(k_pk_victim<26>, dim3(blocks), dim3(448), 0, (hipStream_t)stream, in, out, iters);
+    else if (kind == 27) hipLaunchKernelGGL(k_pk_victim<27>, dim3(blocks), dim3(448), 0, (hipStream_t)stream, in, out, iters);
+    else if (kind == 28) hipLaunchKernelGGL(k_pk_victim<28>, dim3(blocks), dim3(448), 0, (hipStream_t)stream, in, out, iters);
+    else if (kind == 29) hipLaunchKernelGGL(k_pk_victim<29>, dim3(blocks), dim3(448), 0, (hipStream_t)stream, in, out, iters);
+    else if (kind == 30) hipLaunchKernelGGL(k_pk_victim<30>, dim3(blocks), dim3(448), 0, (hipStream_t)stream, in, out, iters);
+    else if (kind == 31) hipLaunchKernelGGL(k_pk_victim<31>, dim3(blocks), dim3(448), 0, (hipStream_t)stream, in, out, iters);
+    else if (kind == 32) hipLaunchKernelGGL(k_pk_victim<32>, dim3(blocks), dim3(448), 0, (hipStream_t)stream, in, out, iters);
+    else if (kind == 33) hipLaunchKernelGGL(k_pk_victim<33>, dim3(blocks), dim3(448), 0, (hipStream_t)stream, in, out, iters);
+    else if (kind == 34) hipLaunchKernelGGL(k_pk_victim<34>, dim3(blocks), dim3(448), 0, (hipStream_t)stream, in, out, iters);
+    else if (kind == 35) hipLaunchKernelGGL(k_pk_victim<35>, dim3(blocks), dim3(448), 0, (hipStream_t)stream, in, out, iters);
+    else if (kind == 36) hipLaunchKernelGGL(k_pk_victim<36>, dim3(blocks), dim3(448), 0, (hipStream_t)stream, in, out, iters);
+    else if (kind == 37) hipLaunchKernelGGL(k_pk_victim<37>, dim3(blocks), dim3(448), 0, (hipStream_t)stream, in, out, iters);
+    else if (kind == 38) hipLaunchKernelGGL(k_pk_victim<38>, dim3(blocks), dim3(448), 0, (hipStream_t)stream, in, out, iters);
+    else if (kind == 39) hipLaunchKernelGGL(k_pk_victim<39>, dim3(blocks), dim3(448), 0, (hipStream_t)stream, in, out, iters);
+    else if (kind == 40) hipLaunchKernelGGL(k_pk_victim<40>, dim3(blocks), dim3(448), 0, (hipStream_t)stream, in, out, iters);
     else hipLaunchKernelGGL(k_pk_victim<2>, dim3(blocks), dim3(448), 0, (hipStream_t)stream, in, out, iters);
     return hipGetLastError() == hipSuccess ? 0 : 1;
 }

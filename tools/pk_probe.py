@@ -9,6 +9,13 @@ import sys
 import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+from isa_forms import PROBE_FORMS   # noqa: E402  (kind -> (mnemonic, modifiers); the ISA guard's allow-list)
+
+NAMES = {0: 'v_pk_fma_f32', 1: 'v_fma_f32', 2: 'LDS round trip + v_pk_fma_f32', 3: 'STFT op_sel packed helpers',
+         4: 'pk_fma op_sel+neg (pk_cmul_t)', 5: 'pk_add op_sel+neg (pk_add_mi)', 6: 'pk_add neg only (pk_sub_conj)',
+         7: 'pk_add op_sel only', 8: 'pk_add_mi / pk_sub_mi as v_pk_fma (round 5)'}
+NAMES.update({k: f"{mn} {mod}" for k, (mn, mod) in PROBE_FORMS.items()})
 
 
 def main():
@@ -40,7 +47,7 @@ def main():
                     idx = diff.nonzero().flatten()
                     elems += idx.numel()
                     lanes |= set((idx % 64).tolist())
-            print(f"kind {kind} ({['v_pk_fma_f32', 'v_fma_f32', 'LDS round trip + v_pk_fma_f32', 'STFT op_sel packed helpers', 'pk_fma op_sel+neg (pk_cmul_t)', 'pk_add op_sel+neg (pk_add_mi)', 'pk_add neg only (pk_sub_conj)', 'pk_add op_sel only', 'pk_add_mi / pk_sub_mi as v_pk_fma (round 5)'][kind]}) {mode}: {nbad} of {reps} runs differ "
+            print(f"kind {kind} ({NAMES.get(kind, '?')}) {mode}: {nbad} of {reps} runs differ "
                   f"({elems} threads); lanes {sorted(lanes)[:16]}{' ...' if len(lanes) > 16 else ''} "
                   f"({len([l for l in lanes if l >= 32])} of {len(lanes)} in 32..63)", flush=True)
 
