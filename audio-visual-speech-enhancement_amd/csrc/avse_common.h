@@ -266,8 +266,15 @@ struct DecTailArgs {
     int pt5, pl5, rows5, pitch5;   // zero-padded d_deconv4 output image
     const float* w6;         // d_deconv6 1x1 weights [64] + bias
     float b6;
+    // split-f16 tail (conv_dects.hip, AVSE_F32_SPLIT): in = d_deconv3's split pairs [N][40][10][8 x (h(16) | l(16))],
+    // w4 / w5 the layers' split packings ([Cout][2 kpad] halves, each 16-k slab row [Wh(16) | Wl(16)]); d_deconv4's
+    // stored pairs report into the range guard
+    unsigned* range_flag;
+    unsigned range_bit;
 };
 bool dec_tail_supported(const DecTailArgs& a);
+bool dec_tail_s16_supported(const DecTailArgs& a);
+int launch_dec_tail_s16(const DecTailArgs& a, hipStream_t s);
 
 // fused audio encoder a_conv1 -> a_conv5, one workgroup per clip (conv_aud.hip, bf16)
 struct AudEncArgs {

@@ -1590,6 +1590,16 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
                 continue;
             }
         }
+        if (i == 3 && split && !opt.unfused_tail && !opt.no_dectail) {
+            // d_deconv4 + d_deconv5 + d_deconv6 on split pairs, one workgroup per half clip (conv_dects.hip)
+            DecTailArgs da = dec_tail_args(L(17), L(18), W, buf(d_in[3]), out, N);
+            da.range_flag = rflag;
+            da.range_bit = 1u << 17;
+            if (dec_tail_s16_supported(da)) {
+                if ((rc = launch_dec_tail_s16(da, s)) || (rc = mark()) || (rc = mark())) return rc;   // d4, d5 stages
+                break;
+            }
+        }
         if (i == 3 && dt == AVSE_BF16 && !opt.unfused_tail && !opt.no_dectail) {
             // d_deconv4 + d_deconv5 + d_deconv6 in one kernel, one workgroup per clip (conv_dec.hip)
             const DecTailArgs da = dec_tail_args(L(17), L(18), W, buf(d_in[3]), out, N);

@@ -30,10 +30,11 @@ PROBE_FORMS = {
     38: ('v_pk_fma_f32', ''),
     39: ('v_pk_fma_f32', 'neg_lo:[0,0,1] neg_hi:[0,0,1]'),
     40: ('v_pk_mul_f32', ''),
+    41: ('v_pk_add_f32', 'op_sel_hi:[1,0]'),   # round 6: conv_dects.hip
 }
 
 # cleared on the MI355X (profiles/r06a_pk_probe_forms.log): every kind 16..40 gave 0 of 8 differing runs beside the
 # MFMA loop, while the known-bad controls (kinds 5, 7) differed in 8 of 8, lanes 48..63
-CLEARED = set(PROBE_FORMS.values())
+CLEARED = set(PROBE_FORMS.values())   # kind 41: profiles/r06b_pk_probe_form41.log
 
 KNOWN_BAD = {("v_pk_add_f32", "op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]"), ("v_pk_add_f32", "op_sel:[0,1] op_sel_hi:[1,0]")}

@@ -66,8 +66,10 @@ def test_split_bench_batch_matches_oracle(gpu, N):
     inter = {}
     vn = R.video_normalize(video_np[clips], mean_np, std_np).astype(np.float32)
     ref = K.forward(model.layer_dict(), mel_np, vn, intermediates=inter)
+    # d_deconv4's output lives only in LDS in the fused split tail (conv_dects.hip): it is checked layer by layer in
+    # test_split_intermediates and test_split_fused_tail_matches_layer_path
     names = ["v_conv1", "v_conv2", "v_conv3", "v_conv4", "v_conv5", "concat", "enc_dense", "dec_dense1", "dec_dense2",
-             "d_deconv1", "d_deconv2", "d_deconv3", "d_deconv4"]
+             "d_deconv1", "d_deconv2", "d_deconv3"]
     sc = scratch(dw, N, clips, names)
     layers = {k: rel_rms(sc[k], inter[k]) for k in names}
     ae = abs_rms(out[clips], ref)
@@ -201,9 +203,10 @@ def test_split_windowed_layers_match_kconv_and_oracle(gpu, N):
     ref = K.forward(model.layer_dict(), mel, video, intermediates=inter)
     names = ["a_conv2", "d_deconv1", "d_deconv2", "d_deconv3", "d_deconv4"]
     dw = ops.DeviceWeights(model, SPLIT)
-    got = ops.forward(dw, ops.to_device(mel), ops.to_device(video)).cpu().numpy()
-    sc = scratch(dw, N, names=names)
-    with _lib.context().options(no_win=1):
+    with _lib.context().options(no_dectail=1):   # d_deconv4 materialised (the fused tail keeps it in LDS)
+        got = ops.forward(dw, ops.to_device(mel), ops.to_device(video)).cpu().numpy()
+        sc = scratch(dw, N, names=names)
+    with _lib.context().options(no_win=1, no_dectail=1):
         got_k = ops.forward(dw, ops.to_device(mel), ops.to_device(video)).cpu().numpy()
         sck = scratch(dw, N, names=names)
     for k in names:
@@ -212,3 +215,31 @@ def test_split_windowed_layers_match_kconv_and_oracle(gpu, N):
     ae, aek = abs_rms(got, ref), abs_rms(got_k, ref)
     print(f"output abs RMS: windowed {ae:.3e}, k_conv {aek:.3e}")
     assert ae <= FP32_ABS and rel_rms(got, got_k) <= 1e-6
+
+
+@pytest.mark.parametrize("N", [1, 3, 37, 512])
+def test_split_fused_tail_matches_layer_path(gpu, N):
+    """conv_dects.hip (d_deconv4 -> d_deconv5 -> d_deconv6 on split pairs, one workgroup per half clip, d_deconv4's
+    output in LDS) against the layer-by-layer path (option no_dectail: k_conv_win + k_conv with the fused d_deconv6 dot)
+    and the float64 oracle: the same products in another summation order, so the two agree within fp32 rounding; both
+    halves of every clip (the recomputed d_deconv4 row at the seam), N = 1 .. the bench batch."""
+    from avse_amd import _lib, ops
+    from avse_amd.model import KerasModel
+    model = db_scale(KerasModel.init(seed=41, randomize=True))
+    mel, video = make_inputs(N, 141)
+    dw = ops.DeviceWeights(model, SPLIT)
+    fused = ops.forward(dw, ops.to_device(mel), ops.to_device(video), checked=True).cpu().numpy()
+    assert dw.last_range_bits == 0
+    with _lib.context().options(no_dectail=1):
+        layer = ops.forward(dw, ops.to_device(mel), ops.to_device(video)).cpu().numpy()
+    clips = spread_clips(N, k=6)
+    ref = K.forward(model.layer_dict(), mel[clips], video[clips])
+    ae, ael = abs_rms(fused[clips], ref), abs_rms(layer[clips], ref)
+    d = rel_rms(fused, layer)
+    print(f"N={N}: fused tail vs layer path rel {d:.2e}; abs RMS vs oracle fused {ae:.3e} layer {ael:.3e}")
+    assert np.isfinite(fused).all()
+    assert d <= 1e-6, d
+    assert ae <= FP32_ABS and rel_rms(fused[clips], ref) <= FP32_REL
+    # the seam: output rows 38..41 come from d_deconv4 rows 19 / 20, computed by both halves
+    seam = rel_rms(fused[:, 36:44], layer[:, 36:44])
+    assert seam <= 1e-6, seam

@@ -170,6 +170,11 @@ __global__ __launch_bounds__(448) void k_pk_victim(const float* in, float* out, 
             const v2f h = x * v2f{0.5f, 0.5f};
             asm volatile("v_pk_mul_f32 %0, %1, %2 " : "=v"(r) : "v"(h), "v"(a));
             x = r + b;
+        } else if constexpr (KIND == 41) {   // v_pk_add_f32 op_sel_hi:[1,0]
+            v2f r;
+            const v2f h = x * v2f{0.5f, 0.5f};
+            asm volatile("v_pk_add_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(r) : "v"(h), "v"(a));
+            x = r + b;
         } else if constexpr (KIND == 3) {
             // the STFT's op_sel / neg packed-fp32 helpers (fft_common.h): a rotation, a -i add and a conjugate add
             const v2f t = pk_cmul_t(x, a);
@@ -254,6 +259,7 @@ extern "C" int pk_victim(int kind, const float* in, float* out, int blocks, int 
     else if (kind == 38) hipLaunchKernelGGL(k_pk_victim<38>, dim3(blocks), dim3(448), 0, (hipStream_t)stream, in, out, iters);
     else if (kind == 39) hipLaunchKernelGGL(k_pk_victim<39>, dim3(blocks), dim3(448), 0, (hipStream_t)stream, in, out, iters);
     else if (kind == 40) hipLaunchKernelGGL(k_pk_victim<40>, dim3(blocks), dim3(448), 0, (hipStream_t)stream, in, out, iters);
+    else if (kind == 41) hipLaunchKernelGGL(k_pk_victim<41>, dim3(blocks), dim3(448), 0, (hipStream_t)stream, in, out, iters);
     else hipLaunchKernelGGL(k_pk_victim<2>, dim3(blocks), dim3(448), 0, (hipStream_t)stream, in, out, iters);
     return hipGetLastError() == hipSuccess ? 0 : 1;
 }
