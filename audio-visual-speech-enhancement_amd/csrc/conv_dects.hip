@@ -35,6 +35,15 @@
 namespace avse {
 namespace {
 
+// timing ablations (tools/_ab variant libraries only; 0 in the library): 1 = no MFMAs (fragment reads kept alive),
+// 2 = no fragment reads in the loops (MFMAs on the prologue's fragments), 4 = no barriers in the loops.  Measured
+// (profiles/r06c_split_tail_ablate.txt, B = 512): full 0.335 ms, 1: 0.188, 2: 0.306, 4: 0.326.  Also measured and
+// not kept: the stream kernels' three-product slab pairs (Wl Al dropped, A' by v_permlane32_swap): 0.343 vs 0.335 ms
+// (the tail is not MFMA-issue-bound: 14 MFMAs per slab per wave, ~54 % MFMA busy)
+#ifndef AVSE_DECTS_ABL
+#define AVSE_DECTS_ABL 0
+#endif
+constexpr int DABL = AVSE_DECTS_ABL;
 constexpr float LRELU = 0.3f;
 constexpr int kOOB = 0x7fffff00;
 constexpr int H = 40, W = 10;                        // d_deconv4 / d_deconv5 grid of a clip
@@ -78,9 +87,13 @@ __device__ __forceinline__ float bn_lrelu(float acc, float sc, float sh) {
     return fmaxf(v, LRELU * v);
 }
 // LDS stores of this wave drained, then the workgroup barrier (global loads stay in flight across it)
-__device__ __forceinline__ void lds_barrier() {
+__device__ __forceinline__ void lds_barrier_raw() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     asm volatile("s_barrier" ::: "memory");
+}
+__device__ __forceinline__ void lds_barrier() { lds_barrier_raw(); }
+__device__ __forceinline__ void loop_barrier() {
+    if constexpr (!(DABL & 4)) lds_barrier_raw();
 }
 template <int... I, typename F>
 __device__ __forceinline__ void unroll(std::integer_sequence<int, I...>, F&& f) {
@@ -124,6 +137,12 @@ __global__ __launch_bounds__(NT, 1) void k_dec_tail_s16(DecTailArgs a) {
     };
     // D = W x A: a lane holds channels 16 cb + 4 kg .. + 3 of pixel r16 of each fragment
     auto mfma_all = [&](const i32x4 (&fa)[SL], const i32x4 (&fw)[2], bool slot6) {
+        if constexpr (DABL & 1) {
+#pragma unroll
+            for (int i = 0; i < SL; ++i) asm volatile("" ::"v"(fa[i]));
+            asm volatile("" ::"v"(fw[0]), "v"(fw[1]));
+            return;
+        }
 #pragma unroll
         for (int i = 0; i < SL; ++i) {
             if (i == SL - 1 && !slot6) continue;
@@ -201,7 +220,10 @@ __global__ __launch_bounds__(NT, 1) void k_dec_tail_s16(DecTailArgs a) {
         lds_barrier();
 
         i32x4 fa[2][SL], fw[2][2];
-        i32x4 pr[NPC];   // next chunk's window pieces: loaded at tap k < NPC, stored at tap k + 3
+        // next chunk's window pieces: loaded at tap k < NPC, stored at tap k + 12, before the chunk's last barrier
+        // (stored 3 taps after the load: 0.335 vs 0.333 ms, not their latency)
+        constexpr int PST = 12;
+        i32x4 pr[NPC];
         int wb = 0;      // byte offset of the window buffer being read
         auto read_a = [&](auto tt, i32x4 (&f)[SL]) {
             constexpr int t = decltype(tt)::value % 16;
@@ -224,18 +246,19 @@ __global__ __launch_bounds__(NT, 1) void k_dec_tail_s16(DecTailArgs a) {
                 else pb[t & 3] = bpiece(std::integral_constant<int, t + 8 - 16>{}, cn);   // past the layer: unused
                 // window piece t of chunk c + 1 (after the last chunk: a harmless re-read, never stored)
                 if constexpr (t < NPC) pr[t] = __builtin_amdgcn_raw_buffer_load_b128(rsIn, psrc[t], cn, 0);
-                if constexpr (t >= 3 && t - 3 < NPC) {
-                    if (pok[t - 3] && c < 7) *reinterpret_cast<i32x4*>(lds + nb + pdst[t - 3]) = pr[t - 3];
+                if constexpr (t >= PST && t - PST < NPC) {
+                    if (pok[t - PST] && c < 7) *reinterpret_cast<i32x4*>(lds + nb + pdst[t - PST]) = pr[t - PST];
                 }
-                if constexpr (t % 4 == 3) lds_barrier();
+                if constexpr (t % 4 == 3) loop_barrier();
                 if constexpr (t == 15) wb = nb;
                 // the next slab's fragments go out before this slab's MFMAs
-                if constexpr (t < 15) {
+                if constexpr (DABL & 2) {
+                } else if constexpr (t < 15) {
                     read_a(std::integral_constant<int, t + 1>{}, fa[(t + 1) & 1]);
                 } else if (c < 7) {
                     read_a(std::integral_constant<int, 0>{}, fa[0]);
                 }
-                read_w((((t + 1) / 4) & 1) * 16384 + ((t + 1) % 4) * 4096, fw[(t + 1) & 1]);
+                if constexpr (!(DABL & 2)) read_w((((t + 1) / 4) & 1) * 16384 + ((t + 1) % 4) * 4096, fw[(t + 1) & 1]);
                 __builtin_amdgcn_sched_barrier(0);
                 mfma_all(fa[t & 1], fw[t & 1], true);
                 if constexpr (t % 8 == 7) flush();
@@ -355,8 +378,8 @@ __global__ __launch_bounds__(NT, 1) void k_dec_tail_s16(DecTailArgs a) {
         __builtin_amdgcn_sched_barrier(0);
         st8(bst + (((g / 4) + 1) & 1) * 16384 + (g % 4) * 4096, pb[g & 3]);
         pb[g & 3] = bpiece5(std::integral_constant<int, g + 8>{});
-        if constexpr (g % 4 == 3) lds_barrier();
-        if constexpr (!last) {
+        if constexpr (g % 4 == 3) loop_barrier();
+        if constexpr (!last && !(DABL & 2)) {
             read_a5(std::integral_constant<int, g + 1>{}, fa[(g + 1) & 1]);
             read_w((((g + 1) / 4) & 1) * 16384 + ((g + 1) % 4) * 4096, fw[(g + 1) & 1]);
         }
