@@ -142,7 +142,8 @@ def test_tiny_activations_keep_fp32_accuracy(gpu, layer, nxt):
     assert ae0 > 3 * ae                    # the subnormal lo pieces cost accuracy without the exponent
 
 
-@pytest.mark.parametrize("layer,nxt", [("v_conv2", "v_conv3"), ("dec_dense1", "dec_dense2"), ("d_deconv4", "d_deconv5")])
+@pytest.mark.parametrize("layer,nxt", [("v_conv2", "v_conv3"), ("dec_dense1", "dec_dense2"), ("d_deconv2", "d_deconv3"),
+                                       ("d_deconv4", "d_deconv5")])
 def test_huge_activations_keep_headroom(gpu, layer, nxt):
     """layer's activations x 2^14 (~1e5 .. 1e6): with exponents the layer stores x 2^-14 .. and no pair overflows; without
     them the range guard fires and the batch is recomputed on the exact-fp32 kernels."""

@@ -36,7 +36,7 @@ def test_split_forward_matches_oracle(gpu, N, db):
 def test_split_intermediates(gpu):
     """Every layer (the split-pair buffers decoded h + l) against the oracle; the fused d_deconv6 is unfused here."""
     from avse_amd import _lib
-    with _lib.context().options(unfused_tail=1):
+    with _lib.context().options(unfused_tail=1):   # every decoder layer materialised
         got, ref, inter, dw = run_case(gpu, 2, SPLIT, seed=21, normalize=True)
         sc = scratch(dw, 2)
     for k in inter:
@@ -67,7 +67,7 @@ def test_split_bench_batch_matches_oracle(gpu, N):
     vn = R.video_normalize(video_np[clips], mean_np, std_np).astype(np.float32)
     ref = K.forward(model.layer_dict(), mel_np, vn, intermediates=inter)
     # d_deconv4's output lives only in LDS in the fused split tail (conv_dects.hip): it is checked layer by layer in
-    # test_split_intermediates and test_split_fused_tail_matches_layer_path
+    # test_split_intermediates and against the layer path in test_split_fused_tail_matches_layer_path
     names = ["v_conv1", "v_conv2", "v_conv3", "v_conv4", "v_conv5", "concat", "enc_dense", "dec_dense1", "dec_dense2",
              "d_deconv1", "d_deconv2", "d_deconv3"]
     sc = scratch(dw, N, clips, names)
