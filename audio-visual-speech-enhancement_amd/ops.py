@@ -107,6 +107,32 @@ def istft(mel_db, stft, sample_rate=16000, n_fft=640, hop_length=160, n_mels=80,
     return out
 
 
+def act_exponent(model, layer):
+    """The AVSE_F32_SPLIT activation exponent rule of csrc/capi.hip act_exponents for one layer: with M =
+    max_c (|beta_c| + |gamma_c|) of its BatchNormalization, 0 for M in [2^-2, 2^8], else 3 - ceil-exponent(M) (M 2^e in
+    (4, 8]), clamped to [-24, 24]."""
+    g = np.abs(np.asarray(model.tensors[layer + "_bn/gamma"], np.float64))
+    b = np.abs(np.asarray(model.tensors[layer + "_bn/beta"], np.float64))
+    m = float(np.max(b + g))
+    if not m > 0.0 or not np.isfinite(m) or 0.25 <= m <= 256.0:
+        return 0
+    return int(max(-24, min(24, 3 - np.frexp(m)[1])))
+
+
+def _warn_concat_exponents(model):
+    """a_conv5 and v_conv6 write the two halves of one concat row that enc_dense reads as one K, so they share one
+    exponent, the smaller (capi.hip act_exponents).  When the halves' own rules disagree, the half that wanted the larger
+    exponent is stored with fewer than the pairs' ~22 bits (its lo pieces run into the f16 subnormals): flag it at load
+    time — the range guard reports overflow and NaN, not this precision loss."""
+    ea, ev = act_exponent(model, "a_conv5"), act_exponent(model, "v_conv6")
+    if ea != ev:
+        import warnings
+        warnings.warn(f"float32_split: the concat halves want activation exponents {ea} (a_conv5) and {ev} (v_conv6); "
+                      f"both are stored at {min(ea, ev)}, so the {'audio' if ea > ev else 'video'} half's activations "
+                      f"lose precision (BatchNormalization parameters outside [2^-2, 2^8]); use dtype float32 for exact "
+                      "fp32 if that matters", RuntimeWarning, stacklevel=3)
+
+
 class DeviceWeights:
     """avse_weights: BN-folded, GEMM-packed weights resident on one device."""
 
@@ -117,6 +143,8 @@ class DeviceWeights:
         self.ctx = _lib.context(device)
         self.T, self.F = model.T, model.F
         self.last_range_bits = 0
+        if self.dtype == _lib.AVSE_F32_SPLIT:
+            _warn_concat_exponents(model)
         blob = model.to_blob()
         # the CDLL is held here: at interpreter exit the module globals may be gone before this object
         self._cdll = _lib.load()

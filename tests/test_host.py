@@ -245,3 +245,21 @@ def test_range_set_aside_keeps_earlier_bits():
     c = Fake()
     c.set_aside_range()
     assert c.range_status() == 0x42 and c.range_status() == 0
+
+
+def test_concat_exponent_mismatch_is_flagged_at_load():
+    """a_conv5 / v_conv6 share the smaller activation exponent; a model whose halves want different ones is
+    flagged when float32_split weights are built (the rule restated from csrc/capi.hip act_exponents)."""
+    import warnings
+    from avse_amd import ops
+    from avse_amd.model import KerasModel
+    m = KerasModel.init(seed=3, randomize=True)
+    assert ops.act_exponent(m, "a_conv5") == ops.act_exponent(m, "v_conv6") == 0
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        ops._warn_concat_exponents(m)
+    for p in ("gamma", "beta"):
+        m.tensors["v_conv6_bn/" + p] = (m.tensors["v_conv6_bn/" + p] * np.float32(2.0 ** -14)).astype(np.float32)
+    assert ops.act_exponent(m, "v_conv6") >= 14
+    with pytest.warns(RuntimeWarning, match="video half"):
+        ops._warn_concat_exponents(m)
