@@ -41,6 +41,8 @@ struct Options {
     int dense_istft = 0;      // AVSE_DENSE_ISTFT: ISTFT through the dense pinv + scratch frames + k_ola (not fused)
     int no_act_scale = 0;     // AVSE_NO_ACT_SCALE: split weights loaded without per-layer activation exponents
     int no_win = 0;           // AVSE_NO_WIN: split stride-1 gather layers on k_conv, not the windowed conv_win.hip
+    int no_v1p = 0;           // AVSE_NO_V1P: split 5-frame v_conv1 on k_conv_v1s (K 160), not k_conv_v1p (K 128; read at load)
+    int side_prio = 0;        // AVSE_SIDE_PRIO: audio side stream priority (0 default, 1 least, 2 greatest; read when created)
 };
 
 #define AVSE_HIP_CHECK(expr)                                                                   \
@@ -331,7 +333,7 @@ int launch_aud_enc(const AudEncArgs& a, hipStream_t s);
 int launch_dec_tail(const DecTailArgs& a, hipStream_t s);
 
 // ---- tiled bf16 video convolutions: conv_v1r.hip (v_conv1), conv_stream.hip (v_conv2..v_conv5) ----
-enum HaloVariant { HALO_NONE = -1, HALO_V1 = 0, HALO_K5 = 1, HALO_K3_16 = 2, HALO_K3_8 = 3 };
+enum HaloVariant { HALO_NONE = -1, HALO_V1 = 0, HALO_K5 = 1, HALO_K3_16 = 2, HALO_K3_8 = 3, HALO_V1P = 4 };
 // output element format of the tiled video convolutions: bf16; split f16 pairs (per pixel and 16 channels,
 // [h(16) | l(16)] with h = f16(x), l = f16(x - h): the next split layer's input); f32
 enum HaloOut { OUT_BF16 = 0, OUT_S16 = 1, OUT_F32 = 2 };

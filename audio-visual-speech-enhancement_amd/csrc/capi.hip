@@ -198,6 +198,8 @@ const OptionName kOptionNames[] = {
     {"dense_istft", "AVSE_DENSE_ISTFT", &Options::dense_istft},
     {"no_act_scale", "AVSE_NO_ACT_SCALE", &Options::no_act_scale},
     {"no_win", "AVSE_NO_WIN", &Options::no_win},
+    {"no_v1p", "AVSE_NO_V1P", &Options::no_v1p},
+    {"side_prio", "AVSE_SIDE_PRIO", &Options::side_prio},
 };
 
 struct avse_weights {
@@ -751,7 +753,8 @@ int build_layer(avse_weights* W, int li, const float* kernel, const float* bias,
     // Split dtype: the same kernels on split-f16 operands (see below).
     if ((W->dtype == AVSE_BF16 || split) && L.kind == CONV && L.pool && L.hin >= 8 && !opt.no_halo) {
         const int ntap = L.kh * L.kw;
-        if ((L.cin == 5 || L.cin == 6) && L.kh == 5) G.halo = HALO_V1;   // conv_v1r.hip: 5 (25 / 29.97 fps) or 6 frames (30)
+        if ((L.cin == 5 || L.cin == 6) && L.kh == 5)   // conv_v1r.hip: 5 (25 / 29.97 fps) or 6 frames (30)
+            G.halo = split && L.cin == 5 && L.kw == 5 && L.cout == 128 && !opt.no_v1p ? HALO_V1P : HALO_V1;
         else if (L.cin % 128) G.halo = HALO_NONE;
         else if (L.kh == 5) G.halo = HALO_K5;
         else if (L.hin >= 16) G.halo = HALO_K3_16;
@@ -782,7 +785,30 @@ int build_layer(avse_weights* W, int li, const float* kernel, const float* bias,
             }
             auto wsc = [&](int n, float v) { return std::ldexp(sgn[n] * v, ex[n]); };
             std::vector<uint16_t> sp;
-            if (G.halo == HALO_V1) {
+            if (G.halo == HALO_V1P) {
+                // conv_v1r.hip k_conv_v1p: [piece h / l][K-slice s][Cout][32]; k-group g = 4 s + kg (8 k each):
+                //   s = 0..2, kg = ky (0..3), and s = 3, kg = s' (0..2) for ky = 4, of type s' / s:
+                //   0: kx 0, 1 x frames 0..3;  1: kx 2, 3 x frames 0..3;  2: kx 4 x frames 0..3, then kx 0..3 x frame 4;
+                //   s = 3, kg = 3: (ky 0..4, kx 4) x frame 4, three zeros
+                const size_t img = (size_t)4 * L.cout * 32;
+                sp.assign(2 * img, 0);
+                auto wt = [&](int n, int ky, int kx, int f) { return wsc(n, kernel[((size_t)(ky * 5 + kx) * 5 + f) * L.cout + n]); };
+                for (int g = 0; g < 16; ++g)
+                    for (int n = 0; n < L.cout; ++n)
+                        for (int j = 0; j < 8; ++j) {
+                            const int sl = g >> 2, kg = g & 3;
+                            const int t = sl < 3 ? sl : kg, ky = sl < 3 ? kg : 4;
+                            float v = 0.f;
+                            if (t == 0) v = wt(n, ky, j >> 2, j & 3);
+                            else if (t == 1) v = wt(n, ky, 2 + (j >> 2), j & 3);
+                            else if (t == 2) v = j < 4 ? wt(n, ky, 4, j) : wt(n, ky, j - 4, 4);
+                            else if (j < 5) v = wt(n, j, 4, 4);
+                            const uint16_t h = f2h(v);
+                            const size_t o = ((size_t)(g >> 2) * L.cout + n) * 32 + (g & 3) * 8 + j;
+                            sp[o] = h;
+                            sp[img + o] = f2h(v - h2f(h));
+                        }
+            } else if (G.halo == HALO_V1) {
                 // conv_v1r.hip k_conv_v1s: [piece h / l][kernel row ky][Cout][32], k = kx * 6 + frame
                 const size_t img = (size_t)L.kh * L.cout * 32;
                 sp.assign(2 * img, 0);
@@ -1398,13 +1424,13 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
                     h.range_flag = rflag;
                     h.range_bit = 1u << (5 + i);
                     h.range_in_bit = kRangeVideoIn;
-                    if (G.halo != HALO_V1) h.Ci = 2 * G.def.cin;
+                    if (G.halo != HALO_V1 && G.halo != HALO_V1P) h.Ci = 2 * G.def.cin;
                     h.out_mode = OUT_S16;
                     h.out_clip_stride *= 2;
                     h.out_pix_stride *= 2;
                     h.out_c_off *= 2;
                 }
-                rc = G.halo == HALO_V1 ? launch_conv_v1r(h, s) : launch_conv_stream(h, s);
+                rc = G.halo == HALO_V1 || G.halo == HALO_V1P ? launch_conv_v1r(h, s) : launch_conv_stream(h, s);
                 if (rc || (rc = mark())) return rc;
                 continue;
             }
@@ -1497,7 +1523,13 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
     hipStream_t sa = s;
     if (concurrent) {
         if (!c->side) {
-            AVSE_HIP_CHECK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+            if (opt.side_prio) {
+                int least = 0, greatest = 0;
+                AVSE_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+                AVSE_HIP_CHECK(hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, opt.side_prio == 1 ? least : greatest));
+            } else {
+                AVSE_HIP_CHECK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+            }
             AVSE_HIP_CHECK(hipEventCreateWithFlags(&c->fork, hipEventDisableTiming));
             AVSE_HIP_CHECK(hipEventCreateWithFlags(&c->join, hipEventDisableTiming));
         }

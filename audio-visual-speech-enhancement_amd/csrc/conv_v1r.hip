@@ -635,12 +635,344 @@ __global__ __launch_bounds__(64 * (CW + 4), 1) void k_conv_v1s(HaloArgs a) {
     range_report(a.range_flag, a.range_bit, bad);
 }
 
+// ------------------------------------------------------------------------------------------------------------
+// k_conv_v1p: split v_conv1 for 5-frame clips (25 / 29.97 fps) with K = 128 instead of k_conv_v1s's 5 x 32 = 160 (125
+// real k: 22 % of v1s's MFMA products multiply zero weights).  The 16 k-groups of 8 (four K-slices of 32) are each two
+// 8-byte LDS reads per lane from one window image laid out per window row y' (0..19) as
+//   P  at   0: pixel x' (0..19): frames 0..3                                (8 B)
+//   R  at 160: x (0..15): frame 4 of pixels x .. x + 3 of the row           (8 B)
+//   S0 at 288: x (0..15), rows y' < 16: frame 4 of pixels (y' .. y' + 3, x + 4)
+//   S1 at 416: x (0..15), rows y' < 16: frame 4 of pixel (y' + 4, x + 4), three zeros
+// and the groups, g = 4 slice + kg (kg = lane >> 4; the B image's k order, capi.hip build_layer HALO_V1P):
+//   slice 0, kg = ky (0..3): P(py + ky, px), P(py + ky, px + 1)        kx 0, 1 x frames 0..3
+//   slice 1, kg = ky:        P(py + ky, px + 2), P(py + ky, px + 3)    kx 2, 3 x frames 0..3
+//   slice 2, kg = ky:        P(py + ky, px + 4), R(py + ky, px)        kx 4 x frames 0..3, then kx 0..3 x frame 4
+//   slice 3: kg 0..2 = slices 0..2's groups for ky = 4; kg 3: S0(py, px), S1(py, px)   (ky 0..4, kx 4) x frame 4
+// so that in slices 0..2 a lane's offsets are its row base + kg rows + a constant (ds_read immediates).
+// Row pitch 544 B: 8 extra LDS cycles over the 64 of a slice's conflict-free A reads (bank model of
+// MI355X_MICROARCH.md §LDS, ds_read_b64: two 32-lane groups, banks (a / 4) mod 64).  The loaders scatter frame 4
+// into R / S0 / S1 (ds_write_b16); S1's zero halves are written once.  Everything else is k_conv_v1s: three MFMA
+// groups per slice (Ah Bh, Ah Bl, Al Bh), compute waves run the epilogue, three window slots.
+constexpr int VP_PITCH = 544, VP_R = 160, VP_S0 = 288, VP_S1 = 416;
+constexpr int VP_IMG = HH * VP_PITCH;                          // one piece (h or l) of a window
+constexpr int VP_SLOT = 2 * VP_IMG;
+constexpr int VP_NSL = 4;                                      // K-slices
+constexpr int VP_WIMG = 2 * VP_NSL * 128 * 64;                 // Bh, Bl: 64 KB
+constexpr int LDS_P = VP_WIMG + NWS * VP_SLOT + SSH;
+static_assert(LDS_P <= 160 * 1024 && VP_SLOT % 16 == 0, "LDS (packed split v_conv1)");
+static_assert(VP_R >= HW * 8 && VP_S0 >= VP_R + TW * 8 && VP_S1 >= VP_S0 + TW * 8 && VP_PITCH >= VP_S1 + TW * 8, "row");
+
+template <int CW>
+__global__ __launch_bounds__(64 * (CW + 4), 1) void k_conv_v1p(HaloArgs a) {
+    static_assert(CW == 4 || CW == 8, "compute waves");
+    constexpr int NF = 5;
+    constexpr int NJ = 32 / CW;
+    extern __shared__ __attribute__((aligned(1024))) char lds[];
+    char* const wimg = lds;                          // [2 pieces][4 slices][128 co][64 B]
+    char* const halo = lds + VP_WIMG;                // [NWS][h image | l image]
+    float* const ssh = reinterpret_cast<float*>(halo + NWS * VP_SLOT);
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int w = wave < CW ? (wave & 3) : wave - CW;
+    const int cb0 = wave < CW ? (wave >> 2) * NJ : 0;
+
+    const int tiles_x = a.Wc / TW, tiles_per_clip = tiles_x * (a.Hc / TH);
+    const int ntiles = a.N * tiles_per_clip;
+    const int gxs = (int)gridDim.x;
+    const int slot = (gxs % 8 == 0) ? ((int)blockIdx.x % 8) * (gxs / 8) + (int)blockIdx.x / 8 : (int)blockIdx.x;
+    const int nmine = (ntiles - slot + gxs - 1) / gxs;
+    if (nmine <= 0) return;
+    auto tile_origin = [&](int k, int& clip, int& oy0, int& ox0) {
+        const int t = slot + k * gxs;
+        clip = t / tiles_per_clip;
+        const int tt = t - clip * tiles_per_clip;
+        oy0 = (tt / tiles_x) * TH;
+        ox0 = (tt % tiles_x) * TW;
+    };
+
+    if (wave >= CW) {
+        // =============================== loader waves ===============================
+        const int L = w * 64 + lane;
+        {
+            const __amdgpu_buffer_rsrc_t wrs = make_rsrc(a.w, (long long)VP_WIMG);
+#pragma unroll
+            for (int i = 0; i < VP_WIMG / 16 / 256; ++i) {
+                const int C = L + 256 * i, row = C >> 2, sl = C & 3;
+                const i32x4 v = __builtin_amdgcn_raw_buffer_load_b128(wrs, C * 16, 0, 0);
+                *reinterpret_cast<i32x4*>(wimg + row * 64 + ((sl ^ wsw(row & 127)) << 4)) = v;
+            }
+            if (L < 128) {
+                ssh[L] = a.scale[L];
+                ssh[128 + L] = a.shift[L];
+            }
+            // S1's three zero halves of every entry (never written by the window stores, which write its first half)
+            for (int i = L; i < NWS * 2 * TH * TW; i += 256) {
+                const int img = i / (TH * TW), e = i - img * (TH * TW);
+                char* p = halo + img * VP_IMG + (e / TW) * VP_PITCH + VP_S1 + (e % TW) * 8;
+                *reinterpret_cast<unsigned short*>(p + 2) = 0;
+                *reinterpret_cast<unsigned*>(p + 4) = 0u;
+            }
+        }
+        const long long clip_bytes = (long long)a.Hc * a.Wc * NF * 4;
+        const bool norm = a.vmean != nullptr;
+        const __amdgpu_buffer_rsrc_t mrs = make_rsrc(norm ? a.vmean : a.video, (long long)a.Hc * a.Wc * 4);
+        const __amdgpu_buffer_rsrc_t srs = make_rsrc(norm ? a.vstd : a.video, (long long)a.Hc * a.Wc * 4);
+        f32x4 v4[2][PPL];
+        float v1[2][PPL], pm[2][PPL], ps[2][PPL];
+        int pok[2][PPL];
+        auto win_load = [&](auto set, int k) {
+            constexpr int Q = decltype(set)::value;
+            int clip, oy0, ox0;
+            tile_origin(k, clip, oy0, ox0);
+            const __amdgpu_buffer_rsrc_t vrs =
+                make_rsrc(reinterpret_cast<const char*>(a.video) + (long long)clip * clip_bytes, clip_bytes);
+#pragma unroll
+            for (int e = 0; e < PPL; ++e) {
+                const int P = L + 256 * e;
+                const int wy = P / HW, wx = P - wy * HW;
+                const int iy = oy0 + wy - PAD, ix = ox0 + wx - PAD;
+                const int ok = (int)(P < HPIX) & (int)((unsigned)iy < (unsigned)a.Hc) & (int)((unsigned)ix < (unsigned)a.Wc);
+                const int pix = iy * a.Wc + ix;
+                const int voff = ok ? pix * NF * 4 : kOOB, moff = ok ? pix * 4 : kOOB;
+                v4[Q][e] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(vrs, voff, 0, 0));
+                v1[Q][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(vrs, voff, 16, 0));
+                pm[Q][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(mrs, moff, 0, 0));
+                ps[Q][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(srs, moff, 0, 0));
+                pok[Q][e] = ok;
+            }
+        };
+        bool in_bad = false;
+        auto win_store = [&](auto set, int hs) {
+            constexpr int Q = decltype(set)::value;
+#pragma unroll
+            for (int e = 0; e < PPL; ++e) {
+                const int P = L + 256 * e;
+                if (P >= HPIX) continue;
+                float f[5] = {v4[Q][e][0], v4[Q][e][1], v4[Q][e][2], v4[Q][e][3], v1[Q][e]};
+                _Float16 h[5], l[5];
+#pragma unroll
+                for (int i = 0; i < NF; ++i) {
+                    const float n = norm ? (f[i] - pm[Q][e]) / ps[Q][e] : f[i];
+                    f[i] = pok[Q][e] ? n : 0.f;
+                    h[i] = (_Float16)f[i];
+                    l[i] = (_Float16)(f[i] - (float)h[i]);
+                    in_bad |= pair_out_of_range(f[i]);
+                }
+                const int wy = P / HW, wx = P - wy * HW;
+#pragma unroll
+                for (int pc = 0; pc < 2; ++pc) {
+                    const _Float16* v = pc ? l : h;
+                    char* img = halo + hs * VP_SLOT + pc * VP_IMG;
+                    *reinterpret_cast<i32x2*>(img + wy * VP_PITCH + wx * 8) =
+                        (i32x2){(int)__builtin_bit_cast(unsigned, (f16x2){v[0], v[1]}),
+                                (int)__builtin_bit_cast(unsigned, (f16x2){v[2], v[3]})};
+                    const unsigned short q = __builtin_bit_cast(unsigned short, v[4]);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)   // R(wy, wx - j)[j]
+                        if (wx - j >= 0 && wx - j < TW)
+                            *reinterpret_cast<unsigned short*>(img + wy * VP_PITCH + VP_R + (wx - j) * 8 + 2 * j) = q;
+                    if (wx >= 4) {
+#pragma unroll
+                        for (int i = 0; i < 4; ++i)   // S0(wy - i, wx - 4)[i]
+                            if (wy - i >= 0 && wy - i < TH)
+                                *reinterpret_cast<unsigned short*>(img + (wy - i) * VP_PITCH + VP_S0 + (wx - 4) * 8 + 2 * i) = q;
+                        if (wy >= 4)   // S1(wy - 4, wx - 4)[0] (wy - 4 < 16 always)
+                            *reinterpret_cast<unsigned short*>(img + (wy - 4) * VP_PITCH + VP_S1 + (wx - 4) * 8) = q;
+                    }
+                }
+            }
+        };
+        using Q0 = std::integral_constant<int, 0>;
+        using Q1 = std::integral_constant<int, 1>;
+        win_load(Q0{}, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        win_store(Q0{}, 0);
+        if (nmine > 1) {
+            win_load(Q1{}, 1);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            win_store(Q1{}, 1);
+        }
+        if (nmine > 2) win_load(Q0{}, 2);
+        if (nmine > 3) win_load(Q1{}, 3);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        barrier_raw();   // B_-1: weights, BN tail, windows 0 and 1
+        auto iter = [&](auto set, int k) {
+            if (k + 2 < nmine) {
+                if constexpr (!(V1S_ABL & 2)) win_store(set, (k + 2) % NWS);
+                if (k + 4 < nmine) win_load(set, k + 4);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            barrier_raw();   // B_k: window k+2 stored; window k is no longer read
+        };
+        for (int k = 0; k < nmine; k += 2) {
+            iter(Q0{}, k);
+            if (k + 1 < nmine) iter(Q1{}, k + 1);
+        }
+        range_report(a.range_flag, a.range_in_bit, in_bad);
+        return;
+    }
+
+    // =============================== compute waves ===============================
+    __builtin_amdgcn_s_setprio(2);
+    const int r16 = lane & 15, kg = lane >> 4;
+    const int q = r16 >> 2, dy = (r16 >> 1) & 1, dx = r16 & 1;
+    const int py = 4 * w + 2 * (q >> 1) + dy, px = 2 * (q & 1) + dx;
+    const int bbase = r16 * 64 + ((kg ^ wsw(r16)) << 4) + 1024 * cb0;   // + piece * 32768 + slice * 8192 + 1024 j
+    // fragment (piece, slice s, column block i) of window slot hs: two 8-B reads at the lane's k-group offsets
+    const int pbk = (py + kg) * VP_PITCH + px * 8;   // slices 0..2: + the slice's constant
+    // slice 3: kg < 3 the ky = 4 groups of slices 0..2, kg = 3 S0 / S1
+    const int o30 = kg == 3 ? py * VP_PITCH + px * 8 + VP_S0 : (py + 4) * VP_PITCH + px * 8 + 16 * kg;
+    const int o31 = kg == 3 ? o30 + (VP_S1 - VP_S0) : kg == 2 ? o30 + (VP_R - 32) : o30 + 8;
+    // The lane's base address is rebuilt per fragment set from the slot (an SGPR) and pinned, so that the compiler
+    // addresses the pieces by immediates instead of holding one precomputed address per (slot, piece, slice, i) in
+    // VGPRs (16 spills); contiguous piece pairs merge into ds_read2_b64 (8 cycles per 16 B, like v1s's two
+    // ds_read2_b32; conflict-free at the 544-B pitch: 16 lanes at 32 r + 8 c mod 128 B)
+    auto fragA = [&](int hs, int piece, int s, i32x4 (&fa)[4]) {
+        const int sb = hs * VP_SLOT + piece * VP_IMG;
+        if (s < 3) {
+            int b0 = sb + pbk;
+            asm volatile("" : "+v"(b0));
+            const char* hp = halo + b0 + 16 * s;
+            constexpr int D[3] = {8, 8, VP_R - 32};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const i32x2 x0 = *reinterpret_cast<const i32x2*>(hp + 32 * i);
+                const i32x2 x1 = *reinterpret_cast<const i32x2*>(hp + D[s < 3 ? s : 0] + 32 * i);
+                fa[i] = (i32x4){x0[0], x0[1], x1[0], x1[1]};
+            }
+        } else {
+            int b0 = sb + o30, b1 = sb + o31;
+            asm volatile("" : "+v"(b0), "+v"(b1));
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const i32x2 x0 = *reinterpret_cast<const i32x2*>(halo + b0 + 32 * i);
+                const i32x2 x1 = *reinterpret_cast<const i32x2*>(halo + b1 + 32 * i);
+                fa[i] = (i32x4){x0[0], x0[1], x1[0], x1[1]};
+            }
+        }
+    };
+    auto fragB = [&](int piece, int s, i32x4 (&fb)[NJ]) {
+        const char* wp = wimg + piece * (VP_NSL * 8192) + s * 8192 + bbase;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) fb[j] = *reinterpret_cast<const i32x4*>(wp + 1024 * j);
+    };
+    barrier_raw();   // B_-1
+
+    f32x4 acc[4][NJ];
+    auto mfmas = [&](const i32x4 (&ca)[4], const i32x4 (&cb)[NJ], bool first) {
+        if constexpr ((V1S_ABL & 4) != 0) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc[i][0][0] += __builtin_bit_cast(float, ca[i][0] ^ cb[i][1]);
+            return;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, ca[i]),
+                                                                    __builtin_bit_cast(f16x8, cb[j]),
+                                                                    first ? (f32x4){0.f, 0.f, 0.f, 0.f} : acc[i][j], 0, 0, 0);
+    };
+    auto sched = [](auto nds) {
+        constexpr int ND = decltype(nds)::value, NM = 4 * NJ, P = ND < NM ? ND : NM;
+#pragma unroll
+        for (int r = 0; r < P; ++r) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
+        }
+        if constexpr (NM > P) __builtin_amdgcn_sched_group_barrier(0x008, NM - P, 0);
+        if constexpr (ND > P) __builtin_amdgcn_sched_group_barrier(0x100, ND - P, 0);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    // slice s of window slot hs, (ah, bh) its Ah / Bh fragments; reads the next slice's (hsn, sn) Ah / Bh
+    auto slice = [&](int hs, int s, int hsn, int sn, i32x4 (&ah)[4], i32x4 (&bh)[NJ], i32x4 (&nah)[4],
+                     i32x4 (&nbh)[NJ], bool first) {
+        i32x4 bl[NJ], al[4];
+        fragB(1, s, bl);
+        mfmas(ah, bh, first);
+        sched(std::integral_constant<int, NJ>{});
+        fragA(hs, 1, s, al);
+        mfmas(ah, bl, false);
+        sched(std::integral_constant<int, 8>{});
+        fragA(hsn, 0, sn, nah);
+        fragB(0, sn, nbh);
+        mfmas(al, bh, false);
+        sched(std::integral_constant<int, 8 + NJ>{});
+    };
+    const int Wp = a.Wc / 2;
+    const long long cbytes = a.out_clip_stride * 2;
+    bool bad = false;
+    auto epilogue = [&](int k) {
+        int clip, oy0, ox0;
+        tile_origin(k, clip, oy0, ox0);
+        const __amdgpu_buffer_rsrc_t ors = make_rsrc(reinterpret_cast<const char*>(a.out) + (long long)clip * cbytes, cbytes);
+        const int opy = (oy0 >> 1) + 2 * w + (kg >> 1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int opx = (ox0 >> 1) + 2 * i + (kg & 1);
+            const int pbase = (opy * Wp + opx) * a.out_pix_stride + a.out_c_off + 32 * cb0 + r16;
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const float mx = fmaxf(fmaxf(acc[i][j][0], acc[i][j][1]), fmaxf(acc[i][j][2], acc[i][j][3]));
+                const int co = 16 * (cb0 + j) + r16;
+                float x = fmaf(mx, ssh[co], ssh[128 + co]);
+                x = fmaxf(x, LRELU * x);
+                const _Float16 h = (_Float16)x;
+                const _Float16 l = (_Float16)(x - (float)h);
+                bad |= pair_out_of_range(x);
+                if constexpr (V1S_ABL & 1) {
+                    if (x == 12345.f) __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, h), ors, 0, 0, 0);
+                    continue;
+                }
+                // (measured: dword channel pairs, the partner's pieces by DPP, 0.693 vs 0.663 ms, r06o)
+                __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, h), ors, (pbase + 32 * j) * 2, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, l), ors, (pbase + 32 * j + 16) * 2, 0, 0);
+            }
+        }
+    };
+    i32x4 fa[4], fb[NJ], na[4], nb[NJ];
+    auto tile = [&](int k, i32x4 (&xa)[4], i32x4 (&xb)[NJ], i32x4 (&ya)[4], i32x4 (&yb)[NJ]) {
+        const int hs = k % NWS, hn = (k + 1) % NWS;
+        slice(hs, 0, hs, 1, xa, xb, ya, yb, true);
+        slice(hs, 1, hs, 2, ya, yb, xa, xb, false);
+        slice(hs, 2, hs, 3, xa, xb, ya, yb, false);
+        // slice 3 reads tile k+1's first fragments (past the last tile a stale slot, never used)
+        slice(hs, 3, hn, 0, ya, yb, xa, xb, false);
+        epilogue(k);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        barrier_raw();   // B_k: window k is no longer read
+    };
+    fragA(0, 0, 0, fa);
+    fragB(0, 0, fb);
+    for (int k = 0; k < nmine; ++k) tile(k, fa, fb, na, nb);
+    range_report(a.range_flag, a.range_bit, bad);
+}
+
 }  // namespace
 
 #ifndef AVSE_V1S_CW
 #define AVSE_V1S_CW 8
 #endif
 int launch_conv_v1r(const HaloArgs& a, hipStream_t s) {
+    if (a.variant == HALO_V1P) {
+        constexpr int CW = AVSE_V1S_CW;
+        if (int rc = ensure_lds_attr((const void*)k_conv_v1p<CW>, LDS_P)) return rc;
+        if (!a.split || a.Hc % TH || a.Wc % TW || a.Co != 128 || a.Ci != 5 || !a.w || a.out_mode != OUT_S16) {
+            set_error("v_conv1 packed split kernel: unexpected layer shape, packing or output format");
+            return 3;
+        }
+        int dev = 0, ncu = 256;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+        const int tiles = a.N * (a.Hc / TH) * (a.Wc / TW);
+        int gx = ncu >= 8 ? ncu / 8 * 8 : ncu;
+        if (gx > tiles) gx = tiles;
+        hipLaunchKernelGGL((k_conv_v1p<CW>), dim3(gx), dim3(64 * (CW + 4)), LDS_P, s, a);
+        AVSE_HIP_CHECK(hipGetLastError());
+        return 0;
+    }
     if (a.split) {
         constexpr int CW = AVSE_V1S_CW;
         const void* kf = a.Ci == 6 ? (const void*)k_conv_v1s<CW, 6> : (const void*)k_conv_v1s<CW, 5>;

@@ -243,3 +243,37 @@ def test_split_fused_tail_matches_layer_path(gpu, N):
     # the seam: output rows 38..41 come from d_deconv4 rows 19 / 20, computed by both halves
     seam = rel_rms(fused[:, 36:44], layer[:, 36:44])
     assert seam <= 1e-6, seam
+
+
+@pytest.mark.parametrize("N", [1, 37, 512])
+def test_split_packed_v1_matches_v1s_and_oracle(gpu, N):
+    """k_conv_v1p (5-frame v_conv1 with K = 128: frames 0..3 as 8-byte pixels, frame 4 scattered into row / column
+    runs; conv_v1r.hip) against k_conv_v1s (K = 160 of 12-byte pixels, option no_v1p at weight load) and the float64
+    oracle: the same products grouped into other 32-product MFMA sums, so the two agree within fp32 rounding; every
+    tile of the 128 x 128 frames (the zero-padded borders included), one clip .. the bench batch."""
+    from avse_amd import _lib, ops
+    from avse_amd.model import KerasModel
+    model = db_scale(KerasModel.init(seed=51, randomize=True))
+    mel, video = make_inputs(N, 151)
+    mean = video.mean(axis=(0, 3)).astype(np.float32)
+    std = (video.std(axis=(0, 3)) + 0.1).astype(np.float32)
+    names = ["v_conv1", "v_conv2"]
+    dw = ops.DeviceWeights(model, SPLIT)
+    with _lib.context().options(no_v1p=1):
+        dw_s = ops.DeviceWeights(model, SPLIT)
+    args = (ops.to_device(mel), ops.to_device(video), ops.to_device(mean), ops.to_device(std))
+    clips = spread_clips(N, k=4)
+    got = ops.forward(dw, *args, checked=True).cpu().numpy()
+    assert dw.last_range_bits == 0
+    sc = scratch(dw, N, clips, names)
+    got_s = ops.forward(dw_s, *args).cpu().numpy()
+    sc_s = scratch(dw_s, N, clips, names)
+    inter = {}
+    vn = R.video_normalize(video[clips], mean, std).astype(np.float32)
+    ref = K.forward(model.layer_dict(), mel[clips], vn, intermediates=inter)
+    for k in names:
+        print(f"{k}: packed vs oracle {rel_rms(sc[k], inter[k]):.2e}, vs v1s {rel_rms(sc[k], sc_s[k]):.2e}")
+        assert rel_rms(sc[k], inter[k]) <= FP32_REL and rel_rms(sc[k], sc_s[k]) <= 1e-6, k
+    ae = abs_rms(got[clips], ref)
+    print(f"N={N}: output abs RMS {ae:.3e}, packed vs v1s rel {rel_rms(got, got_s):.2e}")
+    assert np.isfinite(got).all() and ae <= FP32_ABS and rel_rms(got, got_s) <= 1e-6
