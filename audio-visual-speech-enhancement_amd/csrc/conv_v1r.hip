@@ -933,6 +933,13 @@ __global__ __launch_bounds__(64 * (CW + 4), 1) void k_conv_v1p(HaloArgs a) {
         }
     };
     i32x4 fa[4], fb[NJ], na[4], nb[NJ];
+    // The two compute waves of a SIMD (w, w + 4) take turns on the matrix pipe: wave w runs tile k's epilogue after its
+    // MFMAs, wave w + 4 before tile k + 1's (past the barrier: the epilogue reads no window), so between two barriers
+    // one wave's BN / split / stores overlap the other's MFMAs instead of both idling the pipe at once
+#ifndef AVSE_V1P_STAGGER
+#define AVSE_V1P_STAGGER 1
+#endif
+    const bool late = AVSE_V1P_STAGGER && CW == 8 && wave >= 4;
     auto tile = [&](int k, i32x4 (&xa)[4], i32x4 (&xb)[NJ], i32x4 (&ya)[4], i32x4 (&yb)[NJ]) {
         const int hs = k % NWS, hn = (k + 1) % NWS;
         slice(hs, 0, hs, 1, xa, xb, ya, yb, true);
@@ -940,13 +947,17 @@ __global__ __launch_bounds__(64 * (CW + 4), 1) void k_conv_v1p(HaloArgs a) {
         slice(hs, 2, hs, 3, xa, xb, ya, yb, false);
         // slice 3 reads tile k+1's first fragments (past the last tile a stale slot, never used)
         slice(hs, 3, hn, 0, ya, yb, xa, xb, false);
-        epilogue(k);
+        if (!late) epilogue(k);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         barrier_raw();   // B_k: window k is no longer read
     };
     fragA(0, 0, 0, fa);
     fragB(0, 0, fb);
-    for (int k = 0; k < nmine; ++k) tile(k, fa, fb, na, nb);
+    for (int k = 0; k < nmine; ++k) {
+        if (late && k > 0) epilogue(k - 1);
+        tile(k, fa, fb, na, nb);
+    }
+    if (late) epilogue(nmine - 1);
     range_report(a.range_flag, a.range_bit, bad);
 }
 
