@@ -22,7 +22,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # kernel-name prefix -> labels in launch order within one forward
 LABELS = [("k_spec_seg", ["stft"]), ("k_spec640", ["stft"]), ("k_spec_dft", ["stft"]), ("k_aud_enc", ["audio_enc"]),
-          ("k_conv_v1r", ["v_conv1"]), ("k_conv_v1s", ["v_conv1"]), ("k_splitk_reduce", ["splitk_reduce"]),
+          ("k_conv_v1r", ["v_conv1"]), ("k_conv_v1s", ["v_conv1"]), ("k_conv_v1p", ["v_conv1"]),
+          ("k_splitk_reduce", ["splitk_reduce"]),
           ("k_conv_stream<5,", ["v_conv2"]), ("k_conv_stream<3, 16, 16", ["v_conv3", "v_conv4"]),
           ("k_conv_stream<3, 8, 8", ["v_conv5"]), ("k_gemm<1>", ["v_conv6"]),
           ("k_gemm<0>", ["enc_dense", "dec_dense1", "dec_dense2"]), ("k_dec_head", ["dec_head"]),
