@@ -325,8 +325,14 @@ struct GemmArgs {
     int ksplit;              // split-K over blockIdx.z, reduced by the last workgroup of each tile
     float* partial;          // [tiles][ksplit][128 x 128] fp32
     int* counters;           // [tiles], zero between launches
+    int split;               // 1 = AVSE_F32_SPLIT (k_gemm S16): a / out in the split-pair layout (lda, ldo, out_off in
+                             // halves), w packed [Wh(16) | Wl(16)] per 16 k, kpad in k
+    int slabs_per_split;     // split: slabs per split (whole kFp32Block blocks; 0 = one split)
+    unsigned* range_flag;    // split: range guard of the stored pairs
+    unsigned range_bit;
 };
 int gemm_ksplit(int M, int N, int kpad, int cap);   // cap > 0 limits the split (Options::gemm_ksplit_cap)
+int gemm_s16_ksplit(int N, int kpad, int* slabs_per_split);   // split dense layers: plan from K and N only
 size_t gemm_ws_bytes(int M, int N, int kpad, int cap);
 int launch_gemm(const GemmArgs& g, int mode, hipStream_t s);
 int launch_aud_enc(const AudEncArgs& a, hipStream_t s);

@@ -310,6 +310,10 @@ size_t split_ws_bytes(int64_t N, int dtype, const Options& o, const NetPlan& p) 
         const size_t mp = (size_t)((x.M + 127) / 128) * 128, np = (size_t)((x.Co + bn - 1) / bn) * bn;
         if (ks > 1) mx = std::max(mx, (size_t)ks * mp * np * 4);
         if (dtype == AVSE_BF16) mx = std::max(mx, gemm_ws_bytes((int)x.M, x.Co, x.kpad, o.gemm_ksplit_cap));   // gemm.hip's split-K
+        if (dtype == AVSE_F32_SPLIT && &x != &g[3]) {   // gemm.hip's split dense plan (v_conv6 takes k_conv's, above)
+            const int gks = gemm_s16_ksplit(x.Co, x.kpad, nullptr);
+            if (gks > 1) mx = std::max(mx, (size_t)((x.M + 127) / 128) * ((x.Co + 127) / 128) * gks * 128 * 128 * 4);
+        }
     }
     return mx;
 }
@@ -1364,14 +1368,15 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
     const long long CAT = P.cat, AEMB = P.aemb, EMB = P.emb;
     const Options& opt = c->opt;
     auto buf = [&](int b) { return (void*)(c->arena + off[b]); };
-    // dense layers and v_conv6 on gemm.hip (bf16; Options::no_gemm keeps k_conv + split-K reduce)
-    const bool use_gemm = dt == AVSE_BF16 && !opt.no_gemm;
+    // dense layers and v_conv6 on gemm.hip (bf16, and split pairs: k_gemm S16; Options::no_gemm keeps k_conv + split-K
+    // reduce)
+    const bool use_gemm = (dt == AVSE_BF16 || split) && !opt.no_gemm;
     auto gemm = [&](const GpuLayer& G, const void* in, long long lda, void* outp, long long ldo, int out_off, int mode,
-                    int64_t n) {
+                    int64_t n, size_t part_off, int li) {
         GemmArgs g;
         std::memset(&g, 0, sizeof(g));
         g.a = reinterpret_cast<const bf16_t*>(in);
-        g.lda = lda;
+        g.lda = split ? 2 * lda : lda;
         g.w = reinterpret_cast<const bf16_t*>(G.w);
         g.M = (int)(mode == 1 ? n * 16 : n);
         g.N = G.def.cout;
@@ -1380,10 +1385,23 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
         g.shift = G.shift;
         g.act = 1;
         g.out = reinterpret_cast<bf16_t*>(outp);
-        g.ldo = ldo;
-        g.out_off = out_off;
-        g.ksplit = gemm_ksplit(g.M, g.N, g.kpad, opt.gemm_ksplit_cap);
-        g.partial = reinterpret_cast<float*>(c->arena + off[B_COUNT]);
+        g.ldo = split ? 2 * ldo : ldo;
+        g.out_off = split ? 2 * out_off : out_off;
+        if (split) {
+            // the k_conv path's plans: v_conv6 one block per split (or none), the dense layers from K and N only
+            g.split = 1;
+            if (mode == 1) {
+                g.ksplit = choose_ksplit(g.M, g.N, g.kpad, dt);
+                g.slabs_per_split = g.ksplit > 1 ? kFp32Block : 0;
+            } else {
+                g.ksplit = gemm_s16_ksplit(g.N, g.kpad, &g.slabs_per_split);
+            }
+            g.range_flag = rflag;
+            g.range_bit = 1u << li;
+        } else {
+            g.ksplit = gemm_ksplit(g.M, g.N, g.kpad, opt.gemm_ksplit_cap);
+        }
+        g.partial = reinterpret_cast<float*>(c->arena + part_off);
         g.counters = c->gemm_counters;
         return launch_gemm(g, mode, s);
     };
@@ -1437,7 +1455,7 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
             const long long in_cs = (long long)G.def.hin * G.def.win * (i == 0 ? G.cin_pad : G.def.cin);
             if (i == 5 && use_gemm && G.def.hin == 4 && G.def.win == 4 && G.def.cin == 512 && G.def.kh == 3 && G.def.pool &&
                 G.ph[0].kpad == 9 * 512) {
-                if ((rc = gemm(G, vb(v_in[i]), in_cs, cat, CAT, AEMB, 1, n)) || (rc = mark())) return rc;   // concat[aemb:]
+                if ((rc = gemm(G, vb(v_in[i]), in_cs, cat, CAT, AEMB, 1, n, o[B_COUNT], 10)) || (rc = mark())) return rc;   // concat[aemb:]
                 continue;
             }
             ConvArgs a = (i < 5) ? conv_args(G, vb(v_in[i]), in_cs, vb(v_in[i + 1]), (long long)G.ho * G.wo * G.def.cout, G.def.cout, 0, n)
@@ -1567,9 +1585,9 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
     if (concurrent) AVSE_HIP_CHECK(hipStreamWaitEvent(s, c->join, 0));
     // fusion + decoder dense (network.py:53-58, :66-78)
     if (use_gemm) {
-        if ((rc = gemm(L(11), buf(B_CAT), CAT, buf(B_E1), EMB, 0, 0, N)) || (rc = mark())) return rc;
-        if ((rc = gemm(L(12), buf(B_E1), EMB, buf(B_E2), EMB, 0, 0, N)) || (rc = mark())) return rc;
-        if ((rc = gemm(L(13), buf(B_E2), EMB, buf(B_E3), AEMB, 0, 0, N)) || (rc = mark())) return rc;
+        if ((rc = gemm(L(11), buf(B_CAT), CAT, buf(B_E1), EMB, 0, 0, N, off[B_COUNT], 11)) || (rc = mark())) return rc;
+        if ((rc = gemm(L(12), buf(B_E1), EMB, buf(B_E2), EMB, 0, 0, N, off[B_COUNT], 12)) || (rc = mark())) return rc;
+        if ((rc = gemm(L(13), buf(B_E2), EMB, buf(B_E3), AEMB, 0, 0, N, off[B_COUNT], 13)) || (rc = mark())) return rc;
     } else {
         ConvArgs a = conv_args(L(11), buf(B_CAT), CAT, buf(B_E1), EMB, EMB, 0, N);
         ksplit(a, off[B_COUNT]);

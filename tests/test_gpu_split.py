@@ -277,3 +277,32 @@ def test_split_packed_v1_matches_v1s_and_oracle(gpu, N):
     ae = abs_rms(got[clips], ref)
     print(f"N={N}: output abs RMS {ae:.3e}, packed vs v1s rel {rel_rms(got, got_s):.2e}")
     assert np.isfinite(got).all() and ae <= FP32_ABS and rel_rms(got, got_s) <= 1e-6
+
+
+@pytest.mark.parametrize("N", [1, 37, 512])
+def test_split_gemm_matches_kconv_and_oracle(gpu, N):
+    """gemm.hip's split-pair k_gemm (v_conv6 as an implicit GEMM with the 2x2 pool, enc_dense / dec_dense1 / dec_dense2
+    with split-K over whole fp32 summation blocks) against the same layers on k_conv + split-K reduce (option no_gemm)
+    and the float64 oracle, layer by layer: the same products in other MFMA groupings, so the two agree within fp32
+    rounding; N = 1 takes v_conv6's 36-way split, N = 512 none."""
+    from avse_amd import _lib, ops
+    from avse_amd.model import KerasModel
+    model = db_scale(KerasModel.init(seed=61, randomize=True))
+    mel, video = make_inputs(N, 161)
+    names = ["concat", "enc_dense", "dec_dense1", "dec_dense2", "d_deconv1"]
+    clips = spread_clips(N, k=6)
+    dw = ops.DeviceWeights(model, SPLIT)
+    got = ops.forward(dw, ops.to_device(mel), ops.to_device(video), checked=True).cpu().numpy()
+    assert dw.last_range_bits == 0
+    sc = scratch(dw, N, clips, names)
+    with _lib.context().options(no_gemm=1):
+        got_k = ops.forward(dw, ops.to_device(mel), ops.to_device(video)).cpu().numpy()
+        sck = scratch(dw, N, clips, names)
+    inter = {}
+    ref = K.forward(model.layer_dict(), mel[clips], video[clips], intermediates=inter)
+    for k in names:
+        print(f"{k}: k_gemm vs oracle {rel_rms(sc[k], inter[k]):.2e}, vs k_conv {rel_rms(sc[k], sck[k]):.2e}")
+        assert rel_rms(sc[k], inter[k]) <= FP32_REL and rel_rms(sc[k], sck[k]) <= 1e-6, k
+    ae = abs_rms(got[clips], ref)
+    print(f"N={N}: output abs RMS {ae:.3e}, k_gemm vs k_conv rel {rel_rms(got, got_k):.2e}")
+    assert np.isfinite(got).all() and ae <= FP32_ABS and rel_rms(got, got_k) <= 1e-6
