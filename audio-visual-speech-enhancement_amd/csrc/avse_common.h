@@ -42,6 +42,7 @@ struct Options {
     int no_act_scale = 0;     // AVSE_NO_ACT_SCALE: split weights loaded without per-layer activation exponents
     int no_win = 0;           // AVSE_NO_WIN: split stride-1 gather layers on k_conv, not the windowed conv_win.hip
     int no_v1p = 0;           // AVSE_NO_V1P: split 5-frame v_conv1 on k_conv_v1s (K 160), not k_conv_v1p (K 128; read at load)
+    int no_a1valu = 0;        // AVSE_NO_A1VALU: split a_conv1 on k_conv after audio_prep, not k_aconv1_split
     int side_prio = 0;        // AVSE_SIDE_PRIO: audio side stream priority (0 default, 1 least, 2 greatest; read when created)
 };
 
@@ -372,6 +373,10 @@ int launch_conv_v1r(const HaloArgs& a, hipStream_t s);      // conv_v1r.hip (v_c
 int launch_video_prep(const float* video, const float* mean, const float* stdv, void* out, int64_t N,
                       int F, int dtype, hipStream_t s);
 int launch_audio_prep(const float* audio, void* out, int64_t npix, int dtype, hipStream_t s);
+// split dtype a_conv1 (one input channel) on the vector ALUs straight from the audio input (conv.hip k_aconv1_split)
+int launch_aconv1_split(const float* in, const float* w, const float* scale, const float* shift, void* out, int64_t N,
+                        int H, int W, int Ho, int Wo, int KH, int KW, int S, int pt, int pl, int Co, unsigned* range_flag,
+                        unsigned range_bit, unsigned range_in_bit, hipStream_t s);
 int launch_out_conv(const void* in, const float* w64, float bias, float* out, int64_t npix, int dtype,
                     hipStream_t s);
 int launch_broadcast_row(const void* src, void* dst, int64_t rows, int64_t row_bytes, int64_t stride_bytes,

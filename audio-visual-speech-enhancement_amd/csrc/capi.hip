@@ -174,6 +174,7 @@ struct GpuLayer {
     int halo = HALO_NONE;     // halo-tiled kernel variant (bf16 video convs)
     void* w_halo = nullptr;   // bf16 packing for conv_stream.hip / conv_v1r.hip (see build_layer)
     void* w_dense = nullptr;  // a_conv1 only (bf16): [Cout][32], k = ky * kw + kx, for conv_aud.hip
+    float* w_f32 = nullptr;   // a_conv1 only (split): [kh * kw][Cout] f32 x 2^e_n, for conv.hip k_aconv1_split
     float* scale_h = nullptr; // |scale| for w_halo: channels with a negative BN scale have negated weights
     int2 htaps[MAX_TAPS * MAX_PHASES] = {};   // host copy of taps (conv_dec.hip's kernel arguments)
 };
@@ -199,6 +200,7 @@ const OptionName kOptionNames[] = {
     {"no_act_scale", "AVSE_NO_ACT_SCALE", &Options::no_act_scale},
     {"no_win", "AVSE_NO_WIN", &Options::no_win},
     {"no_v1p", "AVSE_NO_V1P", &Options::no_v1p},
+    {"no_a1valu", "AVSE_NO_A1VALU", &Options::no_a1valu},
     {"side_prio", "AVSE_SIDE_PRIO", &Options::side_prio},
 };
 
@@ -718,6 +720,12 @@ int build_layer(avse_weights* W, int li, const float* kernel, const float* bias,
             if (mx > 0.f) (void)std::frexp(mx, &e2);
             ex[n] = mx > 0.f ? 15 - e2 : 0;
             scale_g[n] = std::ldexp(scale[n], -ex[n]);
+        }
+        if (L.kind == CONV && L.cin == 1) {   // a_conv1: f32 taps with the same per-channel power of two
+            std::vector<float> wf((size_t)L.kh * L.kw * L.cout);
+            for (int t = 0; t < L.kh * L.kw; ++t)
+                for (int n = 0; n < L.cout; ++n) wf[(size_t)t * L.cout + n] = std::ldexp(kernel[(size_t)t * L.cout + n], ex[n]);
+            if ((rc = upload(W, wf, &G.w_f32))) return rc;
         }
         std::vector<uint16_t> sp(2 * packed.size(), 0);
         for (int p = 0; p < G.nphase; ++p)
@@ -1560,9 +1568,22 @@ int forward_impl(avse_ctx* c, const avse_weights* W, const float* audio, const f
         for (int k = 0; k < 6; ++k)
             if ((rc = mark())) return rc;   // audio_prep (= the fused kernel), a_conv1..a_conv5
     }
-    if (!aud_fused && ((rc = launch_audio_prep(audio, buf(B_AIN), N * kMels * P.T, gdt, sa)) || (rc = mark()))) return rc;
+    // split: a_conv1 on the vector ALUs from the audio input itself (conv.hip k_aconv1_split; no audio_prep copy)
+    const bool a1_valu = split && !aud_fused && !opt.no_a1valu && L(0).w_f32 && L(0).def.cin == 1 && L(0).def.kind == CONV &&
+                         L(0).def.cout == 64 && L(0).def.kh == 5 && L(0).def.kw == 5 && L(0).def.sh == L(0).def.sw;
+    if (a1_valu) {
+        const GpuLayer& G = L(0);
+        const int pt = std::max((G.ho - 1) * G.def.sh + G.def.kh - G.def.hin, 0) / 2;
+        const int pl = std::max((G.wo - 1) * G.def.sw + G.def.kw - G.def.win, 0) / 2;
+        if ((rc = mark()) ||
+            (rc = launch_aconv1_split(audio, G.w_f32, G.scale, G.shift, buf(B_A1), N, G.def.hin, G.def.win, G.ho, G.wo,
+                                      G.def.kh, G.def.kw, G.def.sh, pt, pl, G.def.cout, rflag, 1u, kRangeAudioIn, sa)) ||
+            (rc = mark()))
+            return rc;
+    }
+    if (!aud_fused && !a1_valu && ((rc = launch_audio_prep(audio, buf(B_AIN), N * kMels * P.T, gdt, sa)) || (rc = mark()))) return rc;
     const int a_in[5] = {B_AIN, B_A1, B_A2, B_A3, B_A4};
-    for (int i = 0; i < 5 && !aud_fused; ++i) {
+    for (int i = a1_valu ? 1 : 0; i < 5 && !aud_fused; ++i) {
         const GpuLayer& G = L(i);
         const long long in_cs = (long long)G.def.hin * G.def.win * (i == 0 ? G.cin_pad : G.def.cin);
         ConvArgs a = (i < 4) ? conv_args(G, buf(a_in[i]), in_cs, buf(a_in[i + 1]), (long long)G.ho * G.wo * G.def.cout, G.def.cout, 0, N)

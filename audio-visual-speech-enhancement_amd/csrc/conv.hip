@@ -593,6 +593,99 @@ __global__ void k_audio_prep(const float* __restrict__ a, T* __restrict__ out, l
     }
 }
 
+// a_conv1 in the split dtype (network.py:89-91: Conv2D(64, 5x5, strides 2, 'same') on the one-channel mel image ->
+// BatchNorm -> LeakyReLU), straight from the network input audio [N][H][W] f32 (no audio_prep copy): fp32 FMAs on the
+// vector ALUs — the generic split k_conv spent 0.065 ms on its 2-slab K (K = 25) plus 0.012 ms of audio_prep; this
+// kernel 0.040 ms.  A thread owns one output pixel and all 64 channels: the taps run in (ky, kx) order with fmaf (the
+// loop not unrolled: unrolled, the compiler hoisted every weight read and the epilogue's loads over the FMAs — 256
+// VGPRs and scratch; with the weights through scalar loads, 1,492 SGPR spills), each tap's input loaded three taps
+// ahead, weights [tap][64] x 2^e_n and the folded BN scale x 2^-e_n / shift from LDS (exact), then LeakyReLU and the
+// split pairs [h(16) | l(16)] x 4 as 16-B stores.  (Measured: 16 channels per thread, four waves per pixel block,
+// 0.042 ms; eight lanes per pixel with lane-adjacent 16-B stores, 0.045 ms.)  The range guard reports input values
+// past the pair range as before (range_in_bit: the recompute contract of include/avse.h) and stored pairs out of range.
+struct AConv1Args {
+    const float* in;          // [N][H][W]
+    const float* w;           // [KH * KW][Co], x 2^e_n per output channel
+    const float* scale;
+    const float* shift;
+    unsigned short* out;      // split pairs [N][Ho][Wo][Co / 16][h(16) | l(16)]
+    long long N;
+    int H, W, Ho, Wo, KH, KW, S, pt, pl;
+    unsigned* range_flag;
+    unsigned range_bit, range_in_bit;
+};
+constexpr int A1_CO = 64, A1_K = 5;
+__global__ __launch_bounds__(256) void k_aconv1_split(AConv1Args a) {
+    __shared__ __attribute__((aligned(16))) float ws[A1_K * A1_K * A1_CO];
+    __shared__ __attribute__((aligned(16))) float ssc[A1_CO], ssh[A1_CO];
+    for (int i = threadIdx.x; i < A1_K * A1_K * A1_CO / 4; i += 256)
+        reinterpret_cast<float4*>(ws)[i] = reinterpret_cast<const float4*>(a.w)[i];
+    if (threadIdx.x < A1_CO) {
+        ssc[threadIdx.x] = a.scale[threadIdx.x];
+        ssh[threadIdx.x] = a.shift[threadIdx.x];
+    }
+    __syncthreads();
+    const int HW = a.Ho * a.Wo;
+    const long long npix = a.N * HW;
+    const long long p = (long long)blockIdx.x * 256 + threadIdx.x;
+    bool bad = false, in_bad = false;
+    if (p < npix) {
+        const int clip = (int)(p / HW);   // (N x Ho x Wo < 2^31 checked at launch)
+        const int r = (int)p - clip * HW, oy = r / a.Wo, ox = r - oy * a.Wo;
+        const float* img = a.in + (long long)clip * a.H * a.W;
+        auto tap_in = [&](int t) {
+            const int ky = t / A1_K, kx = t - A1_K * (t / A1_K);
+            const int iy = oy * a.S + ky - a.pt, ix = ox * a.S + kx - a.pl;
+            const bool ok = t < A1_K * A1_K && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+            return ok ? img[iy * a.W + ix] : 0.f;
+        };
+        float acc[A1_CO];
+#pragma unroll
+        for (int c = 0; c < A1_CO; ++c) acc[c] = 0.f;
+        float v0 = tap_in(0), v1 = tap_in(1), v2 = tap_in(2);
+#pragma unroll 1
+        for (int t = 0; t < A1_K * A1_K; ++t) {
+            const float v = v0;
+            v0 = v1;
+            v1 = v2;
+            v2 = tap_in(t + 3);
+            in_bad |= pair_out_of_range(v);
+#pragma unroll
+            for (int c = 0; c < A1_CO; c += 4) {
+                const float4 w4 = *reinterpret_cast<const float4*>(ws + t * A1_CO + c);
+                acc[c] = fmaf(v, w4.x, acc[c]);
+                acc[c + 1] = fmaf(v, w4.y, acc[c + 1]);
+                acc[c + 2] = fmaf(v, w4.z, acc[c + 2]);
+                acc[c + 3] = fmaf(v, w4.w, acc[c + 3]);
+            }
+        }
+        uint4* o = reinterpret_cast<uint4*>(a.out + p * A1_CO * 2);
+#pragma unroll
+        for (int g = 0; g < A1_CO / 16; ++g) {
+            unsigned hw[8], lw[8];
+#pragma unroll
+            for (int c = 0; c < 16; c += 2) {
+                const int n = 16 * g + c;
+                float y0 = fmaf(acc[n], ssc[n], ssh[n]);
+                float y1 = fmaf(acc[n + 1], ssc[n + 1], ssh[n + 1]);
+                y0 = y0 >= 0.f ? y0 : 0.3f * y0;
+                y1 = y1 >= 0.f ? y1 : 0.3f * y1;
+                bad = bad || pair_out_of_range(y0) || pair_out_of_range(y1);
+                const _Float16 h0 = (_Float16)y0, h1 = (_Float16)y1;
+                const _Float16 l0 = (_Float16)(y0 - (float)h0), l1 = (_Float16)(y1 - (float)h1);
+                hw[c / 2] = (unsigned)__builtin_bit_cast(unsigned short, h0) | ((unsigned)__builtin_bit_cast(unsigned short, h1) << 16);
+                lw[c / 2] = (unsigned)__builtin_bit_cast(unsigned short, l0) | ((unsigned)__builtin_bit_cast(unsigned short, l1) << 16);
+            }
+            o[4 * g + 0] = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+            o[4 * g + 1] = make_uint4(hw[4], hw[5], hw[6], hw[7]);
+            o[4 * g + 2] = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+            o[4 * g + 3] = make_uint4(lw[4], lw[5], lw[6], lw[7]);
+        }
+    }
+    range_report(a.range_flag, a.range_bit, bad);
+    range_report(a.range_flag, a.range_in_bit, in_bad);
+}
+
 // d_deconv6 (network.py:133): 1x1 Conv2DTranspose 64 -> 1 + bias, no BN / activation.
 template <typename T>
 __global__ void k_out_conv(const T* __restrict__ in, const float* __restrict__ w, float bias, float* __restrict__ out,
@@ -769,6 +862,21 @@ int launch_video_prep(const float* video, const float* mean, const float* stdv, 
 int launch_audio_prep(const float* audio, void* out, int64_t npix, int dtype, hipStream_t s) {
     if (dtype == 1) hipLaunchKernelGGL(k_audio_prep<bf16_t>, dim3(grid_for(npix, 256)), dim3(256), 0, s, audio, (bf16_t*)out, npix);
     else hipLaunchKernelGGL(k_audio_prep<float>, dim3(grid_for(npix, 256)), dim3(256), 0, s, audio, (float*)out, npix);
+    AVSE_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int launch_aconv1_split(const float* in, const float* w, const float* scale, const float* shift, void* out, int64_t N,
+                        int H, int W, int Ho, int Wo, int KH, int KW, int S, int pt, int pl, int Co, unsigned* range_flag,
+                        unsigned range_bit, unsigned range_in_bit, hipStream_t s) {
+    if (Co != A1_CO || KH != A1_K || KW != A1_K || !w || N <= 0 || N * Ho * Wo >= (1LL << 31)) {
+        set_error("a_conv1 split kernel: unexpected layer shape");
+        return 3;
+    }
+    AConv1Args a{in, w, scale, shift, (unsigned short*)out, (long long)N, H, W, Ho, Wo, KH, KW, S, pt, pl,
+                 range_flag, range_bit, range_in_bit};
+    const long long npix = N * Ho * Wo;
+    hipLaunchKernelGGL(k_aconv1_split, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, s, a);
     AVSE_HIP_CHECK(hipGetLastError());
     return 0;
 }

@@ -306,3 +306,32 @@ def test_split_gemm_matches_kconv_and_oracle(gpu, N):
     ae = abs_rms(got[clips], ref)
     print(f"N={N}: output abs RMS {ae:.3e}, k_gemm vs k_conv rel {rel_rms(got, got_k):.2e}")
     assert np.isfinite(got).all() and ae <= FP32_ABS and rel_rms(got, got_k) <= 1e-6
+
+
+@pytest.mark.parametrize("N,T", [(1, 20), (37, 20), (512, 20), (5, 24)])
+def test_split_valu_aconv1_matches_kconv_and_oracle(gpu, N, T):
+    """conv.hip k_aconv1_split (a_conv1 of the split dtype on the vector ALUs, fp32 FMAs straight from the audio input)
+    against the split k_conv after audio_prep (option no_a1valu) and the float64 oracle: a_conv1's output and the
+    forward's; T = 24 is the 29.97 fps geometry (Wo = 12)."""
+    from avse_amd import _lib, ops
+    from avse_amd.model import KerasModel
+    model = db_scale(KerasModel.init(seed=71, randomize=True, audio_shape=(80, T)))
+    rng = np.random.default_rng(171)
+    mel = rng.normal(-40, 15, (N, 80, T)).astype(np.float32)
+    names = ["a_conv1", "a_conv2"] if T == 20 else []   # (the scratch reader knows the 25 fps shapes)
+    clips = spread_clips(N, k=6)
+    dw = ops.DeviceWeights(model, SPLIT)
+    got = ops.forward(dw, ops.to_device(mel), None, checked=True).cpu().numpy()
+    assert dw.last_range_bits == 0
+    sc = scratch(dw, N, clips, names)
+    with _lib.context().options(no_a1valu=1):
+        got_k = ops.forward(dw, ops.to_device(mel), None).cpu().numpy()
+        sck = scratch(dw, N, clips, names)
+    inter = {}
+    ref = K.forward(model.layer_dict(), mel[clips], None, intermediates=inter)
+    for k in names:
+        print(f"{k}: VALU vs oracle {rel_rms(sc[k], inter[k]):.2e}, vs k_conv {rel_rms(sc[k], sck[k]):.2e}")
+        assert rel_rms(sc[k], inter[k]) <= FP32_REL and rel_rms(sc[k], sck[k]) <= 1e-6, k
+    ae = abs_rms(got[clips], ref)
+    print(f"N={N} T={T}: output abs RMS {ae:.3e}, VALU vs k_conv rel {rel_rms(got, got_k):.2e}")
+    assert np.isfinite(got).all() and ae <= FP32_ABS and rel_rms(got, got_k) <= 1e-6
