@@ -132,7 +132,8 @@ def test_split_zero_video(gpu):
 @pytest.mark.parametrize("T,F", [(24, 5), (24, 6)])
 def test_split_other_frame_rates(gpu, T, F):
     """29.97 fps (T = 24, 5 frames) and 30 fps (T = 24, 6 frames) networks in the split dtype: the video encoder runs
-    the split row-run v_conv1 (k_conv_v1s<8, 5> / <8, 6>, conv_v1r.hip) and the split stream kernels at both rates;
+    the split v_conv1 (k_conv_v1p at 5 frames, the row-run k_conv_v1s<8, 6> at 6; conv_v1r.hip) and the split stream
+    kernels at both rates;
     the T = 24 audio / decoder layers run the generic split k_conv."""
     from avse_amd import ops
     from avse_amd.model import KerasModel
