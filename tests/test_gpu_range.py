@@ -114,7 +114,7 @@ def test_zero_video_embedding_overflow_reported_every_call(gpu):
 
 
 @pytest.mark.parametrize("layer,nxt", [("v_conv3", "v_conv4"), ("a_conv2", "a_conv3"), ("d_deconv3", "d_deconv4"),
-                                       ("enc_dense", "dec_dense1")])
+                                       ("enc_dense", "dec_dense1"), ("a_conv1", "a_conv2"), ("v_conv1", "v_conv2")])
 def test_tiny_activations_keep_fp32_accuracy(gpu, layer, nxt):
     """layer's activations x 2^-14 (BN gamma / beta scaled, nxt's kernel compensating): without exponents its pairs' lo
     pieces (and some hi pieces) are f16 subnormals; with them the layer stores x 2^16 and the forward is as accurate as
@@ -143,7 +143,8 @@ def test_tiny_activations_keep_fp32_accuracy(gpu, layer, nxt):
 
 
 @pytest.mark.parametrize("layer,nxt", [("v_conv2", "v_conv3"), ("dec_dense1", "dec_dense2"), ("d_deconv2", "d_deconv3"),
-                                       ("d_deconv4", "d_deconv5")])
+                                       ("d_deconv4", "d_deconv5"), ("a_conv1", "a_conv2"), ("v_conv1", "v_conv2"),
+                                       ("enc_dense", "dec_dense1")])
 def test_huge_activations_keep_headroom(gpu, layer, nxt):
     """layer's activations x 2^14 (~1e5 .. 1e6): with exponents the layer stores x 2^-14 .. and no pair overflows; without
     them the range guard fires and the batch is recomputed on the exact-fp32 kernels."""
