@@ -93,6 +93,11 @@ void avse_ctx_destroy(avse_ctx* ctx);
  *   no_act_scale (AVSE_NO_ACT_SCALE) AVSE_F32_SPLIT weights loaded afterwards keep every activation exponent 0
  *   no_win (AVSE_NO_WIN)             AVSE_F32_SPLIT stride-1 gather layers (decoder phases, a_conv2) on the generic
  *                                    k_conv instead of the windowed kernel
+ *   no_v1p (AVSE_NO_V1P)             AVSE_F32_SPLIT 5-frame v_conv1 on k_conv_v1s (K 160) instead of k_conv_v1p
+ *                                    (K 128; applies to weights loaded afterwards)
+ *   no_a1valu (AVSE_NO_A1VALU)       AVSE_F32_SPLIT a_conv1 on audio_prep + k_conv instead of k_aconv1_split
+ *   side_prio (AVSE_SIDE_PRIO)       audio side stream priority: 0 default, 1 least, 2 greatest (set before the
+ *                                    context's first concurrent forward)
  * Unknown names return AVSE_ERR_INVALID. */
 int avse_ctx_set_option(avse_ctx* ctx, const char* name, int value);
 int avse_ctx_get_option(avse_ctx* ctx, const char* name, int* value);
